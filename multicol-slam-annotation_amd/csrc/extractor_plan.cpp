@@ -1,0 +1,186 @@
+// Host-side plan construction for the extractor (geometry only, no pixel work).
+#include "extractor_plan.hpp"
+#include "common.hpp"
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+
+namespace mcs {
+
+namespace {
+
+int16_t sat_s16_from_float(float v) {
+  int i = cv_roundf(v);
+  return (int16_t)std::min(std::max(i, -32768), 32767);
+}
+
+// cv::resize(INTER_LINEAR) coefficient tables for one src->dst level
+// (OpenCV resize() + resizeGeneric_ table setup).
+void linear_tables(int sw, int sh, int dw, int dh, Plan& pl) {
+  const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+  for (int dx = 0; dx < dw; dx++) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floorf(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= sw && sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    pl.xofs.push_back(sx);
+    pl.alpha.push_back(sat_s16_from_float((1.f - fx) * 2048));
+    pl.alpha.push_back(sat_s16_from_float(fx * 2048));
+  }
+  for (int dy = 0; dy < dh; dy++) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cv_floorf(fy);
+    fy -= sy;
+    pl.yofs.push_back(sy);  // rows are clipped at use (resizeGeneric_ clip(sy, 0, h))
+    pl.beta.push_back(sat_s16_from_float((1.f - fy) * 2048));
+    pl.beta.push_back(sat_s16_from_float(fy * 2048));
+  }
+}
+
+}  // namespace
+
+int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
+  if (W <= 0 || H <= 0 || p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 ||
+      !(p.scale_factor > 1.0f)) {
+    set_error("invalid extractor parameters");
+    return MCS_ERR_ARG;
+  }
+  if (p.desc_size != 16 && p.desc_size != 32 && p.desc_size != 64) {
+    set_error("desc_size must be 16, 32 or 64 (src/cTracking.cpp:133)");
+    return MCS_ERR_ARG;
+  }
+  if (p.use_agast || p.fast_agast_type != 2) {
+    set_error("only FAST TYPE_9_16 (fastAgastType 2, useAgast 0) is implemented");
+    return MCS_ERR_UNSUPPORTED;
+  }
+  if (p.do_dbrief || p.learn_masks) {
+    set_error("dBRIEF / mdBRIEF descriptors are not implemented yet (ORB only)");
+    return MCS_ERR_UNSUPPORTED;
+  }
+  pl.p = p;
+  pl.W = W; pl.H = H; pl.nlevels = p.nlevels;
+  pl.scale_factor = (double)p.scale_factor;
+
+  // scale tables (ctor :153-162) and budgets (:167-179)
+  double sf[kMaxLevels], isf[kMaxLevels];
+  sf[0] = 1; isf[0] = 1;
+  for (int i = 1; i < p.nlevels; i++) sf[i] = sf[i - 1] * pl.scale_factor;
+  const double inv = 1.0 / pl.scale_factor;
+  for (int i = 1; i < p.nlevels; i++) isf[i] = isf[i - 1] * inv;
+  int nfl[kMaxLevels];
+  {
+    const double factor = 1.0 / pl.scale_factor;
+    double nd = p.nfeatures * (1 - factor) / (1 - std::pow(factor, p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; l++) { nfl[l] = cv_round(nd); sum += nfl[l]; nd *= factor; }
+    nfl[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+  }
+
+  int64_t pyr_off = 0, img_off = 0;
+  int32_t slot = 0, sel = 0;
+  pl.cells.clear(); pl.xofs.clear(); pl.yofs.clear(); pl.alpha.clear(); pl.beta.clear();
+  pl.xtab_off.assign(p.nlevels, 0); pl.ytab_off.assign(p.nlevels, 0);
+  pl.max_cells_level = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelPlan& L = pl.lv[l];
+    L.w = cv_round((double)W * isf[l]);
+    L.h = cv_round((double)H * isf[l]);
+    if (L.w > 4095 + 2 * kMinBorder || L.h > 4095 + 2 * kMinBorder) {
+      set_error("level too large for 12-bit candidate packing");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    L.pyr_off = (l == 0) ? 0 : pyr_off;
+    if (l > 0) pyr_off += (int64_t)L.w * L.h;
+    L.img_off = img_off;
+    img_off += (int64_t)L.w * L.h;
+    L.nfeat = nfl[l];
+    L.scale = (float)sf[l];
+    L.patch_size_scaled = (int)(kPatchSize * sf[l]);
+
+    if (l > 0) {
+      const LevelPlan& S = pl.lv[l - 1];
+      pl.xtab_off[l] = (int64_t)pl.xofs.size();
+      pl.ytab_off[l] = (int64_t)pl.yofs.size();
+      linear_tables(S.w, S.h, L.w, L.h, pl);
+      // OpenCV 3.1 VResizeLinearVec_32s8u: 16-wide SSE2 loop (x <= w-16), then 4-wide
+      // (x < w-4); the rest uses the scalar FixedPtCast form.
+      int x = 0;
+      for (; x <= L.w - 16; x += 16) {}
+      for (; x < L.w - 4; x += 4) {}
+      L.simd_end = x;
+    } else {
+      L.simd_end = 0;
+    }
+
+    // FAST cell grid (:876-948)
+    const int maxBX = L.w - kEdgeThreshold + 3, maxBY = L.h - kEdgeThreshold + 3;
+    const double width = maxBX - kMinBorder, height = maxBY - kMinBorder;
+    const int nCols = (int)(width / 30.0), nRows = (int)(height / 30.0);
+    if (nCols < 1 || nRows < 1) {
+      set_error("pyramid level smaller than one 30px FAST cell (reference divides by zero)");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+    if (wCell > kMaxCellDim || hCell > kMaxCellDim) {
+      set_error("FAST cell larger than the kernel's 64px window bound");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    L.cell_begin = (int32_t)pl.cells.size();
+    L.cand_off = slot;
+    for (int i = 0; i < nRows; i++) {
+      const double iniY = kMinBorder + i * hCell;
+      double maxY = iniY + hCell + 6;
+      if (iniY >= maxBY - 3) continue;
+      if (maxY > maxBY) maxY = maxBY;
+      for (int j = 0; j < nCols; j++) {
+        const double iniX = kMinBorder + j * wCell;
+        double maxX = iniX + wCell + 6;
+        if (iniX >= maxBX - 6) continue;
+        if (maxX > maxBX) maxX = maxBX;
+        CellDesc c;
+        c.level = l;
+        c.wx0 = (int16_t)((int)iniX + 3); c.wx1 = (int16_t)((int)maxX - 3);
+        c.wy0 = (int16_t)((int)iniY + 3); c.wy1 = (int16_t)((int)maxY - 3);
+        const int ww = std::max(0, c.wx1 - c.wx0), wh = std::max(0, c.wy1 - c.wy0);
+        c.slot_off = slot;
+        c.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
+        slot += c.slot_cap;
+        pl.cells.push_back(c);
+      }
+    }
+    L.cell_end = (int32_t)pl.cells.size();
+    L.cand_cap = slot - L.cand_off;
+    pl.max_cells_level = std::max(pl.max_cells_level, L.cell_end - L.cell_begin);
+    if (L.cell_end - L.cell_begin > kMaxCellsPerLevel) {
+      set_error("too many FAST cells in one level");
+      return MCS_ERR_UNSUPPORTED;
+    }
+
+    // octree domain (:954-957 -> :641-643)
+    L.width_rel = maxBX - kMinBorder;
+    L.height_rel = maxBY - kMinBorder;
+    L.nini = cv_round((double)L.width_rel / L.height_rel);
+    if (L.nini < 1) {
+      set_error("octree nIni == 0 (level taller than 2x its width): reference indexes out of range");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    L.hx = (double)L.width_rel / L.nini;
+    const int cap = std::max(L.nfeat + 3, 4 * L.nini);
+    if (cap > kOctMaxL) {
+      set_error("per-level feature budget exceeds the octree kernel's node bound (1024)");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    L.sel_off = sel;
+    L.sel_cap = cap;
+    sel += cap;
+  }
+  pl.pyr_frame_bytes = pyr_off;
+  pl.img_frame_bytes = img_off;
+  pl.slots_per_frame = slot;
+  pl.cand_per_frame = slot;
+  pl.sel_per_frame = sel;
+  return MCS_OK;
+}
+
+}  // namespace mcs

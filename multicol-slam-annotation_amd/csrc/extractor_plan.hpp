@@ -1,0 +1,67 @@
+// Extractor plan: all per-configuration geometry computed once on the host at
+// mcs_extractor_create() (the reference recomputes it every call inside
+// ComputePyramid / ComputeKeyPointsOctTree, src/mdBRIEFextractorOct.cpp:1158-1201,
+// 863-971).  Plain structs so they can be passed to kernels by value.
+#pragma once
+#include <cstdint>
+#include <vector>
+#include "../../include/mcs_extractor.h"
+
+namespace mcs {
+
+constexpr int kMaxLevels = 12;
+constexpr int kEdgeThreshold = 25;             // src/mdBRIEFextractorOct.cpp:86
+constexpr int kMinBorder = kEdgeThreshold - 3; // :876
+constexpr int kPatchSize = 32;                 // :84
+constexpr int kHalfPatch = 16;                 // :85
+constexpr int kMaxCellDim = 64;                // window bound per FAST cell (host-checked)
+constexpr int kMaxCellsPerLevel = 4096;        // LDS prefix table in the octree kernel
+constexpr int kOctMaxL = 1024;                 // octree node-list bound (host-checked)
+
+// One FAST cell of ComputeKeyPointsOctTree (:892-948): the detection window is the
+// cell ROI shrunk by 3 px (FAST_t rows/cols [3, n-3)), absolute level coordinates.
+struct CellDesc {
+  int32_t level;
+  int16_t wx0, wy0, wx1, wy1;  // window [wx0,wx1) x [wy0,wy1)
+  int32_t slot_off;            // first candidate slot of this cell within a frame
+  int32_t slot_cap;            // ceil(ww/2)*ceil(wh/2): max survivors of strict 8-NMS
+};
+
+struct LevelPlan {
+  int32_t w, h;               // level size (cvRound(W / 1.2^l))
+  int64_t pyr_off;            // offset of the level inside a frame's pyramid workspace (l >= 1)
+  int64_t img_off;            // offset inside a frame's blurred / mask-pyramid workspace
+  int32_t cell_begin, cell_end;
+  int32_t cand_off, cand_cap; // candidate gather area within a frame (sum of cell caps)
+  int32_t sel_off, sel_cap;   // octree output area within a frame
+  int32_t nfeat;              // mnFeaturesPerLevel[l] (:167-179)
+  int32_t nini;               // cvRound((maxX-minX)/(maxY-minY)) (:641)
+  double hx;                  // (maxX-minX)/nIni (:643)
+  int32_t width_rel, height_rel;  // maxX-minX, maxY-minY of the octree domain
+  int32_t simd_end;           // first dx computed by the scalar vertical resize form
+  int32_t patch_size_scaled;  // (int)(PATCH_SIZE * scaleFactor^l)  (:959)
+  float scale;                // (float)mvScaleFactor[l]  (:1305)
+};
+
+struct Plan {
+  mcs_extractor_params p;
+  int32_t W = 0, H = 0, nlevels = 0;
+  double scale_factor = 1.2;  // double((float)p.scale_factor)  (:147)
+  LevelPlan lv[kMaxLevels];
+  std::vector<CellDesc> cells;
+  int64_t pyr_frame_bytes = 0;   // levels 1..L-1
+  int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred / mask pyramids)
+  int32_t slots_per_frame = 0;   // sum of cell caps
+  int32_t cand_per_frame = 0;    // == slots_per_frame
+  int32_t sel_per_frame = 0;     // sum of level sel caps == mcs_extractor_capacity
+  int32_t max_cells_level = 0;
+  // resize tables (concatenated over levels 1..L-1)
+  std::vector<int32_t> xofs, yofs;
+  std::vector<int16_t> alpha, beta;
+  std::vector<int64_t> xtab_off, ytab_off;  // per level offsets into the tables
+};
+
+// Returns MCS_OK or an error (unsupported geometry / parameters).
+int build_plan(const mcs_extractor_params& p, int W, int H, Plan& plan);
+
+}  // namespace mcs

@@ -1,0 +1,351 @@
+// Hamming matching on gfx950: XOR + v_bcnt_u32_b32 popcount-accumulate, trains staged in
+// LDS and broadcast to a wave of 64 queries (one query per lane, descriptor in VGPRs).
+//
+// Reference: DescriptorDistance64 / ...Masked   src/cORBmatcher.cpp:2443-2477
+//            SearchForTriangulationRaw          src/cORBmatcher.cpp:968-1156
+//            best/second-best scans             src/cORBmatcher.cpp:67-163, 326-475
+#include "common.hpp"
+#include "../../include/mcs_matcher.h"
+#include <algorithm>
+#include <vector>
+
+namespace mcs {
+
+constexpr int kHamThreads = 256;
+constexpr int kHamTile = 256;      // train rows per LDS tile
+
+template <int W>
+__device__ __forceinline__ int ham_dist_v(const uint32_t (&q)[W], const uint4* t4) {
+  int d = 0;
+#pragma unroll
+  for (int w4 = 0; w4 < W / 4; w4++) {
+    const uint4 v = t4[w4];
+    d += __popc(q[4 * w4 + 0] ^ v.x);
+    d += __popc(q[4 * w4 + 1] ^ v.y);
+    d += __popc(q[4 * w4 + 2] ^ v.z);
+    d += __popc(q[4 * w4 + 3] ^ v.w);
+  }
+  return d;
+}
+
+// Top-2 over one (query set, train set) pair; blockIdx.x = query tile, blockIdx.y = pair.
+template <int W>
+__global__ __launch_bounds__(kHamThreads) void k_top2(
+    const uint8_t* __restrict__ qbase, const uint8_t* __restrict__ tbase,
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ pairs, int64_t set_stride,
+    int nq_fixed, int nt_fixed, int cap_out, int32_t* __restrict__ best_idx,
+    int32_t* __restrict__ best_dist, int32_t* __restrict__ second_idx,
+    int32_t* __restrict__ second_dist) {
+  __shared__ uint4 tile[kHamTile * (W / 4)];
+  const int p = blockIdx.y;
+  const uint8_t* Q;
+  const uint8_t* T;
+  int nq, nt;
+  if (pairs) {
+    const int qs = pairs[2 * p], ts = pairs[2 * p + 1];
+    Q = qbase + (int64_t)qs * set_stride;
+    T = tbase + (int64_t)ts * set_stride;
+    nq = counts[qs];
+    nt = counts[ts];
+  } else {
+    Q = qbase; T = tbase; nq = nq_fixed; nt = nt_fixed;
+  }
+  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
+  if (blockIdx.x * kHamThreads >= nq) return;  // uniform per block
+  uint32_t q[W];
+  if (qi < nq) {
+    const uint4* qp = reinterpret_cast<const uint4*>(Q + (int64_t)qi * W * 4);
+#pragma unroll
+    for (int w4 = 0; w4 < W / 4; w4++) {
+      const uint4 v = qp[w4];
+      q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; w++) q[w] = 0;
+  }
+  int b1 = 0x7FFFFFFF, b2 = 0x7FFFFFFF, i1 = -1, i2 = -1;
+  for (int t0 = 0; t0 < nt; t0 += kHamTile) {
+    const int nt_tile = min(kHamTile, nt - t0);
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(T + (int64_t)t0 * W * 4);
+    for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
+    __syncthreads();
+    for (int j = 0; j < nt_tile; j++) {
+      const int d = ham_dist_v<W>(q, &tile[j * (W / 4)]);
+      const int idx = t0 + j;
+      if (d < b1) { b2 = b1; i2 = i1; b1 = d; i1 = idx; }
+      else if (d < b2) { b2 = d; i2 = idx; }
+    }
+  }
+  if (qi < nq) {
+    const int64_t o = (int64_t)p * cap_out + qi;
+    const int none = 8 * 4 * W + 1;
+    best_idx[o] = i1;
+    best_dist[o] = i1 < 0 ? none : b1;
+    second_idx[o] = i2;
+    second_dist[o] = i2 < 0 ? none : b2;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(kHamThreads) void k_dense(const uint8_t* __restrict__ A, int na,
+                                                       const uint8_t* __restrict__ B, int nb,
+                                                       uint16_t* __restrict__ D) {
+  __shared__ uint4 tile[kHamTile * (W / 4)];
+  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
+  const int t0 = blockIdx.y * kHamTile;
+  const int nt_tile = min(kHamTile, nb - t0);
+  const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
+  for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
+  __syncthreads();
+  if (qi >= na) return;
+  uint32_t q[W];
+  const uint4* qp = reinterpret_cast<const uint4*>(A + (int64_t)qi * W * 4);
+#pragma unroll
+  for (int w4 = 0; w4 < W / 4; w4++) {
+    const uint4 v = qp[w4];
+    q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
+  }
+  for (int j = 0; j < nt_tile; j++) D[(int64_t)qi * nb + t0 + j] = (uint16_t)ham_dist_v<W>(q, &tile[j * (W / 4)]);
+}
+
+// radius search for SearchForTriangulationRaw: candidates with dist <= th among trains of
+// the same camera without a map point.  pass 0 counts, pass 1 writes (dist<<20 | idx2).
+template <int W>
+__global__ __launch_bounds__(kHamThreads) void k_radius(
+    const uint8_t* __restrict__ A, const int32_t* __restrict__ camA,
+    const uint8_t* __restrict__ hasA, int na, const uint8_t* __restrict__ B,
+    const int32_t* __restrict__ camB, const uint8_t* __restrict__ hasB, int nb, int th,
+    int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
+    uint32_t* __restrict__ out) {
+  __shared__ uint4 tile[kHamTile * (W / 4)];
+  __shared__ int tcam[kHamTile];
+  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
+  uint32_t q[W];
+  int qc = -1;
+  bool active = qi < na && !hasA[qi];
+  if (qi < na) {
+    qc = camA[qi];
+    const uint4* qp = reinterpret_cast<const uint4*>(A + (int64_t)qi * W * 4);
+#pragma unroll
+    for (int w4 = 0; w4 < W / 4; w4++) {
+      const uint4 v = qp[w4];
+      q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; w++) q[w] = 0;
+  }
+  int cnt = 0;
+  int pos = (offsets && qi < na) ? offsets[qi] : 0;
+  for (int t0 = 0; t0 < nb; t0 += kHamTile) {
+    const int nt_tile = min(kHamTile, nb - t0);
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
+    for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
+    for (int i = threadIdx.x; i < nt_tile; i += kHamThreads)
+      tcam[i] = hasB[t0 + i] ? -2 : camB[t0 + i];
+    __syncthreads();
+    if (!active) continue;
+    for (int j = 0; j < nt_tile; j++) {
+      if (tcam[j] != qc) continue;
+      const int d = ham_dist_v<W>(q, &tile[j * (W / 4)]);
+      if (d <= th) {
+        if (out) out[pos++] = ((uint32_t)d << 20) | (uint32_t)(t0 + j);
+        cnt++;
+      }
+    }
+  }
+  if (!out && qi < na) counts[qi] = active ? cnt : 0;
+}
+
+static int check_bytes(int bytes) {
+  if (bytes != 16 && bytes != 32 && bytes != 64) {
+    set_error("descriptor bytes must be 16, 32 or 64");
+    return MCS_ERR_ARG;
+  }
+  return MCS_OK;
+}
+
+#define MCS_DISPATCH_W(bytes, KERNEL, ...)                                                  \
+  do {                                                                                     \
+    if ((bytes) == 16) hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__);                         \
+    else if ((bytes) == 32) hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__);                    \
+    else hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__);                                      \
+  } while (0)
+
+}  // namespace mcs
+
+using namespace mcs;
+
+extern "C" {
+
+int mcs_descriptor_distance64(const uint64_t* d1, const uint64_t* d2, int32_t dim) {
+  uint64_t dist = 0;
+  for (int d = 0; d < dim / 8; ++d) dist += (uint64_t)__builtin_popcountll(d1[d] ^ d2[d]);
+  return (int)dist;
+}
+
+int mcs_descriptor_distance64_masked(const uint64_t* d1, const uint64_t* d2, const uint64_t* m1,
+                                     const uint64_t* m2, int32_t dim) {
+  uint64_t dist = 0;
+  for (int i = 0; i < dim / 8; ++i) {
+    const uint64_t x = d1[i] ^ d2[i];
+    dist += (uint64_t)__builtin_popcountll(x & m1[i]) + (uint64_t)__builtin_popcountll(x & m2[i]);
+  }
+  return (int)(dist / 2);
+}
+
+int mcs_hamming_dense_device(const uint8_t* d_a, int32_t na, const uint8_t* d_b, int32_t nb,
+                             int32_t bytes, uint16_t* d_dist, void* stream) {
+  int rc = check_bytes(bytes);
+  if (rc) return rc;
+  if (na <= 0 || nb <= 0) return MCS_OK;
+  dim3 g((na + kHamThreads - 1) / kHamThreads, (nb + kHamTile - 1) / kHamTile);
+  MCS_DISPATCH_W(bytes, k_dense, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_a, na, d_b, nb,
+                 d_dist);
+  MCS_HIP_CHECK(hipGetLastError());
+  return MCS_OK;
+}
+
+int mcs_hamming_top2_device(const uint8_t* d_q, int32_t nq, const uint8_t* d_t, int32_t nt,
+                            int32_t bytes, int32_t* d_best_idx, int32_t* d_best_dist,
+                            int32_t* d_second_idx, int32_t* d_second_dist, void* stream) {
+  int rc = check_bytes(bytes);
+  if (rc) return rc;
+  if (nq <= 0) return MCS_OK;
+  dim3 g((nq + kHamThreads - 1) / kHamThreads, 1);
+  MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_q, d_t,
+                 (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, nq, nt, nq,
+                 d_best_idx, d_best_dist, d_second_idx, d_second_dist);
+  MCS_HIP_CHECK(hipGetLastError());
+  return MCS_OK;
+}
+
+int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts,
+                                  const int32_t* d_pairs, int32_t n_pairs, int32_t cap,
+                                  int32_t bytes, int32_t* d_best_idx, int32_t* d_best_dist,
+                                  int32_t* d_second_idx, int32_t* d_second_dist, void* stream) {
+  int rc = check_bytes(bytes);
+  if (rc) return rc;
+  if (n_pairs <= 0) return MCS_OK;
+  if (!d_desc || !d_counts || !d_pairs || cap <= 0) return MCS_ERR_ARG;
+  dim3 g((cap + kHamThreads - 1) / kHamThreads, n_pairs);
+  MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_desc, d_desc,
+                 d_counts, d_pairs, (int64_t)cap * bytes, 0, 0, cap, d_best_idx, d_best_dist,
+                 d_second_idx, d_second_dist);
+  MCS_HIP_CHECK(hipGetLastError());
+  return MCS_OK;
+}
+
+int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
+                                     const uint8_t* has_mp1, const double* rays1, int32_t n1,
+                                     const uint8_t* desc2, const int32_t* cam2,
+                                     const uint8_t* has_mp2, const double* rays2, int32_t n2,
+                                     int32_t ncams, const double* E, int32_t bytes,
+                                     int32_t th_low, double epi_thresh, int32_t* matches12,
+                                     int32_t* n_matches) {
+  int rc = check_bytes(bytes);
+  if (rc) return rc;
+  if (!n_matches || (n1 > 0 && !matches12)) return MCS_ERR_ARG;
+  *n_matches = 0;
+  for (int i = 0; i < n1; i++) matches12[i] = -1;
+  if (n1 <= 0 || n2 <= 0) return MCS_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device visible (no CPU fallback)");
+    return MCS_ERR_NO_DEVICE;
+  }
+  // ---- GPU: per-query candidate lists (same camera, no map point, dist <= th_low)
+  uint8_t *dA = nullptr, *dB = nullptr, *dhA = nullptr, *dhB = nullptr;
+  int32_t *dcA = nullptr, *dcB = nullptr, *dcnt = nullptr, *doff = nullptr;
+  uint32_t* dout = nullptr;
+  std::vector<int32_t> cnt(n1), off(n1 + 1, 0);
+  std::vector<uint32_t> cand;
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
+  chk(hipMalloc((void**)&dA, (size_t)n1 * bytes));
+  chk(hipMalloc((void**)&dB, (size_t)n2 * bytes));
+  chk(hipMalloc((void**)&dhA, n1));
+  chk(hipMalloc((void**)&dhB, n2));
+  chk(hipMalloc((void**)&dcA, 4 * (size_t)n1));
+  chk(hipMalloc((void**)&dcB, 4 * (size_t)n2));
+  chk(hipMalloc((void**)&dcnt, 4 * (size_t)n1));
+  chk(hipMalloc((void**)&doff, 4 * (size_t)n1));
+  chk(hipMemcpy(dA, desc1, (size_t)n1 * bytes, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dB, desc2, (size_t)n2 * bytes, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dhA, has_mp1, n1, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dhB, has_mp2, n2, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dcA, cam1, 4 * (size_t)n1, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dcB, cam2, 4 * (size_t)n2, hipMemcpyHostToDevice));
+  dim3 g((n1 + kHamThreads - 1) / kHamThreads);
+  if (e == hipSuccess) {
+    MCS_DISPATCH_W(bytes, k_radius, g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dcA, dhA, n1, dB,
+                   dcB, dhB, n2, th_low, dcnt, (const int32_t*)nullptr, (uint32_t*)nullptr);
+    chk(hipGetLastError());
+    chk(hipMemcpy(cnt.data(), dcnt, 4 * (size_t)n1, hipMemcpyDeviceToHost));
+  }
+  if (e == hipSuccess) {
+    for (int i = 0; i < n1; i++) off[i + 1] = off[i] + cnt[i];
+    cand.resize(std::max(1, off[n1]));
+    chk(hipMalloc((void**)&dout, 4 * cand.size()));
+    chk(hipMemcpy(doff, off.data(), 4 * (size_t)n1, hipMemcpyHostToDevice));
+    if (e == hipSuccess) {
+      MCS_DISPATCH_W(bytes, k_radius, g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dcA, dhA, n1,
+                     dB, dcB, dhB, n2, th_low, dcnt, (const int32_t*)doff, dout);
+      chk(hipGetLastError());
+      chk(hipMemcpy(cand.data(), dout, 4 * (size_t)off[n1], hipMemcpyDeviceToHost));
+    }
+  }
+  void* bufs[] = {dA, dB, dhA, dhB, dcA, dcB, dcnt, doff, dout};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) { set_hip_error(e, "triangulation radius search", __FILE__, __LINE__); return MCS_ERR_HIP; }
+
+  // ---- host: the order-dependent greedy of :1016-1089 (vbMatched2 state)
+  std::vector<uint8_t> matched2(n2, 0);
+  int nm = 0;
+  for (int i1 = 0; i1 < n1; i1++) {
+    if (has_mp1[i1]) continue;
+    uint32_t* c = cand.data() + off[i1];
+    const int nc = off[i1 + 1] - off[i1];
+    if (nc == 0) continue;
+    std::sort(c, c + nc);  // (dist, idx2) ascending == sort(vDistIndex)
+    int best = -1;
+    for (int k = 0; k < nc; k++)
+      if (!matched2[c[k] & 0xFFFFF]) { best = (int)(c[k] >> 20); break; }
+    if (best < 0) continue;
+    const int th = (int)std::lrint(2.0 * best);
+    const int c1 = cam1[i1];
+    const double* r1 = rays1 + 3 * (size_t)i1;
+    for (int k = 0; k < nc; k++) {
+      const int d = (int)(c[k] >> 20), i2 = (int)(c[k] & 0xFFFFF);
+      if (matched2[i2]) continue;
+      if (d > th) break;
+      const int c2 = cam2[i2];
+      const double* Em = E + 9 * ((size_t)c1 * ncams + c2);
+      const double* r2 = rays2 + 3 * (size_t)i2;
+      // CheckDistEpipolarLine (src/misc.cpp:54-70)
+      double Ex1[3], Etx2[3];
+      for (int r = 0; r < 3; r++) {
+        Ex1[r] = Em[3 * r] * r1[0] + Em[3 * r + 1] * r1[1] + Em[3 * r + 2] * r1[2];
+        Etx2[r] = Em[r] * r2[0] + Em[3 + r] * r2[1] + Em[6 + r] * r2[2];
+      }
+      const double nom = r2[0] * Ex1[0] + r2[1] * Ex1[1] + r2[2] * Ex1[2];
+      const double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
+                         Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
+      if (den == 0.0) continue;
+      if ((nom * nom) / den < epi_thresh) {
+        matched2[i2] = 1;
+        matches12[i1] = i2;
+        nm++;
+        break;
+      }
+    }
+  }
+  *n_matches = nm;
+  return MCS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,205 @@
+"""mcs_amd -- Python host binding of libmcs_amd.so (MI355X-native MultiCol-SLAM front-end
+and local bundle adjustment).
+
+The product is the C-ABI library (include/*.h); this module is a thin ctypes mirror of the
+reference operator surface used by tests and bench.py:
+
+  Extractor(params, w, h)       ~ mdBRIEFextractorOct(nfeatures, scaleFactor, ...)
+                                   (reference include/mdBRIEFextractorOct.h:339-351)
+  Extractor.extract(img, mask)  ~ mdBRIEFextractorOct::operator()(image, mask, kps, cam,
+                                   desc, descMasks)  (src/mdBRIEFextractorOct.cpp:1244-1337)
+  descriptor_distance64(a, b)   ~ DescriptorDistance64 (src/cORBmatcher.cpp:2443-2455)
+
+There is no CPU fallback: if the shared library is missing or no GPU is visible the calls
+raise, so a GPU test can never pass on a silent fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmcs_amd.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
+
+MCS_OK = 0
+MCS_ERR_ARG = -1
+MCS_ERR_CAPACITY = -2
+MCS_ERR_HIP = -3
+MCS_ERR_UNSUPPORTED = -4
+MCS_ERR_NO_DEVICE = -5
+
+
+class McsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("mcs error %d: %s" % (code, msg))
+        self.code = code
+
+
+class ExtractorParams(ctypes.Structure):
+    """Mirror of mcs_extractor_params (include/mcs_extractor.h) with reference defaults."""
+    _fields_ = [("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float),
+                ("nlevels", ctypes.c_int32), ("edge_threshold", ctypes.c_int32),
+                ("first_level", ctypes.c_int32), ("score_type", ctypes.c_int32),
+                ("patch_size", ctypes.c_int32), ("fast_threshold", ctypes.c_int32),
+                ("use_agast", ctypes.c_int32), ("fast_agast_type", ctypes.c_int32),
+                ("do_dbrief", ctypes.c_int32), ("learn_masks", ctypes.c_int32),
+                ("desc_size", ctypes.c_int32)]
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, edge_threshold=25,
+                 first_level=0, score_type=0, patch_size=32, fast_threshold=20,
+                 use_agast=0, fast_agast_type=2, do_dbrief=0, learn_masks=0, desc_size=32):
+        super().__init__(nfeatures, scale_factor, nlevels, edge_threshold, first_level,
+                         score_type, patch_size, fast_threshold, use_agast, fast_agast_type,
+                         do_dbrief, learn_masks, desc_size)
+
+
+# numpy view of mcs_keypoint / cv::KeyPoint
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+
+# name -> (restype, argtypes); every symbol declared in include/*.h must be here
+SIGNATURES = {
+    "mcs_version": (ctypes.c_char_p, []),
+    "mcs_last_error": (ctypes.c_char_p, []),
+    "mcs_device_count": (_I32, []),
+    "mcs_extractor_default_params": (None, [_P]),
+    "mcs_extractor_create": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P]),
+    "mcs_extractor_destroy": (None, [_P]),
+    "mcs_extractor_capacity": (_I32, [_P]),
+    "mcs_extractor_levels": (ctypes.c_int, [_P, _P, _P, _P]),
+    "mcs_extract": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _P, _I32, _P, _P, _P]),
+    "mcs_extractor_set_masks_device": (ctypes.c_int, [_P, _P, _I32, _P]),
+    "mcs_extract_batch_device": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
+    "mcs_extractor_read_stage": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _I64, _P]),
+    # matcher (include/mcs_matcher.h)
+    "mcs_descriptor_distance64": (ctypes.c_int, [_P, _P, _I32]),
+    "mcs_descriptor_distance64_masked": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
+    "mcs_hamming_top2_device": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "mcs_hamming_dense_device": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
+    "mcs_hamming_top2_batch_device": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmcs_amd.so and bind every exported C-ABI symbol (raises if missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise McsError(MCS_ERR_NO_DEVICE, "libmcs_amd.so not built (run __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7)
+    # and loads it by file name, so if our library were loaded first the process would end
+    # up with two HIP/HSA runtimes and torch could not see the GPU.  Loading torch first
+    # makes our NEEDED libamdhip64.so.7 resolve to torch's copy (device pointers and
+    # streams are then shared).  Without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        if not hasattr(L, name):
+            continue  # symbols of modules not yet built are checked by tests
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != MCS_OK:
+        raise McsError(rc, lib().mcs_last_error().decode(errors="replace"))
+
+
+def device_count():
+    return int(lib().mcs_device_count())
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class Extractor:
+    """Host-side mirror of mdBRIEFextractorOct backed by the HIP pipeline."""
+
+    def __init__(self, params, width, height, max_frames=1, device=0):
+        self.params = params
+        self.width, self.height = int(width), int(height)
+        h = ctypes.c_void_p()
+        _check(lib().mcs_extractor_create(ctypes.byref(params), self.width, self.height,
+                                          int(max_frames), int(device), ctypes.byref(h)))
+        self._h = h
+        self.capacity = int(lib().mcs_extractor_capacity(h))
+        self.desc_size = int(params.desc_size)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mcs_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def levels(self):
+        n = ctypes.c_int32()
+        wh = np.zeros(2 * 12, np.int32)
+        nf = np.zeros(12, np.int32)
+        _check(lib().mcs_extractor_levels(self._h, ctypes.byref(n), _ptr(wh), _ptr(nf)))
+        k = n.value
+        return wh[:2 * k].reshape(k, 2), nf[:k]
+
+    def extract(self, image, mask=None):
+        """operator()(image, mask, kps, camModel, desc, descMasks) -> (kps, desc)."""
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        assert image.shape == (self.height, self.width)
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            assert mask.shape == image.shape
+        kps = np.zeros(self.capacity, KEYPOINT_DTYPE)
+        desc = np.zeros((self.capacity, self.desc_size), np.uint8)
+        n = ctypes.c_int32()
+        _check(lib().mcs_extract(self._h, _ptr(image), self.width, _ptr(mask), self.width,
+                                 _ptr(kps), self.capacity, ctypes.byref(n), _ptr(desc), None))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def set_masks_device(self, d_masks_ptr, n_masks, stream=None):
+        _check(lib().mcs_extractor_set_masks_device(self._h, d_masks_ptr, int(n_masks), stream))
+
+    def extract_batch_device(self, d_images, n_frames, d_mask_index, d_kps, d_counts, d_desc,
+                             stream=None):
+        """Device pointers (ints) in, device pointers out; async on `stream`."""
+        _check(lib().mcs_extract_batch_device(self._h, d_images, int(n_frames), d_mask_index,
+                                              d_kps, d_counts, d_desc, stream))
+
+    def read_stage(self, stage, frame, level):
+        wh, _ = self.levels()
+        w, h = wh[level]
+        if stage in (0, 1):
+            buf = np.zeros(w * h, np.uint8)
+        else:
+            buf = np.zeros(3 * (w * h // 4 + 16), np.int32)
+        n = ctypes.c_int64()
+        _check(lib().mcs_extractor_read_stage(self._h, stage, frame, level, _ptr(buf),
+                                              buf.size, ctypes.byref(n)))
+        if stage in (0, 1):
+            return buf.reshape(h, w)
+        return buf[:3 * n.value].reshape(-1, 3)
+
+
+def descriptor_distance64(a, b, dim=None):
+    """DescriptorDistance64 (src/cORBmatcher.cpp:2443-2455) on two descriptor rows."""
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().mcs_descriptor_distance64(_ptr(a), _ptr(b), int(dim or a.size)))

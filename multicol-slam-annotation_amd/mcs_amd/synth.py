@@ -1,0 +1,172 @@
+"""Deterministic synthetic fisheye frames and masks (no dataset is available offline).
+
+Frames are rendered by casting each pixel's ray through the Scaramuzza omni model of the
+Lafida rig (ImgToWorld, reference src/cam_model_omni.cpp:49-67) into a procedural
+panorama (random rectangles + multi-octave noise + checker patches), then adding
+Gaussian sensor noise (sigma = 2 DN).  Pixels outside the mirror mask are black.  The
+mirror mask follows CreateMirrorMask level 0 (src/cam_model_omni.cpp:183-222): a circle
+centred at (row = v0, col = u0) of radius v0 + 22 (float arithmetic, u0/v0 names swapped
+as in the reference).
+
+Calibration values are the Lafida fixtures (Examples/Lafida/InteriorOrientationFisheye*.yaml,
+MultiCamSys_Calibration.yaml) -- numbers only.
+"""
+import numpy as np
+
+# Examples/Lafida/InteriorOrientationFisheye{0,1,2}.yaml
+LAFIDA_CAMS = [
+    dict(Iw=754, Ih=480, c=0.999626131079017, d=-0.0034775192597376, e=0.00385134991673147,
+         u0=392.219508388648, v0=243.494438476351,
+         a=[-209.200757992065, 0.0, 0.00213741670953883, -4.2203617319086e-06, 1.77146086919594e-08],
+         pol=[293.667187375663, 149.982043337335, -10.448650568161, 28.2295300683376,
+              7.13365723186292, 0.056303218962532, 10.4144677485333, 0.166354960773665,
+              -5.86858687381081, 1.18165998645705, 3.1108311354746, 0.810799620714366]),
+]
+
+
+def load_lafida_cams(ref_dir="/root/reference/Examples/Lafida"):
+    """Parse all three Lafida calibrations (when the reference tree is present)."""
+    import os
+    cams = []
+    for c in range(3):
+        p = os.path.join(ref_dir, "InteriorOrientationFisheye%d.yaml" % c)
+        if not os.path.exists(p):
+            return LAFIDA_CAMS
+        kv = {}
+        for line in open(p):
+            line = line.split("#")[0].strip()
+            if ":" in line and not line.startswith("%"):
+                k, v = line.split(":", 1)
+                try:
+                    kv[k.strip()] = float(v)
+                except ValueError:
+                    pass
+        cams.append(dict(Iw=int(kv["Camera.Iw"]), Ih=int(kv["Camera.Ih"]), c=kv["Camera.c"],
+                         d=kv["Camera.d"], e=kv["Camera.e"], u0=kv["Camera.u0"],
+                         v0=kv["Camera.v0"],
+                         a=[kv.get("Camera.a%d" % i, 0.0) for i in range(5)],
+                         pol=[kv.get("Camera.pol%d" % i, 0.0) for i in range(12)]))
+    return cams
+
+
+def scaled_cam(cam, width, height):
+    """Lafida polynomials scaled to a width x height sensor, centred principal point
+    (config D: 1024x1024)."""
+    s = width / float(cam["Iw"])
+    out = dict(cam)
+    out.update(Iw=width, Ih=height, u0=width / 2.0, v0=height / 2.0)
+    # forward poly f(rho): rho scales by s, z scales by s
+    out["a"] = [a * s ** (1 - i) for i, a in enumerate(cam["a"])]
+    out["pol"] = [p * s for p in cam["pol"]]
+    return out
+
+
+def mirror_mask(cam):
+    """CreateMirrorMask level 0 (src/cam_model_omni.cpp:183-222)."""
+    w, h = int(cam["Iw"]), int(cam["Ih"])
+    u0 = np.float32(cam["v0"])  # names swapped in the reference (:189-190)
+    v0 = np.float32(cam["u0"])
+    i = np.arange(h, dtype=np.float64)[:, None]
+    j = np.arange(w, dtype=np.float64)[None, :]
+    di = ((i - np.float64(u0)) ** 2).astype(np.float32)
+    dj = ((j - np.float64(v0)) ** 2).astype(np.float32)
+    ans = np.sqrt((di + dj).astype(np.float32)).astype(np.float32)
+    return np.where(ans < np.float32(u0 + np.float32(22.0)), 255, 0).astype(np.uint8)
+
+
+def img_to_world(cam, u, v):
+    """ImgToWorld (src/cam_model_omni.cpp:49-67), vectorised."""
+    inv_aff = cam["c"] - cam["d"] * cam["e"]
+    ut = u - cam["u0"]
+    vt = v - cam["v0"]
+    x = (ut - cam["d"] * vt) / inv_aff
+    y = (-cam["e"] * ut + cam["c"] * vt) / inv_aff
+    r = np.sqrt(x * x + y * y)
+    z = np.zeros_like(r)
+    for a in reversed(cam["a"]):
+        z = z * r + a
+    z = -z
+    n = np.sqrt(x * x + y * y + z * z)
+    return x / n, y / n, z / n
+
+
+def _panorama(rng, W=2048, H=1024):
+    img = np.zeros((H, W), np.float32)
+    # multi-octave value noise
+    for octave, amp in ((8, 60.0), (32, 30.0), (128, 14.0)):
+        g = rng.random((octave // 2 + 1, octave + 1)).astype(np.float32)
+        yi = np.linspace(0, g.shape[0] - 1, H, dtype=np.float32)
+        xi = np.linspace(0, g.shape[1] - 1, W, dtype=np.float32)
+        y0 = np.floor(yi).astype(int).clip(0, g.shape[0] - 2)
+        x0 = np.floor(xi).astype(int).clip(0, g.shape[1] - 2)
+        fy = (yi - y0)[:, None]
+        fx = (xi - x0)[None, :]
+        a = g[y0][:, x0]
+        b = g[y0][:, x0 + 1]
+        c = g[y0 + 1][:, x0]
+        d = g[y0 + 1][:, x0 + 1]
+        img += amp * ((a * (1 - fx) + b * fx) * (1 - fy) + (c * (1 - fx) + d * fx) * fy)
+    # random rectangles (sharp corners -> FAST corners)
+    for _ in range(900):
+        w = int(rng.integers(6, 90))
+        h = int(rng.integers(6, 70))
+        x = int(rng.integers(0, W - w))
+        y = int(rng.integers(0, H - h))
+        img[y:y + h, x:x + w] = img[y:y + h, x:x + w] * 0.3 + float(rng.uniform(0, 255)) * 0.7
+    # checker patches
+    for _ in range(40):
+        s = int(rng.integers(4, 14))
+        n = int(rng.integers(3, 9))
+        x = int(rng.integers(0, W - s * n))
+        y = int(rng.integers(0, H - s * n))
+        lo, hi = sorted(rng.uniform(0, 255, 2))
+        yy, xx = np.mgrid[0:s * n, 0:s * n]
+        img[y:y + s * n, x:x + s * n] = np.where(((yy // s) + (xx // s)) % 2 == 0, lo, hi)
+    return img
+
+
+_PANO_CACHE = {}
+
+
+def fisheye_frame(width=754, height=480, seed=0, cam_index=0, yaw=0.0, cam=None, noise=2.0):
+    """Render one synthetic 8-bit fisheye frame and its mirror mask."""
+    cams = LAFIDA_CAMS
+    if cam is None:
+        cam = cams[cam_index % len(cams)]
+        if (width, height) != (cam["Iw"], cam["Ih"]):
+            cam = scaled_cam(cam, width, height)
+    key = seed % 7
+    if key not in _PANO_CACHE:
+        _PANO_CACHE[key] = _panorama(np.random.default_rng(1000 + key))
+    pano = _PANO_CACHE[key]
+    rng = np.random.default_rng(seed)
+    yaw = yaw + float(rng.uniform(0, 2 * np.pi))
+    pitch = float(rng.uniform(-0.3, 0.3))
+    v, u = np.mgrid[0:height, 0:width].astype(np.float64)
+    x, y, z = img_to_world(cam, u, v)
+    # rotate: pitch about x, then yaw about the (camera) optical axis
+    cy, sy = np.cos(pitch), np.sin(pitch)
+    y, z = cy * y - sy * z, sy * y + cy * z
+    az = np.arctan2(y, x) + yaw
+    el = np.arctan2(-z, np.sqrt(x * x + y * y))
+    H, W = pano.shape
+    px = ((az / (2 * np.pi)) % 1.0) * (W - 1)
+    py = np.clip((el / np.pi + 0.5), 0, 1) * (H - 1)
+    x0 = np.floor(px).astype(int)
+    y0 = np.floor(py).astype(int)
+    x1 = np.minimum(x0 + 1, W - 1)
+    y1 = np.minimum(y0 + 1, H - 1)
+    fx = px - x0
+    fy = py - y0
+    val = (pano[y0, x0] * (1 - fx) + pano[y0, x1] * fx) * (1 - fy) + \
+          (pano[y1, x0] * (1 - fx) + pano[y1, x1] * fx) * fy
+    val = val + rng.normal(0, noise, val.shape)
+    img = np.clip(np.rint(val), 0, 255).astype(np.uint8)
+    mask = mirror_mask(cam)
+    img[mask == 0] = 0
+    return img, mask
+
+
+def random_frame(width, height, seed):
+    """Unstructured uniform-noise frame (edge-case tests: many weak corners)."""
+    return np.random.default_rng(seed).integers(0, 256, (height, width), dtype=np.uint8)

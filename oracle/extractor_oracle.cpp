@@ -1,0 +1,667 @@
+// ============================================================================
+// ORACLE -- TEST INFRASTRUCTURE ONLY.  Never linked into, or called by, the
+// product library.  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load it (as the checker / the timed CPU baseline).
+//
+// CPU restatement of the reference feature extractor (ORB path of
+// mdBRIEFextractorOct), following /root/reference/src/mdBRIEFextractorOct.cpp
+// line by line, with the OpenCV behaviour it delegates to written down as our
+// own pinned spec:
+//   * cv::resize INTER_LINEAR 8U (11-bit fixed point; OpenCV 3.1 x86 SSE2
+//     vertical pass by default, scalar-only form as a switch)      -- A.1
+//   * cv::resize INTER_NEAREST (mask pyramid)                      -- A.3
+//   * FAST-9/16 score + per-ROI non-max suppression + runByPixelsMask -- A.4
+//   * fastAtan2 (float polynomial, no FMA contraction)             -- A.7
+//   * boxFilter 5x5 normalized (OpenCV 3.x: round(sum/25))         -- A.8
+//   * cvRound = round half to even                                 -- A.9
+//
+// PARITY STATUS: *unpinned* against the real reference binary -- OpenCV is not
+// vendored and absent from this image, and the reference has no tests or golden
+// vectors for this path.  In-repo pins: the learned pattern table, umax, the
+// per-level budget formula and level sizes (all checked in tests/).
+//
+// One deliberate convention: DistributeOctTree sorts (size, node pointer) pairs
+// (mdBRIEFextractorOct.cpp:782); equal sizes are ordered by heap address, which
+// is allocator-dependent.  We order ties by node creation sequence (later
+// created == "higher address"), identically in oracle and GPU path.
+// Build: g++ -O2 -ffp-contract=off -fPIC -shared (see __graft_entry__.build()).
+// ============================================================================
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <cfloat>
+#include <algorithm>
+#include <list>
+#include <vector>
+#include <utility>
+
+namespace {
+
+const int kPatternFull[2048] = {
+#include "../multicol-slam-annotation_amd/csrc/pattern_orb64.inc"
+};
+
+const int EDGE_THRESHOLD = 25;   // mdBRIEFextractorOct.cpp:86
+const int PATCH_SIZE = 32;       // :84
+const int HALF_PATCH_SIZE = 16;  // :85
+const float DEG2RADf = static_cast<float>(3.14159265358979323846) / 180.f;  // :83
+
+inline int cvRound(double v) { return (int)std::lrint(v); }
+inline int cvRoundf(float v) { return (int)std::lrintf(v); }
+inline int cvFloor(double v) { int i = (int)v; return i - (i > v); }
+inline int cvFloorf(float v) { int i = (int)v; return i - (i > v); }
+inline short sat_short_from_float(float v) {
+  int i = cvRoundf(v);
+  return (short)std::min(std::max(i, -32768), 32767);
+}
+inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
+
+struct Img {
+  int w = 0, h = 0;
+  std::vector<uint8_t> d;
+  void create(int W, int H) { w = W; h = H; d.assign((size_t)W * H, 0); }
+  uint8_t* row(int y) { return d.data() + (size_t)y * w; }
+  const uint8_t* row(int y) const { return d.data() + (size_t)y * w; }
+  uint8_t at(int y, int x) const { return d[(size_t)y * w + x]; }
+};
+
+// ---------------------------------------------------------------------------
+// A.1  resize INTER_LINEAR, 8U, downscale (called at mdBRIEFextractorOct.cpp:1179)
+// ---------------------------------------------------------------------------
+struct LinearTables {
+  std::vector<int> xofs, yofs;
+  std::vector<short> alpha, beta;  // 2 per dx / dy
+  int xmax = 0;
+};
+
+void build_linear_tables(int sw, int sh, int dw, int dh, LinearTables& t) {
+  double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+  double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+  t.xofs.resize(dw); t.alpha.resize(2 * dw);
+  t.yofs.resize(dh); t.beta.resize(2 * dh);
+  t.xmax = dw;
+  for (int dx = 0; dx < dw; dx++) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cvFloorf(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= sw) {
+      t.xmax = std::min(t.xmax, dx);
+      if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    }
+    t.xofs[dx] = sx;
+    float c0 = 1.f - fx, c1 = fx;
+    t.alpha[2 * dx] = sat_short_from_float(c0 * 2048);
+    t.alpha[2 * dx + 1] = sat_short_from_float(c1 * 2048);
+  }
+  for (int dy = 0; dy < dh; dy++) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cvFloorf(fy);
+    fy -= sy;
+    t.yofs[dy] = sy;
+    float c0 = 1.f - fy, c1 = fy;
+    t.beta[2 * dy] = sat_short_from_float(c0 * 2048);
+    t.beta[2 * dy + 1] = sat_short_from_float(c1 * 2048);
+  }
+}
+
+inline int clip_row(int y, int h) { return y >= 0 ? (y < h ? y : h - 1) : 0; }
+
+// vertical pass, scalar form (FixedPtCast<int,uchar,22>)
+inline uint8_t vres_scalar(int s0, int s1, short b0, short b1) {
+  return sat_u8((s0 * b0 + s1 * b1 + (1 << 21)) >> 22);
+}
+// vertical pass, SSE2 form of OpenCV 3.1 VResizeLinearVec_32s8u
+inline uint8_t vres_simd(int s0, int s1, short b0, short b1) {
+  int16_t x0 = (int16_t)std::min(std::max(s0 >> 4, -32768), 32767);   // packs_epi32
+  int16_t y0 = (int16_t)std::min(std::max(s1 >> 4, -32768), 32767);
+  int a = ((int)x0 * b0) >> 16;                                       // mulhi_epi16
+  int b = ((int)y0 * b1) >> 16;
+  int s = std::min(std::max(a + b, -32768), 32767);                   // adds_epi16
+  s = std::min(std::max(s + 2, -32768), 32767);                       // adds_epi16(delta)
+  s >>= 2;                                                            // srai_epi16
+  return sat_u8(s);                                                   // packus_epi16
+}
+
+// mode 0 = scalar-only, 1 = OpenCV 3.1 SSE2 split (16-wide, then 4-wide, then scalar)
+void resize_linear(const Img& src, Img& dst, int dw, int dh, int mode) {
+  LinearTables t;
+  build_linear_tables(src.w, src.h, dw, dh, t);
+  dst.create(dw, dh);
+  std::vector<int> r0(dw), r1(dw);
+  auto hres = [&](int sy, std::vector<int>& r) {
+    const uint8_t* S = src.row(sy);
+    int dx = 0;
+    for (; dx < t.xmax; dx++) {
+      int sx = t.xofs[dx];
+      r[dx] = S[sx] * t.alpha[2 * dx] + S[sx + 1] * t.alpha[2 * dx + 1];
+    }
+    for (; dx < dw; dx++) r[dx] = S[t.xofs[dx]] * 2048;
+  };
+  for (int dy = 0; dy < dh; dy++) {
+    int sy0 = t.yofs[dy];
+    hres(clip_row(sy0, src.h), r0);
+    hres(clip_row(sy0 + 1, src.h), r1);
+    short b0 = t.beta[2 * dy], b1 = t.beta[2 * dy + 1];
+    uint8_t* D = dst.row(dy);
+    int x = 0;
+    if (mode == 1) {
+      for (; x <= dw - 16; x += 16)
+        for (int k = 0; k < 16; k++) D[x + k] = vres_simd(r0[x + k], r1[x + k], b0, b1);
+      for (; x < dw - 4; x += 4)
+        for (int k = 0; k < 4; k++) D[x + k] = vres_simd(r0[x + k], r1[x + k], b0, b1);
+    }
+    for (; x < dw; x++) D[x] = vres_scalar(r0[x], r1[x], b0, b1);
+  }
+}
+
+// A.3 resize INTER_NEAREST (mask pyramid, :1182)
+void resize_nearest(const Img& src, Img& dst, int dw, int dh) {
+  dst.create(dw, dh);
+  double ifx = 1. / ((double)dw / src.w), ify = 1. / ((double)dh / src.h);
+  std::vector<int> xo(dw);
+  for (int x = 0; x < dw; x++) xo[x] = std::min(cvFloor(x * ifx), src.w - 1);
+  for (int y = 0; y < dh; y++) {
+    int sy = std::min(cvFloor(y * ify), src.h - 1);
+    for (int x = 0; x < dw; x++) dst.row(y)[x] = src.at(sy, xo[x]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A.4 FAST-9/16 (OpenCV FAST_t<16> + cornerScore<16>) on an ROI, NMS, mask.
+// ---------------------------------------------------------------------------
+const int kCircle[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                            {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+struct Cand { int x, y, score; };
+
+int fast_score16(const Img& im, int x, int y, int threshold) {
+  int v = im.at(y, x);
+  int d[25];
+  for (int k = 0; k < 25; k++) d[k] = v - im.at(y + kCircle[k % 16][1], x + kCircle[k % 16][0]);
+  int a0 = threshold;
+  for (int k = 0; k < 16; k += 2) {
+    int a = std::min(d[k + 1], d[k + 2]);
+    a = std::min(a, d[k + 3]);
+    if (a <= a0) continue;
+    a = std::min(a, d[k + 4]); a = std::min(a, d[k + 5]); a = std::min(a, d[k + 6]);
+    a = std::min(a, d[k + 7]); a = std::min(a, d[k + 8]);
+    a0 = std::max(a0, std::min(a, d[k]));
+    a0 = std::max(a0, std::min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+  for (int k = 0; k < 16; k += 2) {
+    int b = std::max(d[k + 1], d[k + 2]);
+    b = std::max(b, d[k + 3]); b = std::max(b, d[k + 4]); b = std::max(b, d[k + 5]);
+    if (b >= b0) continue;
+    b = std::max(b, d[k + 6]); b = std::max(b, d[k + 7]); b = std::max(b, d[k + 8]);
+    b0 = std::min(b0, std::max(b, d[k]));
+    b0 = std::min(b0, std::max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// corner test exactly as FAST_t: >8 contiguous of the 25-long wrapped circle
+bool fast_is_corner(const Img& im, int x, int y, int threshold) {
+  int v = im.at(y, x);
+  int vt_lo = v - threshold, vt_hi = v + threshold;
+  int cnt = 0;
+  for (int k = 0; k < 25; k++) {
+    int p = im.at(y + kCircle[k % 16][1], x + kCircle[k % 16][0]);
+    if (p < vt_lo) { if (++cnt > 8) return true; } else cnt = 0;
+  }
+  cnt = 0;
+  for (int k = 0; k < 25; k++) {
+    int p = im.at(y + kCircle[k % 16][1], x + kCircle[k % 16][0]);
+    if (p > vt_hi) { if (++cnt > 8) return true; } else cnt = 0;
+  }
+  return false;
+}
+
+// FastFeatureDetector(th, nonmax=true, TYPE_9_16)::detect(roi, kps, maskRoi):
+// FAST on the ROI [x0,x1)x[y0,y1) of `im`, then runByPixelsMask.  Output
+// coordinates are ROI-local, emitted row-major.
+void fast_detect_roi(const Img& im, const Img* mask, int x0, int y0, int x1, int y1,
+                     int threshold, std::vector<Cand>& out) {
+  threshold = std::min(std::max(threshold, 0), 255);
+  int cols = x1 - x0, rows = y1 - y0;
+  std::vector<int> score((size_t)std::max(rows, 0) * std::max(cols, 0), 0);
+  std::vector<uint8_t> corner(score.size(), 0);
+  for (int i = 3; i < rows - 3; i++)
+    for (int j = 3; j < cols - 3; j++)
+      if (fast_is_corner(im, x0 + j, y0 + i, threshold)) {
+        corner[(size_t)i * cols + j] = 1;
+        score[(size_t)i * cols + j] = (uint8_t)fast_score16(im, x0 + j, y0 + i, threshold);
+      }
+  auto S = [&](int i, int j) { return score[(size_t)i * cols + j]; };
+  for (int i = 3; i < rows - 3; i++)
+    for (int j = 3; j < cols - 3; j++) {
+      if (!corner[(size_t)i * cols + j]) continue;
+      int s = S(i, j);
+      bool keep = s > S(i, j + 1) && s > S(i, j - 1) && s > S(i - 1, j - 1) && s > S(i - 1, j) &&
+                  s > S(i - 1, j + 1) && s > S(i + 1, j - 1) && s > S(i + 1, j) && s > S(i + 1, j + 1);
+      if (!keep) continue;
+      if (mask && mask->at(y0 + i, x0 + j) == 0) continue;   // runByPixelsMask, (int)(v+0.5)
+      out.push_back({j, i, s});
+    }
+}
+
+// ---------------------------------------------------------------------------
+// DistributeOctTree (mdBRIEFextractorOct.cpp:569-861)
+// ---------------------------------------------------------------------------
+struct KP { float x, y; float response; int idx; };
+
+struct Node {
+  std::vector<KP> keys;
+  int ULx, ULy, URx, URy, BLx, BLy, BRx, BRy;
+  std::list<Node>::iterator lit;
+  bool bNoMore = false;
+  long seq = 0;  // creation sequence (stand-in for the allocator-dependent pointer order)
+  void divide(Node& n1, Node& n2, Node& n3, Node& n4) const {
+    const int halfX = (int)std::ceil(static_cast<double>(URx - ULx) / 2.0);
+    const int halfY = (int)std::ceil(static_cast<double>(BRy - ULy) / 2.0);
+    n1.ULx = ULx; n1.ULy = ULy; n1.URx = ULx + halfX; n1.URy = ULy;
+    n1.BLx = ULx; n1.BLy = ULy + halfY; n1.BRx = ULx + halfX; n1.BRy = ULy + halfY;
+    n2.ULx = n1.URx; n2.ULy = n1.URy; n2.URx = URx; n2.URy = URy;
+    n2.BLx = n1.BRx; n2.BLy = n1.BRy; n2.BRx = URx; n2.BRy = ULy + halfY;
+    n3.ULx = n1.BLx; n3.ULy = n1.BLy; n3.URx = n1.BRx; n3.URy = n1.BRy;
+    n3.BLx = BLx; n3.BLy = BLy; n3.BRx = n1.BRx; n3.BRy = BLy;
+    n4.ULx = n3.URx; n4.ULy = n3.URy; n4.URx = n2.BRx; n4.URy = n2.BRy;
+    n4.BLx = n3.BRx; n4.BLy = n3.BRy; n4.BRx = BRx; n4.BRy = BRy;
+    for (const KP& kp : keys) {
+      if (kp.x < n1.URx) {
+        if (kp.y < n1.BRy) n1.keys.push_back(kp); else n3.keys.push_back(kp);
+      } else if (kp.y < n1.BRy) n2.keys.push_back(kp);
+      else n4.keys.push_back(kp);
+    }
+    if (n1.keys.size() == 1) n1.bNoMore = true;
+    if (n2.keys.size() == 1) n2.bNoMore = true;
+    if (n3.keys.size() == 1) n3.bNoMore = true;
+    if (n4.keys.size() == 1) n4.bNoMore = true;
+  }
+};
+
+std::vector<KP> distribute_octree(const std::vector<KP>& toDistribute, int minX, int maxX, int minY,
+                                  int maxY, int N) {
+  const int nIni = cvRound(static_cast<double>(maxX - minX) / (maxY - minY));
+  const double hX = static_cast<double>(maxX - minX) / nIni;
+  std::list<Node> lNodes;
+  std::vector<Node*> vpIniNodes(nIni);
+  long seq = 0;
+  for (int i = 0; i < nIni; i++) {
+    Node ni;
+    ni.ULx = (int)(hX * static_cast<double>(i)); ni.ULy = 0;
+    ni.URx = (int)(hX * static_cast<double>(i + 1)); ni.URy = 0;
+    ni.BLx = ni.ULx; ni.BLy = maxY - minY;
+    ni.BRx = ni.URx; ni.BRy = maxY - minY;
+    ni.seq = seq++;
+    lNodes.push_back(ni);
+    vpIniNodes[i] = &lNodes.back();
+  }
+  for (const KP& kp : toDistribute) vpIniNodes[(size_t)(kp.x / hX)]->keys.push_back(kp);
+
+  auto lit = lNodes.begin();
+  while (lit != lNodes.end()) {
+    if (lit->keys.size() == 1) { lit->bNoMore = true; ++lit; }
+    else if (lit->keys.empty()) lit = lNodes.erase(lit);
+    else ++lit;
+  }
+
+  bool bFinish = false;
+  std::vector<std::pair<int, Node*>> vSizeAndPointerToNode;
+  auto push_child = [&](Node& c, bool countExpand, int& nToExpand) {
+    if (c.keys.empty()) return;
+    c.seq = seq++;
+    lNodes.push_front(c);
+    if (c.keys.size() > 1) {
+      if (countExpand) nToExpand++;
+      vSizeAndPointerToNode.push_back(std::make_pair((int)c.keys.size(), &lNodes.front()));
+      lNodes.front().lit = lNodes.begin();
+    }
+  };
+  while (!bFinish) {
+    int prevSize = (int)lNodes.size();
+    lit = lNodes.begin();
+    int nToExpand = 0;
+    vSizeAndPointerToNode.clear();
+    while (lit != lNodes.end()) {
+      if (lit->bNoMore) { ++lit; continue; }
+      Node n1, n2, n3, n4;
+      lit->divide(n1, n2, n3, n4);
+      push_child(n1, true, nToExpand); push_child(n2, true, nToExpand);
+      push_child(n3, true, nToExpand); push_child(n4, true, nToExpand);
+      lit = lNodes.erase(lit);
+    }
+    if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+      bFinish = true;
+    } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+      while (!bFinish) {
+        prevSize = (int)lNodes.size();
+        std::vector<std::pair<int, Node*>> vPrev = vSizeAndPointerToNode;
+        vSizeAndPointerToNode.clear();
+        // (size, pointer) ascending; pointer order pinned to creation sequence
+        std::sort(vPrev.begin(), vPrev.end(), [](const std::pair<int, Node*>& a, const std::pair<int, Node*>& b) {
+          if (a.first != b.first) return a.first < b.first;
+          return a.second->seq < b.second->seq;
+        });
+        int dummy = 0;
+        for (int j = (int)vPrev.size() - 1; j >= 0; j--) {
+          Node n1, n2, n3, n4;
+          vPrev[j].second->divide(n1, n2, n3, n4);
+          push_child(n1, false, dummy); push_child(n2, false, dummy);
+          push_child(n3, false, dummy); push_child(n4, false, dummy);
+          lNodes.erase(vPrev[j].second->lit);
+          if ((int)lNodes.size() >= N) break;
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) bFinish = true;
+      }
+    }
+  }
+  std::vector<KP> res;
+  for (auto& nd : lNodes) {
+    const KP* best = &nd.keys[0];
+    float maxR = best->response;
+    for (size_t k = 1; k < nd.keys.size(); k++)
+      if (nd.keys[k].response > maxR) { best = &nd.keys[k]; maxR = nd.keys[k].response; }
+    res.push_back(*best);
+  }
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+// A.7 fastAtan2 (OpenCV 3.x mathfuncs) and IC_Angle (:221-248)
+// ---------------------------------------------------------------------------
+float fast_atan2(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / 3.14159265358979323846);
+  const float p3 = -0.3258083974640975f * (float)(180 / 3.14159265358979323846);
+  const float p5 = 0.1555786518463281f * (float)(180 / 3.14159265358979323846);
+  const float p7 = -0.04432655554792128f * (float)(180 / 3.14159265358979323846);
+  float ax = std::fabs(x), ay = std::fabs(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+std::vector<int> make_umax() {  // ctor :187-202
+  std::vector<int> umax(HALF_PATCH_SIZE + 1);
+  int v, v0, vmax = (int)std::floor(HALF_PATCH_SIZE * std::sqrt(2.f) / 2 + 1);
+  int vmin = (int)std::ceil(HALF_PATCH_SIZE * std::sqrt(2.f) / 2);
+  const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+  for (v = 0; v <= vmax; ++v) umax[v] = cvRound(std::sqrt(hp2 - v * v));
+  for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+  return umax;
+}
+
+float ic_angle(const Img& im, int cx, int cy, const std::vector<int>& umax, int* m01o = nullptr,
+               int* m10o = nullptr) {
+  int m_01 = 0, m_10 = 0;
+  for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * im.at(cy, cx + u);
+  for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+    int v_sum = 0, d = umax[v];
+    for (int u = -d; u <= d; ++u) {
+      int vp = im.at(cy + v, cx + u), vm = im.at(cy - v, cx + u);
+      v_sum += vp - vm;
+      m_10 += u * (vp + vm);
+    }
+    m_01 += v * v_sum;
+  }
+  if (m01o) *m01o = m_01;
+  if (m10o) *m10o = m_10;
+  return fast_atan2((float)m_01, (float)m_10);
+}
+
+// A.8 boxFilter 5x5 normalized, BORDER_REFLECT_101 (:1301)
+inline int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+void box_blur5(const Img& src, Img& dst) {
+  dst.create(src.w, src.h);
+  for (int y = 0; y < src.h; y++)
+    for (int x = 0; x < src.w; x++) {
+      int s = 0;
+      for (int dy = -2; dy <= 2; dy++)
+        for (int dx = -2; dx <= 2; dx++) s += src.at(reflect101(y + dy, src.h), reflect101(x + dx, src.w));
+      dst.row(y)[x] = (uint8_t)cvRound(s * (1. / 25));
+    }
+}
+
+// A.9 compute_ORB + rotatePattern (:285-354)
+void orb_descriptor(const Img& blurred, float kx, float ky, float angle_deg, int descsize,
+                    uint8_t* desc) {
+  const int npoints = 2 * 8 * descsize;
+  double angle = static_cast<double>(angle_deg * DEG2RADf);
+  double a = std::cos(angle), b = std::sin(angle);
+  int row = cvRound(ky), col = cvRound(kx);
+  for (int i = 0; i < descsize; ++i) {
+    int val = 0;
+    for (int k = 0; k < 8; k++) {
+      int p0 = 16 * i + 2 * k, p1 = p0 + 1;
+      if (p1 >= npoints) break;
+      int x0 = kPatternFull[2 * p0], y0 = kPatternFull[2 * p0 + 1];
+      int x1 = kPatternFull[2 * p1], y1 = kPatternFull[2 * p1 + 1];
+      int rx0 = cvRound(x0 * a - y0 * b), ry0 = cvRound(x0 * b + y0 * a);
+      int rx1 = cvRound(x1 * a - y1 * b), ry1 = cvRound(x1 * b + y1 * a);
+      int t0 = blurred.at(row + ry0, col + rx0), t1 = blurred.at(row + ry1, col + rx1);
+      val |= (t0 < t1) << k;
+    }
+    desc[i] = (uint8_t)val;
+  }
+}
+
+struct Params {
+  int nfeatures; float scale_factor; int nlevels; int fast_threshold; int desc_size; int vresize_mode;
+};
+
+struct Level { int w, h; };
+
+void level_sizes(int W, int H, const Params& p, std::vector<Level>& lv, std::vector<double>& sf,
+                 std::vector<double>& isf) {
+  sf.assign(p.nlevels, 1.0); isf.assign(p.nlevels, 1.0);
+  double scaleFactor = p.scale_factor;  // float ctor argument stored as double (:147)
+  for (int i = 1; i < p.nlevels; i++) sf[i] = sf[i - 1] * scaleFactor;
+  double inv = 1.0 / scaleFactor;
+  for (int i = 1; i < p.nlevels; i++) isf[i] = isf[i - 1] * inv;
+  lv.resize(p.nlevels);
+  for (int l = 0; l < p.nlevels; l++) lv[l] = {cvRound((double)W * isf[l]), cvRound((double)H * isf[l])};
+}
+
+std::vector<int> features_per_level(const Params& p) {  // ctor :167-179
+  std::vector<int> n(p.nlevels);
+  double factor = 1.0 / (double)p.scale_factor;
+  double nd = p.nfeatures * (1 - factor) / (1 - std::pow(factor, p.nlevels));
+  int sum = 0;
+  for (int l = 0; l < p.nlevels - 1; l++) { n[l] = cvRound(nd); sum += n[l]; nd *= factor; }
+  n[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+  return n;
+}
+
+// per-level FAST cell sweep (ComputeKeyPointsOctTree :874-949), candidates in
+// reference order with coordinates relative to minBorder
+void level_candidates(const Img& im, const Img* mask, int fastTh, std::vector<KP>& out) {
+  const double Wc = 30.0;
+  const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+  const int maxBorderX = im.w - EDGE_THRESHOLD + 3, maxBorderY = im.h - EDGE_THRESHOLD + 3;
+  const double width = maxBorderX - minBorderX, height = maxBorderY - minBorderY;
+  const int nCols = (int)(width / Wc), nRows = (int)(height / Wc);
+  const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+  for (int i = 0; i < nRows; i++) {
+    const double iniY = minBorderY + i * hCell;
+    double maxY = iniY + hCell + 6;
+    if (iniY >= maxBorderY - 3) continue;
+    if (maxY > maxBorderY) maxY = maxBorderY;
+    for (int j = 0; j < nCols; j++) {
+      const double iniX = minBorderX + j * wCell;
+      double maxX = iniX + wCell + 6;
+      if (iniX >= maxBorderX - 6) continue;
+      if (maxX > maxBorderX) maxX = maxBorderX;
+      std::vector<Cand> cell;
+      fast_detect_roi(im, mask, (int)iniX, (int)iniY, (int)maxX, (int)maxY, fastTh, cell);
+      for (auto& c : cell)
+        out.push_back({(float)(c.x + j * wCell), (float)(c.y + i * hCell), (float)c.score, (int)out.size()});
+    }
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// extern "C" surface for ctypes (tests / bench cpu_baseline only)
+// ===========================================================================
+extern "C" {
+
+struct oracle_keypoint { float x, y, size, angle, response; int octave, class_id; };
+
+int oracle_level_sizes(int W, int H, int nlevels, float scale_factor, int* wh_out) {
+  Params p{0, scale_factor, nlevels, 20, 32, 1};
+  std::vector<Level> lv; std::vector<double> sf, isf;
+  level_sizes(W, H, p, lv, sf, isf);
+  for (int l = 0; l < nlevels; l++) { wh_out[2 * l] = lv[l].w; wh_out[2 * l + 1] = lv[l].h; }
+  return 0;
+}
+
+int oracle_features_per_level(int nfeatures, int nlevels, float scale_factor, int* out) {
+  Params p{nfeatures, scale_factor, nlevels, 20, 32, 1};
+  auto n = features_per_level(p);
+  for (int l = 0; l < nlevels; l++) out[l] = n[l];
+  return 0;
+}
+
+int oracle_umax(int* out17) {
+  auto u = make_umax();
+  for (int i = 0; i < 17; i++) out17[i] = u[i];
+  return 0;
+}
+
+int oracle_pattern(int* out2048) { std::memcpy(out2048, kPatternFull, sizeof(kPatternFull)); return 0; }
+
+float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+// resize one level (A.1); src w*h, dst dw*dh
+int oracle_resize_linear(const uint8_t* src, int w, int h, uint8_t* dst, int dw, int dh, int mode) {
+  Img s; s.create(w, h); std::memcpy(s.d.data(), src, (size_t)w * h);
+  Img d; resize_linear(s, d, dw, dh, mode);
+  std::memcpy(dst, d.d.data(), (size_t)dw * dh);
+  return 0;
+}
+
+int oracle_resize_nearest(const uint8_t* src, int w, int h, uint8_t* dst, int dw, int dh) {
+  Img s; s.create(w, h); std::memcpy(s.d.data(), src, (size_t)w * h);
+  Img d; resize_nearest(s, d, dw, dh);
+  std::memcpy(dst, d.d.data(), (size_t)dw * dh);
+  return 0;
+}
+
+int oracle_box_blur5(const uint8_t* src, int w, int h, uint8_t* dst) {
+  Img s; s.create(w, h); std::memcpy(s.d.data(), src, (size_t)w * h);
+  Img d; box_blur5(s, d);
+  std::memcpy(dst, d.d.data(), (size_t)w * h);
+  return 0;
+}
+
+// FAST candidates of one level in reference order; xyr out as int triples
+// (x_rel, y_rel, score); mask may be NULL.
+int oracle_level_candidates(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
+                            int* xys_out, int cap, int* n_out) {
+  Img im; im.create(w, h); std::memcpy(im.d.data(), img, (size_t)w * h);
+  Img mk; if (mask) { mk.create(w, h); std::memcpy(mk.d.data(), mask, (size_t)w * h); }
+  std::vector<KP> c;
+  level_candidates(im, mask ? &mk : nullptr, fastTh, c);
+  *n_out = (int)c.size();
+  if ((int)c.size() > cap) return -1;
+  for (size_t i = 0; i < c.size(); i++) {
+    xys_out[3 * i] = (int)c[i].x; xys_out[3 * i + 1] = (int)c[i].y; xys_out[3 * i + 2] = (int)c[i].response;
+  }
+  return 0;
+}
+
+// octree on candidate triples (relative coords); returns selected candidate indices in output order
+int oracle_octree(const int* xys, int n, int minX, int maxX, int minY, int maxY, int N, int* idx_out,
+                  int cap, int* n_out) {
+  std::vector<KP> c(n);
+  for (int i = 0; i < n; i++) c[i] = {(float)xys[3 * i], (float)xys[3 * i + 1], (float)xys[3 * i + 2], i};
+  auto r = distribute_octree(c, minX, maxX, minY, maxY, N);
+  *n_out = (int)r.size();
+  if ((int)r.size() > cap) return -1;
+  for (size_t i = 0; i < r.size(); i++) idx_out[i] = r[i].idx;
+  return 0;
+}
+
+float oracle_ic_angle(const uint8_t* img, int w, int h, int cx, int cy, int* m01, int* m10) {
+  Img im; im.create(w, h); std::memcpy(im.d.data(), img, (size_t)w * h);
+  static std::vector<int> umax = make_umax();
+  return ic_angle(im, cx, cy, umax, m01, m10);
+}
+
+// Full extractor: mdBRIEFextractorOct::operator() ORB path (:1244-1337).
+// kps/desc caller-allocated (cap keypoints).  Returns 0, or -1 if cap too small.
+int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
+                   float scale_factor, int nlevels, int fast_threshold, int desc_size,
+                   int vresize_mode, oracle_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+  Params p{nfeatures, scale_factor, nlevels, fast_threshold, desc_size, vresize_mode};
+  std::vector<Level> lv; std::vector<double> sf, isf;
+  level_sizes(W, H, p, lv, sf, isf);
+  auto nPerLevel = features_per_level(p);
+  auto umax = make_umax();
+  // ComputePyramid (:1158-1201)
+  std::vector<Img> pyr(nlevels), mpyr(nlevels);
+  pyr[0].create(W, H); std::memcpy(pyr[0].d.data(), image, (size_t)W * H);
+  if (mask) { mpyr[0].create(W, H); std::memcpy(mpyr[0].d.data(), mask, (size_t)W * H); }
+  for (int l = 1; l < nlevels; l++) {
+    resize_linear(pyr[l - 1], pyr[l], lv[l].w, lv[l].h, vresize_mode);
+    if (mask) resize_nearest(mpyr[l - 1], mpyr[l], lv[l].w, lv[l].h);
+  }
+  // ComputeKeyPointsOctTree (:863-976)
+  std::vector<std::vector<KP>> all(nlevels);
+  const int minBorder = EDGE_THRESHOLD - 3;
+  for (int l = 0; l < nlevels; l++) {
+    std::vector<KP> cands;
+    level_candidates(pyr[l], mask ? &mpyr[l] : nullptr, fast_threshold, cands);
+    all[l] = distribute_octree(cands, minBorder, pyr[l].w - EDGE_THRESHOLD + 3, minBorder,
+                               pyr[l].h - EDGE_THRESHOLD + 3, nPerLevel[l]);
+    for (auto& k : all[l]) { k.x += minBorder; k.y += minBorder; }
+  }
+  int total = 0;
+  for (int l = 0; l < nlevels; l++) total += (int)all[l].size();
+  *n_out = total;
+  if (total > cap) return -1;
+  int off = 0;
+  for (int l = 0; l < nlevels; l++) {
+    const int scaledPatchSize = (int)(PATCH_SIZE * sf[l]);
+    std::vector<float> ang(all[l].size());
+    for (size_t i = 0; i < all[l].size(); i++)
+      ang[i] = ic_angle(pyr[l], cvRoundf(all[l][i].x), cvRoundf(all[l][i].y), umax);
+    if (all[l].empty()) continue;
+    Img blurred;
+    box_blur5(pyr[l], blurred);
+    float scale = (float)sf[l];
+    for (size_t i = 0; i < all[l].size(); i++) {
+      const KP& k = all[l][i];
+      orb_descriptor(blurred, k.x, k.y, ang[i], desc_size, desc + (size_t)(off + i) * desc_size);
+      oracle_keypoint& o = kps[off + i];
+      o.x = k.x; o.y = k.y;
+      if (l != 0) { o.x = k.x * scale; o.y = k.y * scale; }
+      o.size = (float)scaledPatchSize; o.angle = ang[i]; o.response = k.response;
+      o.octave = l; o.class_id = -1;
+    }
+    off += (int)all[l].size();
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,164 @@
+"""ctypes binding of oracle/build/liboracle.so -- the CPU restatement used as CHECKER.
+
+Test infrastructure only (tests/, __graft_entry__.smoke(), bench.py cpu_baseline leg).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+_SIGS = {
+    "oracle_level_sizes": (_I, [_I, _I, _I, _F, _P]),
+    "oracle_features_per_level": (_I, [_I, _I, _F, _P]),
+    "oracle_umax": (_I, [_P]),
+    "oracle_pattern": (_I, [_P]),
+    "oracle_fast_atan2": (_F, [_F, _F]),
+    "oracle_resize_linear": (_I, [_P, _I, _I, _P, _I, _I, _I]),
+    "oracle_resize_nearest": (_I, [_P, _I, _I, _P, _I, _I]),
+    "oracle_box_blur5": (_I, [_P, _I, _I, _P]),
+    "oracle_level_candidates": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
+    "oracle_octree": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P]),
+    "oracle_ic_angle": (_F, [_P, _I, _I, _I, _I, _P, _P]),
+    "oracle_extract": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _P, _P, _I, _P]),
+    # matcher oracle
+    "oracle_descriptor_distance64": (_I, [_P, _P, _I]),
+    "oracle_descriptor_distance64_masked": (_I, [_P, _P, _P, _P, _I]),
+    "oracle_hamming_top2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
+    "oracle_search_for_triangulation_raw": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            import importlib
+            import sys
+            sys.path.insert(0, ROOT)
+            importlib.import_module("__graft_entry__").build_oracle()
+        L = ctypes.CDLL(ORACLE_LIB)
+        for n, (r, a) in _SIGS.items():
+            if hasattr(L, n):
+                f = getattr(L, n)
+                f.restype = r
+                f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def level_sizes(W, H, nlevels=8, scale=1.2):
+    out = np.zeros(2 * nlevels, np.int32)
+    lib().oracle_level_sizes(W, H, nlevels, scale, _p(out))
+    return out.reshape(nlevels, 2)
+
+
+def features_per_level(nfeatures, nlevels=8, scale=1.2):
+    out = np.zeros(nlevels, np.int32)
+    lib().oracle_features_per_level(nfeatures, nlevels, scale, _p(out))
+    return out
+
+
+def umax():
+    out = np.zeros(17, np.int32)
+    lib().oracle_umax(_p(out))
+    return out
+
+
+def pattern():
+    out = np.zeros(2048, np.int32)
+    lib().oracle_pattern(_p(out))
+    return out
+
+
+def resize_linear(src, dw, dh, mode=1):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh, mode)
+    return dst
+
+
+def resize_nearest(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_nearest(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh)
+    return dst
+
+
+def box_blur5(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().oracle_box_blur5(_p(src), src.shape[1], src.shape[0], _p(dst))
+    return dst
+
+
+def pyramid(img, nlevels=8, scale=1.2, mode=1):
+    sizes = level_sizes(img.shape[1], img.shape[0], nlevels, scale)
+    levels = [np.ascontiguousarray(img, np.uint8)]
+    for l in range(1, nlevels):
+        levels.append(resize_linear(levels[-1], sizes[l][0], sizes[l][1], mode))
+    return levels
+
+
+def mask_pyramid(mask, nlevels=8, scale=1.2):
+    sizes = level_sizes(mask.shape[1], mask.shape[0], nlevels, scale)
+    levels = [np.ascontiguousarray(mask, np.uint8)]
+    for l in range(1, nlevels):
+        levels.append(resize_nearest(levels[-1], sizes[l][0], sizes[l][1]))
+    return levels
+
+
+def level_candidates(level_img, level_mask, fast_th):
+    h, w = level_img.shape
+    cap = w * h // 4 + 16
+    out = np.zeros(3 * cap, np.int32)
+    n = ctypes.c_int()
+    rc = lib().oracle_level_candidates(_p(np.ascontiguousarray(level_img)),
+                                       _p(None if level_mask is None else np.ascontiguousarray(level_mask)),
+                                       w, h, fast_th, _p(out), cap, ctypes.byref(n))
+    assert rc == 0
+    return out[:3 * n.value].reshape(-1, 3)
+
+
+def octree(cands, w, h, N):
+    cands = np.ascontiguousarray(cands, np.int32)
+    minB = 22
+    maxX, maxY = w - 22, h - 22
+    cap = max(N + 3, 64) * 4
+    out = np.zeros(cap, np.int32)
+    n = ctypes.c_int()
+    rc = lib().oracle_octree(_p(cands), len(cands), minB, maxX, minB, maxY, N, _p(out), cap,
+                             ctypes.byref(n))
+    assert rc == 0
+    return out[:n.value]
+
+
+def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, desc_size=32,
+            mode=1):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    cap = nfeatures * 2 + 64 * nlevels
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, desc_size), np.uint8)
+    n = ctypes.c_int()
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    rc = lib().oracle_extract(_p(img), W, H, _p(m), nfeatures, scale, nlevels, fast_th,
+                              desc_size, mode, _p(kps), _p(desc), cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()

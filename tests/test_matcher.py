@@ -1,0 +1,167 @@
+"""Matcher parity: DescriptorDistance64 (host, CPU test), Hamming top-2 / dense / batched
+top-2 and SearchForTriangulationRaw on the GPU vs the oracle -- exact integer equality.
+
+Reference: src/cORBmatcher.cpp:2443-2477 (distances), :968-1156 (triangulation search),
+:67-163 (best / second-best rule).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests import oracle_bind as ob
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _descs(n, bytes_=32, seed=0):
+    return np.random.default_rng(seed).integers(0, 256, (n, bytes_), dtype=np.uint8)
+
+
+def _noisy_copy(d, nflip, seed):
+    rng = np.random.default_rng(seed)
+    out = d.copy()
+    bits = np.unpackbits(out, axis=1)
+    for i in range(len(bits)):
+        idx = rng.choice(bits.shape[1], nflip[i], replace=False)
+        bits[i, idx] ^= 1
+    return np.packbits(bits, axis=1)
+
+
+@pytest.mark.parametrize("nbytes", [16, 32, 64])
+def test_descriptor_distance64_host(built, nbytes):
+    import mcs_amd
+    L = mcs_amd.lib()
+    a = _descs(200, nbytes, 1)
+    b = _descs(200, nbytes, 2)
+    for i in range(200):
+        ref = ob.lib().oracle_descriptor_distance64(_p(a[i]), _p(b[i]), nbytes)
+        assert ref == int(np.unpackbits(a[i] ^ b[i]).sum())
+        assert L.mcs_descriptor_distance64(_p(a[i]), _p(b[i]), nbytes) == ref
+    ma = _descs(200, nbytes, 3)
+    mb = _descs(200, nbytes, 4)
+    for i in range(50):
+        ref = ob.lib().oracle_descriptor_distance64_masked(_p(a[i]), _p(b[i]), _p(ma[i]), _p(mb[i]), nbytes)
+        got = L.mcs_descriptor_distance64_masked(_p(a[i]), _p(b[i]), _p(ma[i]), _p(mb[i]), nbytes)
+        assert got == ref
+
+
+def _oracle_top2(q, t):
+    n = len(q)
+    bi = np.zeros(n, np.int32)
+    bd = np.zeros(n, np.int32)
+    sd = np.zeros(n, np.int32)
+    ob.lib().oracle_hamming_top2(_p(np.ascontiguousarray(q)), len(q), _p(np.ascontiguousarray(t)),
+                                 len(t), q.shape[1], _p(bi), _p(bd), _p(sd))
+    return bi, bd, sd
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq,nt,nbytes", [(1000, 1300, 32), (257, 5, 16), (600, 700, 64), (1, 1, 32)])
+def test_top2_device(gpu, nq, nt, nbytes):
+    import torch
+    import mcs_amd
+    L = mcs_amd.lib()
+    q = _descs(nq, nbytes, 5)
+    t = np.concatenate([_noisy_copy(q[:min(nq, nt) // 2], [3] * (min(nq, nt) // 2), 6),
+                        _descs(nt - min(nq, nt) // 2, nbytes, 7)])
+    t[-1] = t[0]  # duplicate -> exercises the tie rule
+    dq = torch.from_numpy(q).cuda()
+    dt = torch.from_numpy(t).cuda()
+    out = [torch.zeros(nq, dtype=torch.int32, device="cuda") for _ in range(4)]
+    rc = L.mcs_hamming_top2_device(dq.data_ptr(), nq, dt.data_ptr(), nt, nbytes,
+                                   *[o.data_ptr() for o in out],
+                                   torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    bi, bd, sd = _oracle_top2(q, t)
+    assert np.array_equal(out[0].cpu().numpy(), bi)
+    assert np.array_equal(out[1].cpu().numpy(), bd)
+    assert np.array_equal(out[3].cpu().numpy(), sd)
+
+
+@pytest.mark.gpu
+def test_dense_device(gpu):
+    import torch
+    import mcs_amd
+    a = _descs(300, 32, 8)
+    b = _descs(517, 32, 9)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dd = torch.zeros((300, 517), dtype=torch.int16, device="cuda")
+    assert mcs_amd.lib().mcs_hamming_dense_device(da.data_ptr(), 300, db.data_ptr(), 517, 32,
+                                                  dd.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    ref = np.unpackbits(a[:, None, :] ^ b[None, :, :], axis=2).sum(2)
+    assert np.array_equal(dd.cpu().numpy().astype(np.int64), ref)
+
+
+@pytest.mark.gpu
+def test_top2_batch_ragged(gpu):
+    import torch
+    import mcs_amd
+    cap, nb = 700, 32
+    counts = np.array([700, 5, 0, 333], np.int32)
+    sets = np.zeros((4, cap, nb), np.uint8)
+    for s in range(4):
+        sets[s, :counts[s]] = _descs(counts[s], nb, 20 + s)
+    pairs = np.array([[0, 3], [3, 0], [1, 0], [2, 3], [3, 2]], np.int32)
+    d = torch.from_numpy(sets).cuda()
+    dc = torch.from_numpy(counts).cuda()
+    dp = torch.from_numpy(pairs).cuda()
+    out = [torch.full((len(pairs), cap), -7, dtype=torch.int32, device="cuda") for _ in range(4)]
+    rc = mcs_amd.lib().mcs_hamming_top2_batch_device(d.data_ptr(), dc.data_ptr(), dp.data_ptr(),
+                                                     len(pairs), cap, nb,
+                                                     *[o.data_ptr() for o in out], None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    for p, (qs, ts) in enumerate(pairs):
+        nq = counts[qs]
+        bi, bd, sd = _oracle_top2(sets[qs, :nq], sets[ts, :counts[ts]])
+        assert np.array_equal(out[0][p, :nq].cpu().numpy(), bi)
+        assert np.array_equal(out[1][p, :nq].cpu().numpy(), bd)
+        assert np.array_equal(out[3][p, :nq].cpu().numpy(), sd)
+
+
+def _tri_problem(seed, n1=1500, n2=1400, ncams=3, nbytes=32):
+    rng = np.random.default_rng(seed)
+    d1 = _descs(n1, nbytes, seed)
+    nm = min(n1, n2) // 2
+    perm = rng.permutation(n2)
+    d2 = _descs(n2, nbytes, seed + 1)
+    d2[perm[:nm]] = _noisy_copy(d1[:nm], rng.integers(0, 40, nm), seed + 2)
+    cam1 = rng.integers(0, ncams, n1).astype(np.int32)
+    cam2 = rng.integers(0, ncams, n2).astype(np.int32)
+    cam2[perm[:nm]] = cam1[:nm]
+    has1 = (rng.random(n1) < 0.1).astype(np.uint8)
+    has2 = (rng.random(n2) < 0.1).astype(np.uint8)
+    r1 = rng.normal(size=(n1, 3))
+    r1 /= np.linalg.norm(r1, axis=1, keepdims=True)
+    r2 = rng.normal(size=(n2, 3))
+    r2 /= np.linalg.norm(r2, axis=1, keepdims=True)
+    E = rng.normal(size=(ncams, ncams, 3, 3))
+    return d1, d2, cam1, cam2, has1, has2, r1, r2, E
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_search_for_triangulation_raw(gpu, seed):
+    import mcs_amd
+    d1, d2, cam1, cam2, has1, has2, r1, r2, E = _tri_problem(seed)
+    thresh = 0.3
+    ref = np.zeros(len(d1), np.int32)
+    nref = ob.lib().oracle_search_for_triangulation_raw(
+        _p(d1), len(d1), _p(d2), len(d2), 32, _p(cam1), _p(cam2), _p(has1), _p(has2),
+        _p(np.ascontiguousarray(r1)), _p(np.ascontiguousarray(r2)),
+        _p(np.ascontiguousarray(E)), thresh, 3, _p(ref))
+    got = np.zeros(len(d1), np.int32)
+    nm = ctypes.c_int32()
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw(
+        _p(d1), _p(cam1), _p(has1), _p(np.ascontiguousarray(r1)), len(d1),
+        _p(d2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), len(d2), 3,
+        _p(np.ascontiguousarray(E)), 32, 64, thresh, _p(got), ctypes.byref(nm))
+    assert rc == 0
+    assert nref > 50
+    assert nm.value == nref
+    assert np.array_equal(got, ref)
