@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Headline benchmark: kfeatures/sec (+ LocalBA iters/sec) for the MultiCol-SLAM
+front-end on MI355X.
+
+Workload (BASELINE.json configs[1], "config B"): 3-camera Lafida rig, 754x480 fisheye
+frames, 2000 features per camera, extract + match on one MI355X.  One step = one batch of
+M multi-frames (3*M camera-frames, default M=171 -> 513 camera-frames, inputs resident in
+HBM): pyramid -> FAST -> octree -> orientation -> ORB descriptor for every camera-frame,
+then brute-force Hamming best/second-best matching of every camera's descriptors against
+the same camera of the previous multi-frame (the O(N1*N2) part of
+SearchForTriangulationRaw, src/cORBmatcher.cpp:968-1156).
+
+Multi-GPU (torchrun, one process per GPU): every rank runs the same step on its own
+segment of multi-frames (independent units -> weak scaling, no data-path collective);
+the timed region is bracketed by barrier + synchronize and the max over ranks is taken.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "multicol-slam-annotation_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+METRIC = "kfeatures/sec + LocalBA iters/sec, 3×754×480 fisheye, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# algorithmic bytes of pyramid + FAST per 754x480 camera-frame
+PYR_FAST_BYTES_754x480 = 2_970_708
+
+
+def alg_bytes_pyr_fast(level_wh):
+    """B = sum_{l>=1}(|L_{l-1}| + |L_l|) + sum_l |L_l|  (SURVEY.md §8(d))."""
+    px = [int(w) * int(h) for w, h in level_wh]
+    return sum(px[l - 1] + px[l] for l in range(1, len(px))) + sum(px)
+
+
+def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
+    """Oracle (CPU restatement) on a bounded sample: one thread per camera, like the
+    reference's `#pragma omp parallel for num_threads(nrCams)` (src/cMultiFrame.cpp:128);
+    matching single-threaded per camera pair.  Returns (kfeatures/s, sample text, threads)."""
+    from tests import oracle_bind as ob
+    ob.lib()
+    nkp = 0
+    descs = [[None] * ncams for _ in range(n_multiframes)]
+    lock = threading.Lock()
+
+    def work(c):
+        nonlocal nkp
+        for t in range(n_multiframes):
+            k, d = ob.extract(imgs[t * ncams + c], masks[c], nfeatures=nfeatures)
+            descs[t][c] = d
+            with lock:
+                nkp += len(k)
+        for t in range(1, n_multiframes):
+            q, tr = descs[t - 1][c], descs[t][c]
+            _ = _oracle_top2(ob, q, tr)
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(c,)) for c in range(ncams)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    sample = "%d multi-frames x %d cams (extract+match), oracle restatement" % (n_multiframes, ncams)
+    return nkp / dt / 1e3, sample, ncams
+
+
+def _oracle_top2(ob, q, t):
+    import ctypes
+    n = len(q)
+    bi = np.zeros(n, np.int32)
+    bd = np.zeros(n, np.int32)
+    sd = np.zeros(n, np.int32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    ob.lib().oracle_hamming_top2(p(np.ascontiguousarray(q)), len(q), p(np.ascontiguousarray(t)),
+                                 len(t), q.shape[1], p(bi), p(bd), p(sd))
+    return bi, bd, sd
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--multiframes", type=int, default=171, help="multi-frames per rank per step")
+    ap.add_argument("--unique", type=int, default=12, help="distinct rendered multi-frames")
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--cpu-sample", type=int, default=12, help="multi-frames timed on the CPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stage-timing", type=int, default=1)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import mcs_amd
+    from mcs_amd import synth
+    L = mcs_amd.lib()
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream()
+
+    W, H, NC = 754, 480, 3
+    M = args.multiframes
+    U = min(args.unique, M)
+    uimgs, masks = synth.rig_sequence(U, W, H, NC, seed=1 + rank)
+    idx = np.arange(M) % U
+    imgs = uimgs.reshape(U, NC, H, W)[idx].reshape(M * NC, H, W)
+    F = M * NC
+
+    params = mcs_amd.ExtractorParams(nfeatures=args.nfeatures, fast_threshold=20)
+    ex = mcs_amd.Extractor(params, W, H, max_frames=F, device=local_rank)
+    cap = ex.capacity
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_mask = torch.from_numpy(masks).to(dev)
+    ex.set_masks_device(d_mask.data_ptr(), NC, stream.cuda_stream)
+    d_midx = torch.from_numpy(np.tile(np.arange(NC, dtype=np.int32), M)).to(dev)
+    d_kps = torch.zeros((F, cap * 7), dtype=torch.int32, device=dev)
+    d_cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    pairs = np.array([[t * NC + c, (t + 1) * NC + c] for t in range(M - 1) for c in range(NC)],
+                     np.int32)
+    d_pairs = torch.from_numpy(pairs).to(dev)
+    NP = len(pairs)
+    d_m = [torch.zeros((NP, cap), dtype=torch.int32, device=dev) for _ in range(4)]
+
+    ev_m0 = torch.cuda.Event(enable_timing=True)
+    ev_m1 = torch.cuda.Event(enable_timing=True)
+
+    def step(timed):
+        ex.extract_batch_device(d_img.data_ptr(), F, d_midx.data_ptr(), d_kps.data_ptr(),
+                                d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
+        if timed:
+            ev_m0.record(stream)
+        rc = L.mcs_hamming_top2_batch_device(d_desc.data_ptr(), d_cnt.data_ptr(),
+                                             d_pairs.data_ptr(), NP, cap, 32,
+                                             *[t.data_ptr() for t in d_m], stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError("matcher failed %d" % rc)
+        if timed:
+            ev_m1.record(stream)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if args.stage_timing:
+        ex.enable_timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    # matcher device time of the last step (events on the launch stream)
+    match_ms_last = ev_m0.elapsed_time(ev_m1)
+    stages, ncalls = ex.read_timing() if args.stage_timing else ({}, 0)
+
+    kp_per_step = int(d_cnt.sum().item())
+    t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
+    kp_tot = torch.tensor([kp_per_step * args.steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kp_tot, op=dist.ReduceOp.SUM)
+    dt_max = float(t_max.item())
+    value = float(kp_tot.item()) / dt_max / 1e3
+
+    wh, _ = ex.levels()
+    bpf = alg_bytes_pyr_fast(wh)
+    roofline = None
+    stage_ms = {}
+    if ncalls:
+        stage_ms = {k: v / ncalls for k, v in stages.items()}
+        t_pf = (stage_ms["pyramid"] + stage_ms["fast"]) / 1e3
+        achieved = bpf * F / t_pf / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get("pyramid+fast_bytes_per_call")
+            except Exception:
+                traffic = None
+        roofline = {"kernel": "pyramid+fast (k_resize_linear x7 + k_fast_cells)",
+                    "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "alg_bytes_per_call": bpf * F}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        S = min(args.cpu_sample, U)
+        v, sample, cores = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
+        cpu = {"value": round(v, 3), "unit": "kfeatures/s", "cores": cores, "kind": "port",
+               "sample": sample}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "kfeatures/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (Lafida-calibrated fisheye renders, resident in HBM)",
+            "config": {"workload": "config B: 3-cam Lafida rig 754x480, 2000 feat/cam, "
+                                   "extract + consecutive-multi-frame top-2 Hamming match",
+                       "camera_frames_per_step_per_gpu": F,
+                       "keypoints_per_step_per_gpu": kp_per_step,
+                       "match_pairs_per_step_per_gpu": NP,
+                       "parallelism": "dp%d (independent multi-frame segments)" % world},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+            "match_ms_per_step": round(match_ms_last, 4),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

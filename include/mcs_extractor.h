@@ -102,6 +102,17 @@ int mcs_extract_batch_device(mcs_extractor* h, const uint8_t* d_images, int32_t 
 int mcs_extractor_read_stage(mcs_extractor* h, int32_t stage, int32_t frame, int32_t level,
                              void* dst, int64_t cap, int64_t* n_out);
 
+/* Live per-stage device timing (hipEvents recorded on the call's stream around each
+ * stage of every batch call; no host synchronisation inside the call).  Stages:
+ * 0 pyramid (k_resize_linear x L-1), 1 blur (k_blur5), 2 FAST cells (k_fast_cells),
+ * 3 octree (k_octree), 4 orientation + descriptor (k_orient_desc).
+ * read_timing synchronises, returns the summed milliseconds per stage over the recorded
+ * calls and their number, and optionally resets.  At most 256 calls are kept. */
+#define MCS_EXTRACTOR_NSTAGES 5
+int mcs_extractor_enable_timing(mcs_extractor* h, int32_t enable);
+int mcs_extractor_read_timing(mcs_extractor* h, float* ms_per_stage, int32_t* ncalls,
+                              int32_t reset);
+
 #ifdef __cplusplus
 }
 #endif

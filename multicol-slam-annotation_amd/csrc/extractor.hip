@@ -764,6 +764,11 @@ struct mcs_extractor {
   // last call (for read_stage)
   const uint8_t* last_img0 = nullptr;
   int last_frames = 0;
+  // live stage timing: ring of event sets (MCS_EXTRACTOR_NSTAGES + 1 events per call)
+  static constexpr int kRing = 256;
+  bool timing = false;
+  hipEvent_t* ev = nullptr;   // [kRing][NSTAGES+1]
+  int ev_count = 0;           // calls recorded since last reset (<= kRing)
 };
 
 namespace mcs {
@@ -797,6 +802,11 @@ static int build_mask_pyramids(mcs_extractor* h, const uint8_t* d_masks, int n, 
   return MCS_OK;
 }
 
+static inline void stage_mark(mcs_extractor* h, int stage, hipStream_t st) {
+  if (!h->timing || h->ev_count >= mcs_extractor::kRing) return;
+  (void)hipEventRecord(h->ev[h->ev_count * (MCS_EXTRACTOR_NSTAGES + 1) + stage], st);
+}
+
 // Core batched pipeline on device buffers.
 static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uint8_t* mask_pyr,
                      const int32_t* d_mask_index, mcs_keypoint* d_kps, int32_t* d_counts,
@@ -805,6 +815,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   const int nl = pl.nlevels;
   const int64_t img0_fs = (int64_t)pl.W * pl.H;
   dim3 b256(256);
+  stage_mark(h, 0, st);
   // K1: pyramid chain
   for (int l = 1; l < nl; l++) {
     const LevelPlan& S = pl.lv[l - 1];
@@ -817,6 +828,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
                        h->d_alpha + 2 * pl.xtab_off[l], h->d_yofs + pl.ytab_off[l],
                        h->d_beta + 2 * pl.ytab_off[l], D.simd_end);
   }
+  stage_mark(h, 1, st);
   // K5: blur every level (only levels with keypoints are read)
   for (int l = 0; l < nl; l++) {
     const LevelPlan& L = pl.lv[l];
@@ -826,6 +838,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     hipLaunchKernelGGL(k_blur5, g, b256, 0, st, src, sfs, h->d_blur + L.img_off,
                        pl.img_frame_bytes, L.w, L.h);
   }
+  stage_mark(h, 2, st);
   // K2: FAST cells
   {
     FastArgs fa;
@@ -841,8 +854,9 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     dim3 g((unsigned)pl.cells.size(), F);
     hipLaunchKernelGGL(k_fast_cells, g, dim3(64), 0, st, fa);
   }
-  // K3: octree
   MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));
+  stage_mark(h, 3, st);
+  // K3: octree
   {
     OctArgs oa;
     std::memcpy(oa.lv, pl.lv, sizeof(oa.lv));
@@ -856,6 +870,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     dim3 g(nl, F);
     hipLaunchKernelGGL(k_octree, g, dim3(kOctThreads), 0, st, oa);
   }
+  stage_mark(h, 4, st);
   // K4+K6: orientation + descriptor
   {
     DescArgs da;
@@ -870,6 +885,8 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     dim3 g((pl.sel_per_frame + 3) / 4, F);
     hipLaunchKernelGGL(k_orient_desc, g, b256, 0, st, da);
   }
+  stage_mark(h, 5, st);
+  if (h->timing && h->ev_count < mcs_extractor::kRing) h->ev_count++;
   MCS_HIP_CHECK(hipGetLastError());
   h->last_img0 = d_images;
   h->last_frames = F;
@@ -977,7 +994,44 @@ void mcs_extractor_destroy(mcs_extractor* h) {
                   h->d_mask_pyr, h->d_mask_single, h->d_in, h->d_kps, h->d_desc, h->d_count};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (h->ev) {
+    for (int i = 0; i < mcs_extractor::kRing * (MCS_EXTRACTOR_NSTAGES + 1); i++)
+      (void)hipEventDestroy(h->ev[i]);
+    delete[] h->ev;
+  }
   delete h;
+}
+
+int mcs_extractor_enable_timing(mcs_extractor* h, int32_t enable) {
+  if (!h) return MCS_ERR_ARG;
+  MCS_HIP_CHECK(hipSetDevice(h->device));
+  if (enable && !h->ev) {
+    const int n = mcs_extractor::kRing * (MCS_EXTRACTOR_NSTAGES + 1);
+    h->ev = new hipEvent_t[n];
+    for (int i = 0; i < n; i++) MCS_HIP_CHECK(hipEventCreate(&h->ev[i]));
+  }
+  h->timing = enable != 0;
+  h->ev_count = 0;
+  return MCS_OK;
+}
+
+int mcs_extractor_read_timing(mcs_extractor* h, float* ms_per_stage, int32_t* ncalls,
+                              int32_t reset) {
+  if (!h || !ms_per_stage) return MCS_ERR_ARG;
+  MCS_HIP_CHECK(hipSetDevice(h->device));
+  for (int s = 0; s < MCS_EXTRACTOR_NSTAGES; s++) ms_per_stage[s] = 0.f;
+  const int K = MCS_EXTRACTOR_NSTAGES + 1;
+  for (int c = 0; c < h->ev_count; c++) {
+    MCS_HIP_CHECK(hipEventSynchronize(h->ev[c * K + K - 1]));
+    for (int s = 0; s < MCS_EXTRACTOR_NSTAGES; s++) {
+      float ms = 0.f;
+      MCS_HIP_CHECK(hipEventElapsedTime(&ms, h->ev[c * K + s], h->ev[c * K + s + 1]));
+      ms_per_stage[s] += ms;
+    }
+  }
+  if (ncalls) *ncalls = h->ev_count;
+  if (reset) h->ev_count = 0;
+  return MCS_OK;
 }
 
 int32_t mcs_extractor_capacity(const mcs_extractor* h) { return h ? h->plan.sel_per_frame : 0; }

@@ -76,6 +76,8 @@ SIGNATURES = {
     "mcs_extractor_set_masks_device": (ctypes.c_int, [_P, _P, _I32, _P]),
     "mcs_extract_batch_device": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_extractor_read_stage": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _I64, _P]),
+    "mcs_extractor_enable_timing": (ctypes.c_int, [_P, _I32]),
+    "mcs_extractor_read_timing": (ctypes.c_int, [_P, _P, _P, _I32]),
     # matcher (include/mcs_matcher.h)
     "mcs_descriptor_distance64": (ctypes.c_int, [_P, _P, _I32]),
     "mcs_descriptor_distance64_masked": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
@@ -182,6 +184,18 @@ class Extractor:
         """Device pointers (ints) in, device pointers out; async on `stream`."""
         _check(lib().mcs_extract_batch_device(self._h, d_images, int(n_frames), d_mask_index,
                                               d_kps, d_counts, d_desc, stream))
+
+    STAGES = ("pyramid", "blur", "fast", "octree", "orient_desc")
+
+    def enable_timing(self, on=True):
+        _check(lib().mcs_extractor_enable_timing(self._h, 1 if on else 0))
+
+    def read_timing(self, reset=True):
+        """-> (dict stage -> summed device ms, number of recorded batch calls)."""
+        ms = np.zeros(len(self.STAGES), np.float32)
+        n = ctypes.c_int32()
+        _check(lib().mcs_extractor_read_timing(self._h, _ptr(ms), ctypes.byref(n), 1 if reset else 0))
+        return dict(zip(self.STAGES, ms.tolist())), n.value
 
     def read_stage(self, stage, frame, level):
         wh, _ = self.levels()

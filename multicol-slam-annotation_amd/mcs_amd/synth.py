@@ -21,6 +21,25 @@ LAFIDA_CAMS = [
          pol=[293.667187375663, 149.982043337335, -10.448650568161, 28.2295300683376,
               7.13365723186292, 0.056303218962532, 10.4144677485333, 0.166354960773665,
               -5.86858687381081, 1.18165998645705, 3.1108311354746, 0.810799620714366]),
+    dict(Iw=754, Ih=480, c=1.00025900216253, d=-0.0123492665428806, e=0.012594227848688,
+         u0=378.722262294544, v0=253.62515782861,
+         a=[-209.071570423477, 0.0, 0.00216428966944475, -4.82076123755912e-06, 1.91902225328321e-08],
+         pol=[294.569975726124, 148.608451179358, -12.8584962393538, 28.8889327437629,
+              6.33883105861485, -0.89043629163529, 12.3786448516946, 0.165754338732521,
+              -7.71927140996498, 0.995360127219927, 3.74959014924028, 1.01240838118284]),
+    dict(Iw=754, Ih=480, c=0.99992772614797, d=0.0334716840387143, e=-0.0332451389561491,
+         u0=372.796912405235, v0=225.645071214684,
+         a=[-208.409533164304, 0.0, 0.00225243935068085, -5.55430532694086e-06, 2.07875001352451e-08],
+         pol=[293.775776115273, 147.35852428463, -14.3964307215767, 29.078338589251,
+              6.03461468718202, -2.07410652721192, 13.4359111214281, 0.984397095348803,
+              -8.64924421339311, 0.491570292475276, 3.92296807229949, 1.10563269391099]),
+]
+
+# Examples/Lafida/MultiCamSys_Calibration.yaml: M_c of each camera as Cayley (r1,r2,r3,t1,t2,t3)
+LAFIDA_MC = [
+    [-0.0238361786473007, -2.05998171167958, 0.695126790868671, -0.140202124607334, 0.0219677971160655, -0.0226322662838432],
+    [-0.0103943566650926, 1.12505249943085, -0.402901183146028, 0.108753418890423, 0.0636197216520153, 0.0657911760105832],
+    [0.0, 0.0, 0.0, -0.00157612288268783, 0.103615531247527, 0.201416323496156],
 ]
 
 
@@ -128,7 +147,8 @@ def _panorama(rng, W=2048, H=1024):
 _PANO_CACHE = {}
 
 
-def fisheye_frame(width=754, height=480, seed=0, cam_index=0, yaw=0.0, cam=None, noise=2.0):
+def fisheye_frame(width=754, height=480, seed=0, cam_index=0, yaw=0.0, cam=None, noise=2.0,
+                  noise_seed=None):
     """Render one synthetic 8-bit fisheye frame and its mirror mask."""
     cams = LAFIDA_CAMS
     if cam is None:
@@ -160,11 +180,27 @@ def fisheye_frame(width=754, height=480, seed=0, cam_index=0, yaw=0.0, cam=None,
     fy = py - y0
     val = (pano[y0, x0] * (1 - fx) + pano[y0, x1] * fx) * (1 - fy) + \
           (pano[y1, x0] * (1 - fx) + pano[y1, x1] * fx) * fy
-    val = val + rng.normal(0, noise, val.shape)
+    nrng = rng if noise_seed is None else np.random.default_rng(noise_seed)
+    val = val + nrng.normal(0, noise, val.shape)
     img = np.clip(np.rint(val), 0, 255).astype(np.uint8)
     mask = mirror_mask(cam)
     img[mask == 0] = 0
     return img, mask
+
+
+def rig_sequence(n_multiframes, width=754, height=480, ncams=3, seed=0, yaw_step=0.015):
+    """A moving multi-camera rig: frame (t, c) rotates camera c's view by t*yaw_step.
+    Returns images [n_multiframes*ncams, H, W] (t-major, camera-minor, like the
+    cMultiFrame camera concatenation) and masks [ncams, H, W]."""
+    imgs = np.zeros((n_multiframes * ncams, height, width), np.uint8)
+    masks = np.zeros((ncams, height, width), np.uint8)
+    for t in range(n_multiframes):
+        for c in range(ncams):
+            img, m = fisheye_frame(width, height, seed=seed * 100 + c, cam_index=c,
+                                   yaw=t * yaw_step, noise_seed=seed * 100000 + t * 16 + c)
+            imgs[t * ncams + c] = img
+            masks[c] = m
+    return imgs, masks
 
 
 def random_frame(width, height, seed):
