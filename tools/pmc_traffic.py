@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; collected in SEPARATE runs as
+MI355X_MICROARCH.md prescribes) into HBM bytes per kernel launch.
+
+Units/corrections (MI355X_MICROARCH.md "HBM"): both counters are in KiB.  On gfx950
+FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced stream, so the corrected
+read bytes are 2 * FETCH_SIZE * 1024; for other access widths the factor is uncalibrated,
+so both the raw and the x2-corrected figures are recorded.  WRITE_SIZE * 1024 is exact for
+16 B/lane stores.
+
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            name = row["Kernel_Name"]
+            per[name].append(float(row["Counter_Value"]))
+    return per
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("mcs::", "")
+
+
+def main(fetch_csv, write_csv, out_json):
+    fe = load(fetch_csv, "FETCH_SIZE")
+    wr = load(write_csv, "WRITE_SIZE")
+    out = {"note": "bytes per launch; fetch_raw = FETCH_SIZE*1024, fetch_x2 = gfx950 wide-read "
+                   "correction (exact only for 16B/lane streams); write = WRITE_SIZE*1024",
+           "kernels": {}}
+    for name in sorted(set(fe) | set(wr)):
+        f = fe.get(name, [])
+        w = wr.get(name, [])
+        out["kernels"][short(name)] = {
+            "launches": max(len(f), len(w)),
+            "fetch_raw": (sum(f) / len(f) * 1024) if f else None,
+            "fetch_x2": (2 * sum(f) / len(f) * 1024) if f else None,
+            "write": (sum(w) / len(w) * 1024) if w else None,
+        }
+    k = out["kernels"]
+    # per extractor call: 7 resize launches (one per level 1..7) + 1 FAST launch
+    rs = k.get("k_resize_linear")
+    fa = k.get("k_fast_cells")
+    if rs and fa:
+        nres = 7
+        rd = rs["fetch_raw"] * nres + fa["fetch_raw"]
+        rd2 = rs["fetch_x2"] * nres + fa["fetch_x2"]
+        wt = rs["write"] * nres + (fa["write"] or 0)
+        out["pyramid+fast_bytes_per_call"] = rd + wt
+        out["pyramid+fast_bytes_per_call_x2read"] = rd2 + wt
+    json.dump(out, open(out_json, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
