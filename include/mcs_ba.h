@@ -1,0 +1,100 @@
+/*
+ * mcs_ba.h -- C-ABI drop-in boundary for the MultiCol bundle adjustment.
+ *
+ * Replaces (billamiable/MultiCol-SLAM-Annotation):
+ *   cOptimizer::LocalBundleAdjustment(pKF, pMap, nrIters, getCovMats, pbStopFlag)
+ *       include/cOptimizer.h:61-65, src/cOptimizer.cpp:489-908   -> mcs_local_ba
+ *   g2o::SparseOptimizer::initializeOptimization(0) + optimize(n) with
+ *       OptimizationAlgorithmLevenberg + BlockSolver_6_3 + LinearSolverEigen and a
+ *       SparseOptimizerTerminateAction        ThirdParty/g2o/g2o/core/*       -> mcs_ba_optimize
+ *   EdgeProjectXYZ2MCS::computeError / linearizeOplus (+ mcsJacs1), VertexMt_cayley,
+ *       VertexPointXYZ, VertexMc_cayley, VertexOmniCameraParameters
+ *       include/g2o_MultiCol_vertices_edges.h:42-216, src/g2o_MultiCol_vertices_edges.cpp
+ *
+ * The host keeps the map traversal that builds the problem (local / fixed keyframe
+ * selection, one edge per observation, :503-769) and the write-back (:859-903); this ABI
+ * takes the resulting graph as flat SoA arrays.  Mc and IO vertices are fixed, as in
+ * LocalBundleAdjustment (:636-664).  All doubles.  Status codes as mcs_common.h.
+ */
+#ifndef MCS_BA_H
+#define MCS_BA_H
+
+#include <stdint.h>
+#include "mcs_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mcs_ba_problem {
+  int32_t n_poses, n_points, n_edges, n_cams;
+  const double* poses;        /* [n_poses][6] M_t as (r1,r2,r3,t1,t2,t3): Cayley + t, body->world */
+  const uint8_t* pose_fixed;  /* [n_poses] 1 = fixed vertex */
+  const double* points;       /* [n_points][3] world coordinates (marginalised vertices) */
+  const double* mc;           /* [n_cams][6] M_c camera->body (Cayley + t), fixed */
+  const double* cam;          /* [n_cams][17] c,d,e,u0,v0,invP[0..11] (VertexOmniCameraParameters) */
+  const int32_t* edge_pose;   /* [n_edges] vertex 0 (Mt) */
+  const int32_t* edge_point;  /* [n_edges] vertex 1 (point) */
+  const int32_t* edge_cam;    /* [n_edges] vertices 2/3 (Mc, IO) */
+  const double* edge_meas;    /* [n_edges][2] measured (distorted) pixel, kp.pt */
+  const double* edge_info;    /* [n_edges] information = edge_info * I2 (invSigma2(octave)) */
+  double huber_delta;         /* RobustKernelHuber delta: 1.345*2 (LocalBA), sqrt(5.991) (global) */
+} mcs_ba_problem;
+
+typedef struct mcs_ba_options {
+  int32_t max_iterations;       /* optimize(n): 10 (LocalBA round 1), 15 (round 2) */
+  double gain_threshold;        /* SparseOptimizerTerminateAction gain threshold: 1e-6 */
+  int32_t terminate_max_iter;   /* SparseOptimizerTerminateAction max iterations: 15 */
+  int32_t max_trials;           /* LM maxTrialsAfterFailure: 10 */
+  double tau;                   /* LM lambda init factor: 1e-5 */
+} mcs_ba_options;
+
+typedef struct mcs_ba_report {
+  int32_t iterations;           /* optimize() return value (iterations run) */
+  int32_t stop_flag;            /* value of the (caller's or auxiliary) stop flag afterwards */
+  double chi2_initial;          /* robust chi2 before the first iteration */
+  double chi2_final;            /* robust chi2 at the final estimate */
+  double lambda_final;
+  int32_t n_active_edges;
+  int32_t n_active_poses;       /* non-fixed poses with >= 1 active edge */
+  int32_t n_active_points;
+  double* trace_chi2;           /* nullable [trace_cap]: robust chi2 after each iteration */
+  int32_t trace_cap;
+} mcs_ba_report;
+
+typedef struct mcs_ba_ctx mcs_ba_ctx;
+
+void mcs_ba_default_options(mcs_ba_options* o);
+/* Device context sized for problems up to the given counts (grown on demand). */
+int mcs_ba_create(int32_t device, mcs_ba_ctx** out);
+void mcs_ba_destroy(mcs_ba_ctx* c);
+
+/* One initializeOptimization(0) + optimize(max_iterations) on the GPU.
+ * poses/points: in/out (n_poses*6 / n_points*3 doubles), updated in place.
+ * edge_level: in [n_edges], 0 = active edge (level 0), nonzero = disabled (level 1).
+ * edge_chi2: out (nullable) unrobust chi2 e^T*Omega*e of every edge at the final estimate.
+ * stop_flag: the caller's force-stop flag (nullable, like pbStopFlag); polled between LM
+ * trials and written by the terminate action exactly as g2o does
+ * (sparse_optimizer_terminate_action.cpp:21-72). */
+int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o,
+                    double* poses, double* points, const uint8_t* edge_level,
+                    double* edge_chi2, volatile int32_t* stop_flag, mcs_ba_report* rep);
+
+/* cOptimizer::LocalBundleAdjustment after graph construction (src/cOptimizer.cpp:771-903):
+ * round 1 optimize(10); if the stop flag is set afterwards -> return (no write-back);
+ * else disable edges with chi2 > delta^2, round 2 optimize(15), cull again.
+ * Outputs: poses/points (in/out; only meaningful when *write_back == 1), edge_inlier[n_edges]
+ * (0 = observation erased), write_back (bDoMore of the reference), reports of both rounds. */
+int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* points,
+                 uint8_t* edge_inlier, int32_t* write_back, volatile int32_t* stop_flag,
+                 mcs_ba_report* rep_round1, mcs_ba_report* rep_round2);
+
+/* Per-edge error and Jacobians (vertex order Mt, point) at the given estimate, for tests:
+ * err [n][2], jac_pose [n][2][6], jac_point [n][2][3] (g2o sign: d(meas - proj)/d(param)). */
+int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double* jac_pose,
+                     double* jac_point);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCS_BA_H */

@@ -1,0 +1,90 @@
+// Kernel argument blocks and launch wrappers of the extractor pipeline (one .hip file per
+// stage; the host orchestration lives in extractor.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "extractor_plan.hpp"
+
+namespace mcs {
+
+// Workgroup -> (frame, item) mapping that keeps all workgroups of one frame on one XCD
+// (dispatch deals workgroups round-robin over the 8 XCDs; speed only, never correctness).
+// Grid = 8 * ceil(F/8) * items_per_frame workgroups; returns false for padding groups.
+__device__ __forceinline__ bool xcd_frame_map(int b, int F, int items, int* frame, int* item) {
+  const int x = b & 7, k = b >> 3;
+  const int f = x + 8 * (k / items);
+  *item = k % items;
+  *frame = f;
+  return f < F;
+}
+inline unsigned xcd_grid(int F, int items) { return (unsigned)(8 * ((F + 7) / 8) * items); }
+
+struct LevelPtrs {
+  int32_t w[kMaxLevels], h[kMaxLevels], pitch[kMaxLevels], bpitch[kMaxLevels];
+  int64_t pyr_off[kMaxLevels], img_off[kMaxLevels], mask_off[kMaxLevels];
+};
+
+// ---- K1+K5 fused: resize level l-1 -> l (or take level 0) + 5x5 blur of the level
+struct PyrArgs {
+  const uint8_t* src; int64_t src_fstride; int sw, sh, spitch;  // level l-1 (or level 0)
+  uint8_t* dst; int64_t dst_fstride; int dpitch;                // level l raw (RESIZE only)
+  uint8_t* blur; int64_t blur_fstride; int bpitch;              // level l blurred
+  int dw, dh;
+  const int32_t* xofs; const int16_t* alpha; const int32_t* yofs; const int16_t* beta;
+  int simd_end;
+  int tiles_x, tiles_y, nframes;
+};
+void launch_pyr_blur(const PyrArgs& a, bool resize, hipStream_t st);
+
+void launch_mask_pyramids(const Plan& pl, const uint8_t* d_masks, int n, uint8_t* dst,
+                          hipStream_t st);
+// flags[m][cell] = any(mask level pixel != 0 inside the cell's detection window)
+void launch_cell_maskflags(const Plan& pl, const CellDesc* d_cells, const uint8_t* mask_pyr,
+                           int n_masks, uint8_t* flags, hipStream_t st);
+
+// ---- K2: FAST cells
+struct FastArgs {
+  const uint8_t* img0; int64_t img0_fstride;
+  const uint8_t* pyr; int64_t pyr_fstride;
+  const uint8_t* mask_pyr; int64_t mask_fstride;
+  const uint8_t* cell_flags;                     // [mask][cell] (nullable)
+  const int32_t* mask_index;
+  const CellDesc* cells; int ncells;
+  uint32_t* slots; int64_t slots_fstride;
+  int32_t* cell_counts;
+  int threshold;
+  int nframes;
+  LevelPtrs lp;
+};
+void launch_fast_cells(const FastArgs& a, hipStream_t st);
+
+// ---- K3: octree
+struct OctArgs {
+  LevelPlan lv[kMaxLevels];
+  const CellDesc* cells;
+  const int32_t* cell_counts; int ncells;
+  const uint32_t* slots; int64_t slots_fstride;
+  uint32_t* cand; int32_t* cnode; int64_t cand_fstride;
+  uint32_t* sel; int64_t sel_fstride;
+  int32_t* sel_count; int nlevels;
+  int32_t* frame_count;
+  int nframes;
+};
+void launch_octree(const OctArgs& a, int max_list, hipStream_t st);
+
+// ---- K4+K6: orientation + descriptors
+struct DescArgs {
+  LevelPlan lv[kMaxLevels];
+  int nlevels;
+  const uint8_t* img0; int64_t img0_fstride;
+  const uint8_t* pyr; int64_t pyr_fstride;
+  const uint8_t* blur; int64_t blur_fstride;
+  const uint32_t* sel; int64_t sel_fstride; int sel_per_frame;
+  const int32_t* sel_count;
+  mcs_keypoint* kps; uint8_t* desc; int cap; int desc_size;
+  int nframes;
+};
+void launch_orient_desc(const DescArgs& a, hipStream_t st);
+int upload_desc_constants();
+
+}  // namespace mcs

@@ -77,7 +77,8 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     nfl[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
   }
 
-  int64_t pyr_off = 0, img_off = 0;
+  int64_t pyr_off = 0, img_off = 0, mask_off = 0;
+  auto align = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
   int32_t slot = 0, sel = 0;
   pl.cells.clear(); pl.xofs.clear(); pl.yofs.clear(); pl.alpha.clear(); pl.beta.clear();
   pl.xtab_off.assign(p.nlevels, 0); pl.ytab_off.assign(p.nlevels, 0);
@@ -90,10 +91,14 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
       set_error("level too large for 12-bit candidate packing");
       return MCS_ERR_UNSUPPORTED;
     }
+    L.bpitch = (int32_t)align(L.w, 64);
+    L.pitch = (l == 0) ? W : L.bpitch;
     L.pyr_off = (l == 0) ? 0 : pyr_off;
-    if (l > 0) pyr_off += (int64_t)L.w * L.h;
+    if (l > 0) pyr_off = align(pyr_off + (int64_t)L.pitch * L.h, 256);
     L.img_off = img_off;
-    img_off += (int64_t)L.w * L.h;
+    img_off = align(img_off + (int64_t)L.bpitch * L.h, 256);
+    L.mask_off = mask_off;
+    mask_off += (int64_t)L.w * L.h;
     L.nfeat = nfl[l];
     L.scale = (float)sf[l];
     L.patch_size_scaled = (int)(kPatchSize * sf[l]);
@@ -177,6 +182,7 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
   }
   pl.pyr_frame_bytes = pyr_off;
   pl.img_frame_bytes = img_off;
+  pl.mask_frame_bytes = mask_off;
   pl.slots_per_frame = slot;
   pl.cand_per_frame = slot;
   pl.sel_per_frame = sel;

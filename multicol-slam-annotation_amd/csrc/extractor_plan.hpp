@@ -15,8 +15,9 @@ constexpr int kMinBorder = kEdgeThreshold - 3; // :876
 constexpr int kPatchSize = 32;                 // :84
 constexpr int kHalfPatch = 16;                 // :85
 constexpr int kMaxCellDim = 64;                // window bound per FAST cell (host-checked)
-constexpr int kMaxCellsPerLevel = 4096;        // LDS prefix table in the octree kernel
+constexpr int kMaxCellsPerLevel = 2048;        // LDS prefix table in the octree kernel
 constexpr int kOctMaxL = 1024;                 // octree node-list bound (host-checked)
+constexpr double kMaxScaleFactor = 2.2;        // pyramid source-tile bound (k_pyramid.hip)
 
 // One FAST cell of ComputeKeyPointsOctTree (:892-948): the detection window is the
 // cell ROI shrunk by 3 px (FAST_t rows/cols [3, n-3)), absolute level coordinates.
@@ -29,8 +30,12 @@ struct CellDesc {
 
 struct LevelPlan {
   int32_t w, h;               // level size (cvRound(W / 1.2^l))
+  int32_t pitch;              // row pitch of raw level l (level 0: the input width) and of
+                              // the blurred level (all levels: align64(w))
+  int32_t bpitch;
   int64_t pyr_off;            // offset of the level inside a frame's pyramid workspace (l >= 1)
-  int64_t img_off;            // offset inside a frame's blurred / mask-pyramid workspace
+  int64_t img_off;            // offset inside a frame's blurred-level workspace (pitch bpitch)
+  int64_t mask_off;           // offset inside a mask pyramid (pitch w, unpadded)
   int32_t cell_begin, cell_end;
   int32_t cand_off, cand_cap; // candidate gather area within a frame (sum of cell caps)
   int32_t sel_off, sel_cap;   // octree output area within a frame
@@ -50,7 +55,8 @@ struct Plan {
   LevelPlan lv[kMaxLevels];
   std::vector<CellDesc> cells;
   int64_t pyr_frame_bytes = 0;   // levels 1..L-1
-  int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred / mask pyramids)
+  int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred levels, padded pitch)
+  int64_t mask_frame_bytes = 0;  // levels 0..L-1 (mask pyramid, unpadded)
   int32_t slots_per_frame = 0;   // sum of cell caps
   int32_t cand_per_frame = 0;    // == slots_per_frame
   int32_t sel_per_frame = 0;     // sum of level sel caps == mcs_extractor_capacity

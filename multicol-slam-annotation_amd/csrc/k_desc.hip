@@ -1,0 +1,161 @@
+// K4 + K6: intensity-centroid orientation (unblurred level) and rotated BRIEF (blurred
+// level), one wave per keypoint; all keypoints of a frame run on one XCD so the frame's
+// level images stay in that XCD's L2.
+//
+// Reference: IC_Angle src/mdBRIEFextractorOct.cpp:221-248 (+ fastAtan2),
+// compute_ORB / rotatePattern :285-354, keypoint finalisation :959-970,
+// :1326-1335.  Compiled with -ffp-contract=off; the float/double ops below are additionally
+// spelled with _rn intrinsics so no FMA contraction can change a rounding.
+#include "common.hpp"
+#include "extractor_kernels.hpp"
+
+namespace mcs {
+
+__constant__ int c_pattern[2048] = {
+#include "pattern_orb64.inc"
+};
+// IC_Angle patch: 33x33 square scanned as 18 slots of 64 lanes; entry = (u+16) | (v+16)<<8
+// | inside<<16 (inside <=> |u| <= umax[|v|], the circular r=16 patch of the reference)
+__constant__ int c_icpatch[18 * 64];
+
+int upload_desc_constants() {
+  int umax[kHalfPatch + 1];
+  int v, v0, vmax = (int)std::floor(kHalfPatch * std::sqrt(2.f) / 2 + 1);  // ctor :187-202
+  int vmin = (int)std::ceil(kHalfPatch * std::sqrt(2.f) / 2);
+  const double hp2 = kHalfPatch * kHalfPatch;
+  for (v = 0; v <= vmax; ++v) umax[v] = cv_round(std::sqrt(hp2 - v * v));
+  for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+  int tab[18 * 64];
+  for (int i = 0; i < 18 * 64; i++) {
+    if (i >= 33 * 33) { tab[i] = 16 | (16 << 8); continue; }  // centre, weight 0 (outside)
+    const int vv = i / 33 - kHalfPatch, uu = i % 33 - kHalfPatch;
+    const bool in = std::abs(uu) <= umax[std::abs(vv)];
+    tab[i] = (uu + 16) | ((vv + 16) << 8) | ((in ? 1 : 0) << 16);
+  }
+  MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_icpatch), tab, sizeof(tab)));
+  return MCS_OK;
+}
+
+__device__ __forceinline__ float fast_atan2_dev(float y, float x) {
+  // OpenCV fastAtan2
+  const float k = (float)(180 / 3.14159265358979323846);
+  const float p1 = __fmul_rn(0.9997878412794807f, k), p3 = __fmul_rn(-0.3258083974640975f, k);
+  const float p5 = __fmul_rn(0.1555786518463281f, k), p7 = __fmul_rn(-0.04432655554792128f, k);
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  const float eps = (float)2.220446049250313080847e-16;
+  if (ax >= ay) {
+    c = __fdiv_rn(ay, __fadd_rn(ax, eps));
+    c2 = __fmul_rn(c, c);
+    a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+  } else {
+    c = __fdiv_rn(ax, __fadd_rn(ay, eps));
+    c2 = __fmul_rn(c, c);
+    a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+  }
+  if (x < 0) a = __fsub_rn(180.f, a);
+  if (y < 0) a = __fsub_rn(360.f, a);
+  return a;
+}
+
+__device__ __forceinline__ int rot_round(double px, double py, double ca, double sa, bool xaxis) {
+  // cvRound(x*cos - y*sin) / cvRound(x*sin + y*cos), double, round-half-even
+  return xaxis ? (int)rint(__dsub_rn(__dmul_rn(px, ca), __dmul_rn(py, sa)))
+               : (int)rint(__dadd_rn(__dmul_rn(px, sa), __dmul_rn(py, ca)));
+}
+
+__global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
+  const int lane = threadIdx.x & 63;
+  int f, item;
+  const int chunks = (a.sel_per_frame + 3) / 4;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, chunks, &f, &item)) return;
+  const int j = item * 4 + (threadIdx.x >> 6);
+  if (j >= a.sel_per_frame) return;
+  int l = 0;
+  while (l + 1 < a.nlevels && j >= a.lv[l + 1].sel_off) l++;
+  const LevelPlan& L = a.lv[l];
+  const int i = j - L.sel_off;
+  const int32_t* scount = a.sel_count + (int64_t)f * a.nlevels;
+  if (i >= scount[l]) return;
+  int outIdx = i;
+  for (int t = 0; t < l; t++) outIdx += scount[t];
+  const uint32_t pk = a.sel[(int64_t)f * a.sel_fstride + j];
+  const int cx = (int)(pk & 0xFFF) + kMinBorder, cy = (int)((pk >> 12) & 0xFFF) + kMinBorder;
+  const int score = (int)(pk >> 24);
+  const int pitch = L.pitch;
+  const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
+                                : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
+  const uint8_t* ctr = img + (int64_t)cy * pitch + cx;
+  // ---- IC_Angle: 18 independent byte gathers per lane, integer moments
+  int m10 = 0, m01 = 0;
+  {
+    int e[18], I[18];
+#pragma unroll
+    for (int t = 0; t < 18; t++) e[t] = c_icpatch[t * 64 + lane];
+#pragma unroll
+    for (int t = 0; t < 18; t++) {
+      const int u = (e[t] & 0xFF) - 16, v = ((e[t] >> 8) & 0xFF) - 16;
+      I[t] = ctr[(int64_t)v * pitch + u];
+    }
+#pragma unroll
+    for (int t = 0; t < 18; t++) {
+      const int u = (e[t] & 0xFF) - 16, v = ((e[t] >> 8) & 0xFF) - 16;
+      const int w = (e[t] >> 16) & 1;
+      m10 += w * u * I[t];
+      m01 += w * v * I[t];
+    }
+  }
+  m10 = dev::wave_sum(m10);
+  m01 = dev::wave_sum(m01);
+  const float angle = fast_atan2_dev((float)m01, (float)m10);
+  // ---- rotated BRIEF on the blurred level
+  const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
+  const double theta = (double)__fmul_rn(angle, DEG2RADf);
+  const double ca = cos(theta), sa = sin(theta);
+  const int bp = L.bpitch;
+  const uint8_t* bc = a.blur + (int64_t)f * a.blur_fstride + L.img_off + (int64_t)cy * bp + cx;
+  const int nwords = a.desc_size / 8;
+  uint8_t* dptr = a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size;
+  uint64_t words[8];
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    if (r < nwords) {
+      const int t = r * 64 + lane;  // test t: byte t/8, bit t%8
+      const double px0 = c_pattern[4 * t], py0 = c_pattern[4 * t + 1];
+      const double px1 = c_pattern[4 * t + 2], py1 = c_pattern[4 * t + 3];
+      const int o0 = rot_round(px0, py0, ca, sa, false) * bp + rot_round(px0, py0, ca, sa, true);
+      const int o1 = rot_round(px1, py1, ca, sa, false) * bp + rot_round(px1, py1, ca, sa, true);
+      const int t0 = bc[o0], t1 = bc[o1];
+      words[r] = __ballot(t0 < t1);
+    }
+  }
+  if (lane < nwords) {
+    uint64_t w = words[0];
+#pragma unroll
+    for (int r = 1; r < 8; r++)
+      if (lane == r) w = words[r];
+    reinterpret_cast<uint64_t*>(dptr)[lane] = w;
+  }
+  if (lane == 0) {
+    mcs_keypoint kp;
+    kp.x = (float)cx; kp.y = (float)cy;
+    if (l != 0) { kp.x = __fmul_rn((float)cx, L.scale); kp.y = __fmul_rn((float)cy, L.scale); }
+    kp.size = (float)L.patch_size_scaled;
+    kp.angle = angle;
+    kp.response = (float)score;
+    kp.octave = l;
+    kp.class_id = -1;
+    a.kps[(int64_t)f * a.cap + outIdx] = kp;
+  }
+}
+
+void launch_orient_desc(const DescArgs& a, hipStream_t st) {
+  const unsigned g = xcd_grid(a.nframes, (a.sel_per_frame + 3) / 4);
+  hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(256), 0, st, a);
+}
+
+}  // namespace mcs

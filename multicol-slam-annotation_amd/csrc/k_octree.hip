@@ -1,0 +1,384 @@
+// K3: DistributeOctTree (src/mdBRIEFextractorOct.cpp:569-861) as an order-exact,
+// data-parallel emulation: one 256-thread workgroup per (frame, level); node lists in LDS
+// (ping-pong), candidates + their current node in global memory (L2-resident).
+#include "common.hpp"
+#include "extractor_kernels.hpp"
+
+namespace mcs {
+
+// ===========================================================================
+// K3: DistributeOctTree as a data-parallel, order-exact emulation, one workgroup per
+// (frame, level).  See DESIGN.md "octree".  The std::list order of the reference is
+// reproduced exactly: children are pushed to the front in (node order, n1..n4) order,
+// untouched nodes keep their relative order; final-phase node choice follows
+// sort(size, pointer) with pointer order pinned to creation order.
+// ===========================================================================
+
+constexpr int kOctThreads = 256;
+
+__device__ __forceinline__ int oct_quad(uint32_t pk, int midx, int midy) {
+  const int x = pk & 0xFFF, y = (pk >> 12) & 0xFFF;
+  return (x >= midx ? 1 : 0) + (y >= midy ? 2 : 0);
+}
+
+template <int MAXL>
+__global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
+  constexpr int kOctPer = MAXL / kOctThreads;  // nodes per thread in node scans
+  int f, l;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, a.nlevels, &f, &l)) return;
+  const int tid = threadIdx.x;
+  const LevelPlan& L = a.lv[l];
+  __shared__ int s_pref[kMaxCellsPerLevel];  // cell prefix; reused as sort keys
+  __shared__ int s_scan[kOctThreads / 64 + 1];
+  __shared__ int16_t nx0[2][MAXL], ny0[2][MAXL], nx1[2][MAXL], ny1[2][MAXL];
+  __shared__ int ncnt[2][MAXL], nseq[2][MAXL];
+  __shared__ int ccnt[MAXL * 4];  // child counts; reused for best keys
+  __shared__ int npos[MAXL * 4];  // new position per (node, child); kept uses slot 0
+  __shared__ int nflag[MAXL];     // expanding / in-E / processed flags
+  __shared__ int s_var[8];
+
+  uint32_t* cand = a.cand + (int64_t)f * a.cand_fstride + L.cand_off;
+  int32_t* cnode = a.cnode + (int64_t)f * a.cand_fstride + L.cand_off;
+  const uint32_t* slots = a.slots + (int64_t)f * a.slots_fstride;
+  const int32_t* counts = a.cell_counts + (int64_t)f * a.ncells + L.cell_begin;
+  const int nc = L.cell_end - L.cell_begin;
+  const int N = L.nfeat;
+
+  // ---- 1. gather candidates of this level in reference (cell, row, col) order
+  int n = 0;
+  for (int base = 0; base < nc; base += kOctThreads) {
+    const int i = base + tid;
+    const int v = i < nc ? counts[i] : 0;
+    int tot;
+    const int ex = dev::block_excl_scan<kOctThreads>(v, s_scan, &tot);
+    if (i < nc) s_pref[i] = n + ex;
+    n += tot;
+  }
+  __syncthreads();
+  {
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int c = wv; c < nc; c += kOctThreads / 64) {
+      const int cnt = counts[c];
+      const uint32_t* src = slots + a.cells[L.cell_begin + c].slot_off;
+      const int dst = s_pref[c];
+      for (int k = lane; k < cnt; k += 64) cand[dst + k] = src[k];
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. initial nodes (:650-683)
+  const int nIni = L.nini;
+  int cur = 0;
+  if (tid < nIni) {
+    nx0[0][tid] = (int16_t)(int)(L.hx * (double)tid);
+    nx1[0][tid] = (int16_t)(int)(L.hx * (double)(tid + 1));
+    ny0[0][tid] = 0;
+    ny1[0][tid] = (int16_t)L.height_rel;
+    ncnt[0][tid] = 0;
+    nseq[0][tid] = tid;
+  }
+  __syncthreads();
+  _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+    const int x = cand[k] & 0xFFF;
+    const int node = (int)((double)(float)x / L.hx);
+    cnode[k] = node;
+    atomicAdd(&ncnt[0][node], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {  // erase empty initial nodes, keep order
+    int m = 0;
+    for (int i = 0; i < nIni; i++) {
+      if (ncnt[0][i] > 0) {
+        nx0[1][m] = nx0[0][i]; ny0[1][m] = ny0[0][i]; nx1[1][m] = nx1[0][i]; ny1[1][m] = ny1[0][i];
+        ncnt[1][m] = ncnt[0][i]; nseq[1][m] = nseq[0][i];
+        npos[i] = m++;
+      }
+    }
+    s_var[0] = m;
+  }
+  __syncthreads();
+  _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) cnode[k] = npos[cnode[k]];
+  cur = 1;
+  int Lsz = s_var[0];
+  int seqc = nIni;
+  __syncthreads();
+
+  // ---- 3. main subdivision loop (:692-837)
+  bool finished = false;
+  int lastPushBase = 0;
+  while (true) {
+    const int prevSize = Lsz;
+    const int nxt = cur ^ 1;
+    for (int i = tid; i < Lsz; i += kOctThreads) {
+      nflag[i] = ncnt[cur][i] > 1;
+      ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
+    }
+    __syncthreads();
+    _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+      const int nd = cnode[k];
+      if (nflag[nd]) {
+        const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+        const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+        atomicAdd(&ccnt[4 * nd + oct_quad(cand[k], midx, midy)], 1);
+      }
+    }
+    __syncthreads();
+    // per thread: kOctPer consecutive nodes -> pushes (expanding) / kept
+    int pushes = 0, kept = 0, expandKids = 0;
+    const int i0 = tid * kOctPer;
+    for (int j = 0; j < kOctPer; j++) {
+      const int i = i0 + j;
+      if (i >= Lsz) break;
+      if (nflag[i]) {
+        for (int q = 0; q < 4; q++) {
+          const int cq = ccnt[4 * i + q];
+          pushes += cq > 0;
+          expandKids += cq > 1;
+        }
+      } else {
+        kept++;
+      }
+    }
+    int P, K, E2;
+    const int pushBase = dev::block_excl_scan<kOctThreads>(pushes, s_scan, &P);
+    const int keptBase = dev::block_excl_scan<kOctThreads>(kept, s_scan, &K);
+    dev::block_excl_scan<kOctThreads>(expandKids, s_scan, &E2);
+    {
+      int s = pushBase, kp = keptBase;
+      for (int j = 0; j < kOctPer; j++) {
+        const int i = i0 + j;
+        if (i >= Lsz) break;
+        if (nflag[i]) {
+          const int x0 = nx0[cur][i], y0 = ny0[cur][i], x1 = nx1[cur][i], y1 = ny1[cur][i];
+          const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+          for (int q = 0; q < 4; q++) {
+            const int cq = ccnt[4 * i + q];
+            if (cq == 0) continue;
+            const int pos = P - 1 - s;
+            npos[4 * i + q] = pos;
+            nx0[nxt][pos] = (int16_t)((q & 1) ? mx : x0);
+            nx1[nxt][pos] = (int16_t)((q & 1) ? x1 : mx);
+            ny0[nxt][pos] = (int16_t)((q & 2) ? my : y0);
+            ny1[nxt][pos] = (int16_t)((q & 2) ? y1 : my);
+            ncnt[nxt][pos] = cq;
+            nseq[nxt][pos] = seqc + s;
+            s++;
+          }
+        } else {
+          const int pos = P + kp;
+          npos[4 * i] = pos;
+          nx0[nxt][pos] = nx0[cur][i]; nx1[nxt][pos] = nx1[cur][i];
+          ny0[nxt][pos] = ny0[cur][i]; ny1[nxt][pos] = ny1[cur][i];
+          ncnt[nxt][pos] = ncnt[cur][i];
+          nseq[nxt][pos] = nseq[cur][i];
+          kp++;
+        }
+      }
+    }
+    __syncthreads();
+    _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+      const int nd = cnode[k];
+      if (nflag[nd]) {
+        const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+        const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+        cnode[k] = npos[4 * nd + oct_quad(cand[k], midx, midy)];
+      } else {
+        cnode[k] = npos[4 * nd];
+      }
+    }
+    lastPushBase = seqc;
+    seqc += P;
+    Lsz = P + K;
+    cur = nxt;
+    __syncthreads();
+    if (Lsz >= N || Lsz == prevSize) { finished = true; break; }
+    if (Lsz + 3 * E2 > N) break;  // -> final phase
+  }
+
+  // ---- 4. final phase (:771-836): divide largest nodes first until >= N
+  if (!finished) {
+    int roundBase = lastPushBase;
+    while (true) {
+      const int prevSize = Lsz;
+      const int nxt = cur ^ 1;
+      unsigned long long* keys = reinterpret_cast<unsigned long long*>(s_pref);  // 2048 x u64
+      // E = nodes created in the previous round with > 1 key
+      int inE = 0;
+      const int i0 = tid * kOctPer;
+      for (int j = 0; j < kOctPer; j++) {
+        const int i = i0 + j;
+        if (i < Lsz) inE += (nseq[cur][i] >= roundBase && ncnt[cur][i] > 1);
+      }
+      int M;
+      int eb = dev::block_excl_scan<kOctThreads>(inE, s_scan, &M);
+      int M2 = 1;
+      while (M2 < M) M2 <<= 1;
+      for (int j = 0; j < kOctPer; j++) {
+        const int i = i0 + j;
+        if (i < Lsz) {
+          const bool e = nseq[cur][i] >= roundBase && ncnt[cur][i] > 1;
+          nflag[i] = 0;
+          ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
+          if (e) {
+            keys[eb++] = ((unsigned long long)ncnt[cur][i] << 40) |
+                         ((unsigned long long)nseq[cur][i] << 12) | (unsigned long long)i;
+            nflag[i] = 1;
+          }
+        }
+      }
+      for (int i = M + tid; i < M2; i += kOctThreads) keys[i] = 0ull;
+      __syncthreads();
+      // bitonic sort, descending
+      for (int k = 2; k <= M2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < M2; i += kOctThreads) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const unsigned long long ki = keys[i], kj = keys[ixj];
+              const bool desc = (i & k) == 0;
+              if (desc ? (ki < kj) : (ki > kj)) { keys[i] = kj; keys[ixj] = ki; }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // child counts of E nodes
+      _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+        const int nd = cnode[k];
+        if (nflag[nd]) {
+          const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+          const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+          atomicAdd(&ccnt[4 * nd + oct_quad(cand[k], midx, midy)], 1);
+        }
+      }
+      __syncthreads();
+      // sorted position j -> delta (nonempty children - 1); processed prefix
+      int dsum = 0;
+      const int j0 = tid * kOctPer;  // M <= MAXL
+      int dl[kOctPer], kl[kOctPer];
+      for (int jj = 0; jj < kOctPer; jj++) {
+        const int j = j0 + jj;
+        dl[jj] = 0; kl[jj] = 0;
+        if (j < M) {
+          const int nd = (int)(keys[j] & 0xFFF);
+          int kids = 0;
+          for (int q = 0; q < 4; q++) kids += ccnt[4 * nd + q] > 0;
+          kl[jj] = kids;
+          dl[jj] = kids - 1;
+        }
+        dsum += dl[jj];
+      }
+      int Dtot;
+      int dpre = dev::block_excl_scan<kOctThreads>(dsum, s_scan, &Dtot);
+      // first j with Lsz + inclusive(delta) >= N -> processed = j+1
+      if (tid == 0) s_var[1] = M;
+      __syncthreads();
+      {
+        int run = dpre;
+        for (int jj = 0; jj < kOctPer; jj++) {
+          const int j = j0 + jj;
+          if (j >= M) break;
+          run += dl[jj];
+          if (Lsz + run >= N) { atomicMin(&s_var[1], j + 1); break; }
+        }
+      }
+      __syncthreads();
+      const int Mp = s_var[1];
+      // pushes of processed sorted nodes (in sorted order, children n1..n4)
+      int mykids = 0;
+      for (int jj = 0; jj < kOctPer; jj++)
+        if (j0 + jj < Mp) mykids += kl[jj];
+      int Pn;
+      int kbase = dev::block_excl_scan<kOctThreads>(mykids, s_scan, &Pn);
+      // mark processed (nflag = 2) and place children
+      {
+        int s = kbase;
+        for (int jj = 0; jj < kOctPer; jj++) {
+          const int j = j0 + jj;
+          if (j >= Mp) break;
+          const int nd = (int)(keys[j] & 0xFFF);
+          nflag[nd] = 2;
+          const int x0 = nx0[cur][nd], y0 = ny0[cur][nd], x1 = nx1[cur][nd], y1 = ny1[cur][nd];
+          const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+          for (int q = 0; q < 4; q++) {
+            const int cq = ccnt[4 * nd + q];
+            if (cq == 0) continue;
+            const int pos = Pn - 1 - s;
+            npos[4 * nd + q] = pos;
+            nx0[nxt][pos] = (int16_t)((q & 1) ? mx : x0);
+            nx1[nxt][pos] = (int16_t)((q & 1) ? x1 : mx);
+            ny0[nxt][pos] = (int16_t)((q & 2) ? my : y0);
+            ny1[nxt][pos] = (int16_t)((q & 2) ? y1 : my);
+            ncnt[nxt][pos] = cq;
+            nseq[nxt][pos] = seqc + s;
+            s++;
+          }
+        }
+      }
+      __syncthreads();
+      // remaining (unprocessed) list nodes keep their order after the pushes
+      int kept = 0;
+      for (int j = 0; j < kOctPer; j++) {
+        const int i = i0 + j;
+        if (i < Lsz && nflag[i] != 2) kept++;
+      }
+      int Kn;
+      int kb = dev::block_excl_scan<kOctThreads>(kept, s_scan, &Kn);
+      for (int j = 0; j < kOctPer; j++) {
+        const int i = i0 + j;
+        if (i < Lsz && nflag[i] != 2) {
+          const int pos = Pn + kb++;
+          npos[4 * i] = pos;
+          nx0[nxt][pos] = nx0[cur][i]; nx1[nxt][pos] = nx1[cur][i];
+          ny0[nxt][pos] = ny0[cur][i]; ny1[nxt][pos] = ny1[cur][i];
+          ncnt[nxt][pos] = ncnt[cur][i];
+          nseq[nxt][pos] = nseq[cur][i];
+        }
+      }
+      __syncthreads();
+      _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+        const int nd = cnode[k];
+        if (nflag[nd] == 2) {
+          const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+          const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+          cnode[k] = npos[4 * nd + oct_quad(cand[k], midx, midy)];
+        } else {
+          cnode[k] = npos[4 * nd];
+        }
+      }
+      roundBase = seqc;
+      seqc += Pn;
+      Lsz = Pn + Kn;
+      cur = nxt;
+      __syncthreads();
+      if (Lsz >= N || Lsz == prevSize) break;
+    }
+  }
+
+  // ---- 5. retain the best (first max) key per node, in list order (:839-858)
+  unsigned int* best = reinterpret_cast<unsigned int*>(ccnt);
+  for (int i = tid; i < Lsz; i += kOctThreads) best[i] = 0u;
+  __syncthreads();
+  _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+    const uint32_t pk = cand[k];
+    atomicMax(&best[cnode[k]], ((pk >> 24) << 24) | (0xFFFFFFu - (unsigned)k));
+  }
+  __syncthreads();
+  uint32_t* sel = a.sel + (int64_t)f * a.sel_fstride + L.sel_off;
+  for (int i = tid; i < Lsz; i += kOctThreads) sel[i] = cand[0xFFFFFFu - (best[i] & 0xFFFFFFu)];
+  if (tid == 0) {
+    a.sel_count[(int64_t)f * a.nlevels + l] = Lsz;
+    atomicAdd(&a.frame_count[f], Lsz);
+  }
+}
+
+
+void launch_octree(const OctArgs& a, int max_list, hipStream_t st) {
+  const unsigned g = xcd_grid(a.nframes, a.nlevels);
+  if (max_list <= 512)
+    hipLaunchKernelGGL(k_octree<512>, dim3(g), dim3(kOctThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_octree<1024>, dim3(g), dim3(kOctThreads), 0, st, a);
+}
+
+}  // namespace mcs

@@ -185,7 +185,7 @@ class Extractor:
         _check(lib().mcs_extract_batch_device(self._h, d_images, int(n_frames), d_mask_index,
                                               d_kps, d_counts, d_desc, stream))
 
-    STAGES = ("pyramid", "blur", "fast", "octree", "orient_desc")
+    STAGES = ("pyramid", "blur0", "fast", "octree", "orient_desc")
 
     def enable_timing(self, on=True):
         _check(lib().mcs_extractor_enable_timing(self._h, 1 if on else 0))

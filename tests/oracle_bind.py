@@ -162,3 +162,64 @@ def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, de
                               desc_size, mode, _p(kps), _p(desc), cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+# ---------------------------------------------------------------------------
+# bundle adjustment oracle
+# ---------------------------------------------------------------------------
+def _ba_sigs():
+    L = lib()
+    for n, a in (("oracle_ba_edge", [_P] * 8),
+                 ("oracle_ba_optimize", [_P] * 8),
+                 ("oracle_local_ba", [_P] * 8)):
+        f = getattr(L, n)
+        f.restype = _I
+        f.argtypes = a
+    return L
+
+
+def ba_edge(pose, X, mc, cam, meas):
+    L = _ba_sigs()
+    a = [np.ascontiguousarray(v, np.float64) for v in (pose, X, mc, cam, meas)]
+    err = np.zeros(2)
+    jp = np.zeros((2, 6))
+    jl = np.zeros((2, 3))
+    L.oracle_ba_edge(*[_p(v) for v in a], _p(err), _p(jp), _p(jl))
+    return err, jp, jl
+
+
+def ba_optimize(pr, options=None, edge_level=None, stop_flag=None, trace=0):
+    import ctypes as C
+    from mcs_amd import ba
+    L = _ba_sigs()
+    s = ba.as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    lvl = np.zeros(len(pr["edge_pose"]), np.uint8) if edge_level is None else \
+        np.ascontiguousarray(edge_level, np.uint8)
+    chi = np.zeros(len(pr["edge_pose"]))
+    o = options or ba.BAOptions()
+    tr = np.zeros(max(trace, 1))
+    rep = ba.BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(tr) if trace else None, trace)
+    sf = None if stop_flag is None else C.c_int32(int(stop_flag))
+    L.oracle_ba_optimize(C.byref(s), C.byref(o), _p(poses), _p(points), _p(lvl), _p(chi),
+                         C.byref(sf) if sf is not None else None, C.byref(rep))
+    return dict(poses=poses, points=points, edge_chi2=chi, report=rep,
+                stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
+
+
+def local_ba(pr, stop_flag=0):
+    import ctypes as C
+    from mcs_amd import ba
+    L = _ba_sigs()
+    s = ba.as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    inl = np.zeros(len(pr["edge_pose"]), np.uint8)
+    wb = C.c_int32()
+    sf = C.c_int32(int(stop_flag))
+    r1, r2 = ba.BAReport(), ba.BAReport()
+    L.oracle_local_ba(C.byref(s), _p(poses), _p(points), _p(inl), C.byref(wb), C.byref(sf),
+                      C.byref(r1), C.byref(r2))
+    return dict(poses=poses, points=points, edge_inlier=inl, write_back=wb.value,
+                stop_flag=sf.value, report1=r1, report2=r2)
