@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=12, help="multi-frames timed on the CPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-timing", type=int, default=1)
+    ap.add_argument("--ba-calls", type=int, default=5, help="timed LocalBA calls (config C)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -205,6 +206,39 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "alg_bytes_per_call": bpf * F}
 
+    # ---- LocalBA (config C): 10 local MultiKeyFrames + 3 fixed observers, 3k points, ~20k edges
+    localba = None
+    cpu_ba = None
+    if args.ba_calls > 0:
+        from mcs_amd import ba as mba
+        pr = mba.make_problem(seed=1 + rank)
+        solver = mba.Solver(device=local_rank)
+        solver.local_ba(pr)  # warm-up
+        t0 = time.perf_counter()
+        iters = 0
+        for _ in range(args.ba_calls):
+            r = solver.local_ba(pr)
+            iters += r["report1"].iterations + r["report2"].iterations
+        tba = time.perf_counter() - t0
+        it_rate = torch.tensor([iters / tba], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(it_rate, op=dist.ReduceOp.SUM)
+        localba = {"iters_per_s": round(float(it_rate.item()), 1),
+                   "calls_per_s_per_gpu": round(args.ba_calls / tba, 2),
+                   "ms_per_call": round(tba / args.ba_calls * 1e3, 3),
+                   "iterations_per_call": [r["report1"].iterations, r["report2"].iterations],
+                   "problem": "config C: %d poses (%d fixed), %d points, %d edges, 3 cams" % (
+                       len(pr["poses"]), int(pr["pose_fixed"].sum()), len(pr["points"]),
+                       len(pr["edge_pose"]))}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from tests import oracle_bind as ob
+            t0 = time.perf_counter()
+            o = ob.local_ba(pr)
+            tc = time.perf_counter() - t0
+            cpu_ba = {"value": round((o["report1"].iterations + o["report2"].iterations) / tc, 2),
+                      "unit": "LocalBA iters/s", "cores": 1, "kind": "port",
+                      "sample": "1 LocalBA call (config C), oracle restatement, single thread"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         S = min(args.cpu_sample, U)
@@ -234,6 +268,8 @@ def main():
                        "parallelism": "dp%d (independent multi-frame segments)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "localba": localba,
+            "cpu_baseline_localba": cpu_ba,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),
         }

@@ -6,7 +6,7 @@
  *       include/cOptimizer.h:61-65, src/cOptimizer.cpp:489-908   -> mcs_local_ba
  *   g2o::SparseOptimizer::initializeOptimization(0) + optimize(n) with
  *       OptimizationAlgorithmLevenberg + BlockSolver_6_3 + LinearSolverEigen and a
- *       SparseOptimizerTerminateAction        ThirdParty/g2o/g2o/core/*       -> mcs_ba_optimize
+ *       SparseOptimizerTerminateAction        (ThirdParty/g2o/g2o/core)        -> mcs_ba_optimize
  *   EdgeProjectXYZ2MCS::computeError / linearizeOplus (+ mcsJacs1), VertexMt_cayley,
  *       VertexPointXYZ, VertexMc_cayley, VertexOmniCameraParameters
  *       include/g2o_MultiCol_vertices_edges.h:42-216, src/g2o_MultiCol_vertices_edges.cpp

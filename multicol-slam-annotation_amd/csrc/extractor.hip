@@ -109,7 +109,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     }
     a.blur = h->d_blur + D.img_off; a.blur_fstride = pl.img_frame_bytes; a.bpitch = D.bpitch;
     a.dw = D.w; a.dh = D.h;
-    a.tiles_x = (D.w + 63) / 64; a.tiles_y = (D.h + 15) / 16;
+    a.tiles_x = (D.w + 123) / 124; a.tiles_y = (D.h + 15) / 16;
     a.nframes = F;
     return a;
   };

@@ -68,12 +68,29 @@ __device__ __forceinline__ int rot_round(double px, double py, double ca, double
                : (int)rint(__dadd_rn(__dmul_rn(px, sa), __dmul_rn(py, ca)));
 }
 
+// Both patches (raw r=16 for the moments, blurred r=21 for the rotated pattern) are staged
+// into LDS with aligned dword loads right after the keypoint is known, so a keypoint costs
+// two dependent memory round trips (selection entry, then both patches) instead of one per
+// gather batch.
+constexpr int kRawW = 9;    // dwords per raw patch row (33 bytes + alignment -> 36)
+constexpr int kRawH = 33;
+constexpr int kBlrW = 12;   // dwords per blurred patch row (43 bytes + alignment -> 48)
+constexpr int kBlrH = 43;
+
+__device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
+  const uintptr_t u = (uintptr_t)g;
+  const uint32_t* ap = reinterpret_cast<const uint32_t*>(u & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)(u & 3));
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
-  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t s_raw[4][kRawH * kRawW];
+  __shared__ uint32_t s_blr[4][kBlrH * kBlrW];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int f, item;
   const int chunks = (a.sel_per_frame + 3) / 4;
   if (!xcd_frame_map(blockIdx.x, a.nframes, chunks, &f, &item)) return;
-  const int j = item * 4 + (threadIdx.x >> 6);
+  const int j = item * 4 + wv;
   if (j >= a.sel_per_frame) return;
   int l = 0;
   while (l + 1 < a.nlevels && j >= a.lv[l + 1].sel_off) l++;
@@ -86,40 +103,48 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   const uint32_t pk = a.sel[(int64_t)f * a.sel_fstride + j];
   const int cx = (int)(pk & 0xFFF) + kMinBorder, cy = (int)((pk >> 12) & 0xFFF) + kMinBorder;
   const int score = (int)(pk >> 24);
-  const int pitch = L.pitch;
+  const int pitch = L.pitch, bp = L.bpitch;
   const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
                                 : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
-  const uint8_t* ctr = img + (int64_t)cy * pitch + cx;
-  // ---- IC_Angle: 18 independent byte gathers per lane, integer moments
-  int m10 = 0, m01 = 0;
+  const uint8_t* blr = a.blur + (int64_t)f * a.blur_fstride + L.img_off;
+  // ---- stage both patches (independent loads, issued together)
   {
-    int e[18], I[18];
-#pragma unroll
-    for (int t = 0; t < 18; t++) e[t] = c_icpatch[t * 64 + lane];
-#pragma unroll
-    for (int t = 0; t < 18; t++) {
-      const int u = (e[t] & 0xFF) - 16, v = ((e[t] >> 8) & 0xFF) - 16;
-      I[t] = ctr[(int64_t)v * pitch + u];
+    const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
+    for (int q = lane; q < kRawH * kRawW; q += 64) {
+      const int r = q / kRawW, c = q - r * kRawW;
+      s_raw[wv][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
     }
-#pragma unroll
-    for (int t = 0; t < 18; t++) {
-      const int u = (e[t] & 0xFF) - 16, v = ((e[t] >> 8) & 0xFF) - 16;
-      const int w = (e[t] >> 16) & 1;
-      m10 += w * u * I[t];
-      m01 += w * v * I[t];
+    const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21);
+    for (int q = lane; q < kBlrH * kBlrW; q += 64) {
+      const int r = q / kBlrW, c = q - r * kBlrW;
+      s_blr[wv][q] = load_aligned_dword(b0 + (int64_t)r * bp + 4 * c);
     }
+  }
+  dev::wave_sync();
+  const uint8_t* raw = reinterpret_cast<const uint8_t*>(s_raw[wv]);
+  const uint8_t* bl = reinterpret_cast<const uint8_t*>(s_blr[wv]);
+  // ---- IC_Angle: integer moments over the circular r=16 patch
+  int m10 = 0, m01 = 0;
+#pragma unroll
+  for (int t = 0; t < 18; t++) {
+    const int e = c_icpatch[t * 64 + lane];
+    const int u = (e & 0xFF) - 16, v = ((e >> 8) & 0xFF) - 16;
+    const int w = (e >> 16) & 1;
+    const int I = raw[(v + 16) * (4 * kRawW) + (u + 16)];
+    m10 += w * u * I;
+    m01 += w * v * I;
   }
   m10 = dev::wave_sum(m10);
   m01 = dev::wave_sum(m01);
   const float angle = fast_atan2_dev((float)m01, (float)m10);
-  // ---- rotated BRIEF on the blurred level
+  // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
   const double ca = cos(theta), sa = sin(theta);
-  const int bp = L.bpitch;
-  const uint8_t* bc = a.blur + (int64_t)f * a.blur_fstride + L.img_off + (int64_t)cy * bp + cx;
   const int nwords = a.desc_size / 8;
   uint8_t* dptr = a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size;
+  constexpr int BW = 4 * kBlrW;
+  const uint8_t* bc = bl + 21 * BW + 21;
   uint64_t words[8];
 #pragma unroll
   for (int r = 0; r < 8; r++) {
@@ -127,10 +152,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
       const int t = r * 64 + lane;  // test t: byte t/8, bit t%8
       const double px0 = c_pattern[4 * t], py0 = c_pattern[4 * t + 1];
       const double px1 = c_pattern[4 * t + 2], py1 = c_pattern[4 * t + 3];
-      const int o0 = rot_round(px0, py0, ca, sa, false) * bp + rot_round(px0, py0, ca, sa, true);
-      const int o1 = rot_round(px1, py1, ca, sa, false) * bp + rot_round(px1, py1, ca, sa, true);
-      const int t0 = bc[o0], t1 = bc[o1];
-      words[r] = __ballot(t0 < t1);
+      const int o0 = rot_round(px0, py0, ca, sa, false) * BW + rot_round(px0, py0, ca, sa, true);
+      const int o1 = rot_round(px1, py1, ca, sa, false) * BW + rot_round(px1, py1, ca, sa, true);
+      words[r] = __ballot(bc[o0] < bc[o1]);
     }
   }
   if (lane < nwords) {

@@ -63,8 +63,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
   const int npx = ww * wh;
   const int th = wh + 6, nd = (ww + 6 + 3) >> 2;
   // ---- stage tile (window + 3px halo) with aligned dword loads + alignbyte
-  for (int i = lane; i < th * nd; i += 64) {
-    const int r = i / nd, j = i - r * nd;
+  constexpr int kDW = kFTP / 4;  // 19 dword slots per tile row (constant divisor)
+  for (int i = lane; i < th * kDW; i += 64) {
+    const int r = i / kDW, j = i - r * kDW;
+    if (j >= nd) continue;
     const uintptr_t g = (uintptr_t)(img + (int64_t)(c.wy0 - 3 + r) * pitch + (c.wx0 - 3) + 4 * j);
     const uint32_t* ap = reinterpret_cast<const uint32_t*>(g & ~(uintptr_t)3);
     const uint32_t d0 = ap[0], d1 = ap[1];
@@ -87,9 +89,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
       bool keep = false;
       int x = 0, y = 0, s = 0;
       if (j < nc) {
-        const int idx = L.corner[buf][j];
-        y = idx / ww; x = idx - y * ww;
-        s = L.smap[idx] - 1;
+        const int pk = L.corner[buf][j];
+        y = pk >> 8; x = pk & 0xFF;
+        s = L.smap[y * ww + x] - 1;
         keep = true;
 #pragma unroll
         for (int dy = -1; dy <= 1; dy++)
@@ -116,6 +118,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     }
   };
 
+  // raster position of this lane's pixel, advanced by 64 pixels per step without divisions
+  int py = lane / max(ww, 1), px = lane - py * max(ww, 1);
+  const int sdy = 64 / max(ww, 1), sdx = 64 - sdy * max(ww, 1);
   for (int ch = 0; ch < nchunks; ch++) {
     const int base = ch * kChunk;
     // ---- A: compass pre-test, ordered compaction of survivors
@@ -123,9 +128,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
 #pragma unroll
     for (int k = 0; k < kChunk / 64; k++) {
       const int i = base + 64 * k + lane;
+      const int y = py, x = px;
+      px += sdx; py += sdy;
+      if (px >= ww) { px -= ww; py++; }
       bool pass = false;
       if (i < npx) {
-        const int y = i / ww, x = i - y * ww;
         const uint8_t* p = &L.tile[(y + 3) * kFTP + x + 3];
         const int v = p[0];
         const int q0 = p[3 * kFTP], q4 = p[3], q8 = p[-3 * kFTP], q12 = p[-3];
@@ -136,7 +143,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
                (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0);
       }
       const uint64_t bal = __ballot(pass);
-      if (pass) L.surv[ns + __popcll(bal & dev::lanemask_lt())] = (uint16_t)i;
+      if (pass) L.surv[ns + __popcll(bal & dev::lanemask_lt())] = (uint16_t)((y << 8) | x);
       ns += __popcll(bal);
     }
     dev::wave_sync();
@@ -149,7 +156,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
       int idx = 0;
       if (j < ns) {
         idx = L.surv[j];
-        const int y = idx / ww, x = idx - y * ww;
+        const int y = idx >> 8, x = idx & 0xFF;
         const uint8_t* p = &L.tile[(y + 3) * kFTP + x + 3];
         const int v = p[0];
         int d[16];
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         corner = dark > t || bright > t;
         if (corner) {
           const int score = max(max(t, dark), bright) - 1;
-          L.smap[idx] = (uint8_t)(score + 1);
+          L.smap[y * ww + x] = (uint8_t)(score + 1);
         }
       }
       const uint64_t bal = __ballot(corner);

@@ -6,18 +6,18 @@
 // BORDER_REFLECT_101 (:1185-1197) only so that later stages may read outside it; nothing
 // downstream reads outside a level except the blur, which reflects explicitly here.
 //
-// Tile: 64 x 16 output pixels per 256-thread workgroup; the level-l tile is recomputed with
-// a 2-pixel halo so raw and blurred tiles leave in one pass (stores are aligned dwords:
-// levels >= 1 and all blurred levels have a 64-byte-aligned row pitch).
+// Tile: 124 x 16 output pixels per 256-thread workgroup; the level-l tile is recomputed
+// with a 2-pixel halo (128 x 20) so raw and blurred tiles leave in one pass (stores are
+// aligned dwords: levels >= 1 and all blurred levels have a 64-byte-aligned row pitch).
 #include "common.hpp"
 #include "extractor_kernels.hpp"
 
 namespace mcs {
 
-constexpr int kPTW = 64, kPTH = 16, kPH = 2;
-constexpr int kSrcMaxW = 160, kSrcMaxH = 48;   // host-checked bounds of the source tile
-constexpr int kLvlW = kPTW + 8;                 // level tile origin at x0-4 (aligned core)
-constexpr int kLvlH = kPTH + 2 * kPH;
+constexpr int kPTW = 124, kPTH = 16, kPH = 2;   // core tile; halo tile = 128 x 20
+constexpr int kHH = kPTH + 2 * kPH;              // 20 halo rows = 5 per wave
+constexpr int kSrcMaxW = 288, kSrcMaxH = 48;     // source tile bound (scale <= 2.2, host-checked)
+constexpr int kLvlW = kPTW + 8;                  // level tile origin at x0-4 (aligned core)
 
 __device__ __forceinline__ int refl101(int p, int n) {
   p = p < 0 ? -p : p;
@@ -39,83 +39,124 @@ __device__ __forceinline__ int vres(int s0, int s1, int b0, int b1, bool simd) {
   return max(0, min(255, v));
 }
 
+// One workgroup = 4 waves; wave w owns halo rows w, w+4, ...; lane owns halo columns
+// lane and lane+64 (their resize coefficients stay in registers, row coefficients are
+// wave-uniform scalars).
 template <bool RESIZE>
 __global__ __launch_bounds__(256) void k_pyr_blur(PyrArgs a) {
   __shared__ uint8_t s_src[RESIZE ? kSrcMaxH * kSrcMaxW : 4];
-  __shared__ __attribute__((aligned(16))) uint8_t s_lvl[kLvlH * kLvlW];
-  __shared__ uint16_t s_hs[kLvlH * kPTW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lvl[kHH * kLvlW];
+  __shared__ uint16_t s_hs[kHH * kPTW];
   int f, item;
   if (!xcd_frame_map(blockIdx.x, a.nframes, a.tiles_x * a.tiles_y, &f, &item)) return;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int x0 = (item % a.tiles_x) * kPTW, y0 = (item / a.tiles_x) * kPTH;
   const int dw = a.dw, dh = a.dh;
-  const int ry0 = max(0, y0 - kPH), ry1 = min(dh, y0 + kPTH + kPH);
-  const int rx0 = max(0, x0 - kPH), rx1 = min(dw, x0 + kPTW + kPH);
-  const int hr = ry1 - ry0, hc = rx1 - rx0;
   const int lrow0 = y0 - kPH;  // s_lvl row 0 <-> level row y0-2
   const int lcol0 = x0 - 4;    // s_lvl col 0 <-> level col x0-4
   const uint8_t* S = a.src + (int64_t)f * a.src_fstride;
+  const int ry0 = max(0, lrow0), ry1 = min(dh, y0 + kPTH + kPH);
+  const int rx0 = max(0, x0 - kPH), rx1 = min(dw, x0 + kPTW + kPH);
 
   if (RESIZE) {
     const int sh = a.sh, sw = a.sw;
-    auto clipr = [sh](int y) { return y < 0 ? 0 : (y < sh ? y : sh - 1); };
-    const int sr0 = clipr(a.yofs[ry0]), sr1 = clipr(a.yofs[ry1 - 1] + 1) + 1;
+    const int sr0 = min(max(a.yofs[ry0], 0), sh - 1);
+    const int sr1 = min(max(a.yofs[ry1 - 1] + 1, 0), sh - 1) + 1;
     const int sc0 = a.xofs[rx0], sc1 = min(a.xofs[rx1 - 1] + 1, sw - 1) + 1;
-    const int srows = sr1 - sr0, scols = sc1 - sc0;
-    for (int i = tid; i < srows * scols; i += 256) {
-      const int r = i / scols, c = i - r * scols;
-      s_src[r * kSrcMaxW + c] = S[(int64_t)(sr0 + r) * a.spitch + sc0 + c];
+    for (int r = wv; r < sr1 - sr0; r += 4) {
+      const uint8_t* srow = S + (int64_t)(sr0 + r) * a.spitch + sc0;
+      for (int c = lane; c < sc1 - sc0; c += 64) s_src[r * kSrcMaxW + c] = srow[c];
+    }
+    // per-lane column coefficients for halo columns lane, lane + 64
+    int sx[2], sx1[2], a0[2], a1[2];
+    bool simd[2], cval[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+      const int c = x0 - kPH + lane + 64 * m;
+      cval[m] = c >= rx0 && c < rx1;
+      const int cc = cval[m] ? c : rx0;
+      sx[m] = a.xofs[cc] - sc0;
+      sx1[m] = min(a.xofs[cc] + 1, sw - 1) - sc0;
+      a0[m] = a.alpha[2 * cc];
+      a1[m] = a.alpha[2 * cc + 1];
+      simd[m] = cc < a.simd_end;
     }
     __syncthreads();
-    for (int i = tid; i < hr * hc; i += 256) {
-      const int r = ry0 + i / hc, c = rx0 + i % hc;
-      const int sx = a.xofs[c] - sc0;
-      const int sx1 = min(a.xofs[c] + 1, sw - 1) - sc0;
-      const int a0 = a.alpha[2 * c], a1 = a.alpha[2 * c + 1];
+    for (int r = ry0 + wv; r < ry1; r += 4) {
       const int sy = a.yofs[r];
-      const uint8_t* r0 = s_src + (clipr(sy) - sr0) * kSrcMaxW;
-      const uint8_t* r1 = s_src + (clipr(sy + 1) - sr0) * kSrcMaxW;
-      const int s0 = r0[sx] * a0 + r0[sx1] * a1;
-      const int s1 = r1[sx] * a0 + r1[sx1] * a1;
-      s_lvl[(r - lrow0) * kLvlW + (c - lcol0)] =
-          (uint8_t)vres(s0, s1, a.beta[2 * r], a.beta[2 * r + 1], c < a.simd_end);
+      const int b0 = a.beta[2 * r], b1 = a.beta[2 * r + 1];
+      const uint8_t* r0 = s_src + (min(max(sy, 0), sh - 1) - sr0) * kSrcMaxW;
+      const uint8_t* r1 = s_src + (min(max(sy + 1, 0), sh - 1) - sr0) * kSrcMaxW;
+      uint8_t* out = s_lvl + (r - lrow0) * kLvlW + (x0 - kPH - lcol0);
+#pragma unroll
+      for (int m = 0; m < 2; m++) {
+        if (!cval[m]) continue;
+        const int s0 = r0[sx[m]] * a0[m] + r0[sx1[m]] * a1[m];
+        const int s1 = r1[sx[m]] * a0[m] + r1[sx1[m]] * a1[m];
+        out[lane + 64 * m] = (uint8_t)vres(s0, s1, b0, b1, simd[m]);
+      }
     }
   } else {
-    for (int i = tid; i < hr * hc; i += 256) {
-      const int r = ry0 + i / hc, c = rx0 + i % hc;
-      s_lvl[(r - lrow0) * kLvlW + (c - lcol0)] = S[(int64_t)r * a.spitch + c];
+    for (int r = ry0 + wv; r < ry1; r += 4) {
+      const uint8_t* srow = S + (int64_t)r * a.spitch;
+      uint8_t* out = s_lvl + (r - lrow0) * kLvlW;
+#pragma unroll
+      for (int m = 0; m < 2; m++) {
+        const int c = x0 - kPH + lane + 64 * m;
+        if (c >= rx0 && c < rx1) out[c - lcol0] = srow[c];
+      }
     }
   }
   __syncthreads();
-  // raw level-l core tile -> HBM (aligned dwords)
-  const int ty = tid >> 4, tx = (tid & 15) * 4;
-  const int y = y0 + ty;
-  if (RESIZE && y < dh && x0 + tx < dw) {
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(&s_lvl[(ty + kPH) * kLvlW + 4 + tx]);
-    *reinterpret_cast<uint32_t*>(a.dst + (int64_t)f * a.dst_fstride + (int64_t)y * a.dpitch + x0 + tx) = v;
-  }
-  // horizontal 5-sums for the halo rows, core columns (reflect-101 at the level border)
-  for (int i = tid; i < hr * kPTW; i += 256) {
-    const int r = i / kPTW, c = x0 + (i % kPTW);
-    int s = 0;
-    if (c < dw) {
-      const uint8_t* row = s_lvl + (ry0 + r - lrow0) * kLvlW;
-#pragma unroll
-      for (int d = -2; d <= 2; d++) s += row[refl101(c + d, dw) - lcol0];
+  // raw level-l core tile -> HBM (aligned dwords: 31 per row, 16 rows)
+  if (RESIZE) {
+    for (int i = tid; i < kPTH * (kPTW / 4); i += 256) {
+      const int ty = i / (kPTW / 4), tx = (i % (kPTW / 4)) * 4;
+      const int y = y0 + ty;
+      if (y < dh && x0 + tx < dw) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(&s_lvl[(ty + kPH) * kLvlW + 4 + tx]);
+        *reinterpret_cast<uint32_t*>(a.dst + (int64_t)f * a.dst_fstride + (int64_t)y * a.dpitch + x0 + tx) = v;
+      }
     }
-    s_hs[(ry0 + r - lrow0) * kPTW + (c - x0)] = (uint16_t)s;
   }
-  __syncthreads();
-  if (y < dh && x0 + tx < dw) {
-    uint32_t packed = 0;
+  // horizontal 5-sums (reflect-101 only at the level border), core columns
+  for (int r = ry0 + wv; r < ry1; r += 4) {
+    const uint8_t* row = s_lvl + (r - lrow0) * kLvlW;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int m = 0; m < 2; m++) {
+      const int cl = lane + 64 * m;
+      if (cl >= kPTW) continue;
+      const int c = x0 + cl;
       int s = 0;
+      if (c < dw) {
+        if (c >= 2 && c < dw - 2) {
+          const uint8_t* q = row + (c - lcol0);
+          s = q[-2] + q[-1] + q[0] + q[1] + q[2];
+        } else {
 #pragma unroll
-      for (int d = -2; d <= 2; d++) s += s_hs[(refl101(y + d, dh) - lrow0) * kPTW + tx + k];
-      packed |= (uint32_t)((2 * s + 25) / 50) << (8 * k);
+          for (int d = -2; d <= 2; d++) s += row[refl101(c + d, dw) - lcol0];
+        }
+      }
+      s_hs[(r - lrow0) * kPTW + cl] = (uint16_t)s;
     }
-    *reinterpret_cast<uint32_t*>(a.blur + (int64_t)f * a.blur_fstride + (int64_t)y * a.bpitch + x0 + tx) = packed;
+  }
+  __syncthreads();
+  for (int i = tid; i < kPTH * (kPTW / 4); i += 256) {
+    const int ty = i / (kPTW / 4), tx = (i % (kPTW / 4)) * 4;
+    const int y = y0 + ty;
+    if (y < dh && x0 + tx < dw) {
+      int rr[5];
+#pragma unroll
+      for (int d = -2; d <= 2; d++) rr[d + 2] = (refl101(y + d, dh) - lrow0) * kPTW;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int s = s_hs[rr[0] + tx + k] + s_hs[rr[1] + tx + k] + s_hs[rr[2] + tx + k] +
+                      s_hs[rr[3] + tx + k] + s_hs[rr[4] + tx + k];
+        packed |= (uint32_t)((2 * s + 25) / 50) << (8 * k);
+      }
+      *reinterpret_cast<uint32_t*>(a.blur + (int64_t)f * a.blur_fstride + (int64_t)y * a.bpitch + x0 + tx) = packed;
+    }
   }
 }
 

@@ -84,6 +84,13 @@ SIGNATURES = {
     "mcs_hamming_top2_device": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P]),
     "mcs_hamming_dense_device": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     "mcs_hamming_top2_batch_device": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    # bundle adjustment (include/mcs_ba.h)
+    "mcs_ba_default_options": (None, [_P]),
+    "mcs_ba_create": (ctypes.c_int, [_I32, _P]),
+    "mcs_ba_destroy": (None, [_P]),
+    "mcs_ba_optimize": (ctypes.c_int, [_P] * 9),
+    "mcs_local_ba": (ctypes.c_int, [_P] * 9),
+    "mcs_ba_linearize": (ctypes.c_int, [_P] * 5),
     "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
 }
 
