@@ -201,7 +201,7 @@ def main():
                 traffic = json.load(open(tf)).get("pyramid+fast_bytes_per_call")
             except Exception:
                 traffic = None
-        roofline = {"kernel": "pyramid+fast (k_resize_linear x7 + k_fast_cells)",
+        roofline = {"kernel": "pyramid+fast (k_pyr_rows<true> x7: resize + fused blur, k_fast_cells)",
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "alg_bytes_per_call": bpf * F}

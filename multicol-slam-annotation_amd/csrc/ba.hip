@@ -289,30 +289,67 @@ __global__ __launch_bounds__(256) void k_points_build(Dev d) {
   d.red[l] = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
 }
 
-// per active pose: Hpp (6x6), b_p; 36 threads each own one element, edges in order
-__global__ __launch_bounds__(64) void k_poses_build(Dev d) {
-  const int i = blockIdx.x, t = threadIdx.x;
-  double acc = 0.0;
-  if (t < 42) {
-    for (int q = d.ps_ptr[i]; q < d.ps_ptr[i + 1]; q++) {
-      const int e = d.ps_edges[q];
-      const double* jp = d.jp + 12 * e;
-      const double w = d.w[e];
-      if (t < 36) {
-        const int a = t / 6, b = t % 6;
-        acc += w * (jp[a] * jp[b] + jp[6 + a] * jp[6 + b]);
-      } else {
-        const int a = t - 36;
-        const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
-        acc += jp[a] * we0 + jp[6 + a] * we1;
-      }
-    }
-    if (t < 36) d.Hpp[36 * i + t] = acc;
-    else d.bp[6 * i + t - 36] = acc;
+// Deterministic block sum of NV per-thread partials: fixed xor-butterfly inside each wave,
+// then the 4 wave sums in wave order.  On return sm[v * 4] holds sum v (after the barrier).
+template <int NV>
+__device__ __forceinline__ void block_sum_vec(double (&acc)[NV], double* sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[v] += __shfl_xor(acc[v], o);
   }
-  if (t < 6) d.red[d.nl + 6 * i + t] = 0.0;  // placeholder, filled below
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < NV; v++) sm[v * 4 + w] = acc[v];
+  }
   __syncthreads();
-  if (t < 6) d.red[d.nl + 6 * i + t] = fabs(d.Hpp[36 * i + 7 * t]);
+  if (threadIdx.x < NV) {
+    const int v = threadIdx.x;
+    sm[v * 4] = ((sm[v * 4] + sm[v * 4 + 1]) + sm[v * 4 + 2]) + sm[v * 4 + 3];
+  }
+  __syncthreads();
+}
+
+constexpr int kRedNT = 256;
+constexpr int kUpper6[21][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, {1, 1},
+                                {1, 2}, {1, 3}, {1, 4}, {1, 5}, {2, 2}, {2, 3}, {2, 4},
+                                {2, 5}, {3, 3}, {3, 4}, {3, 5}, {4, 4}, {4, 5}, {5, 5}};
+
+// per active pose: Hpp (6x6, upper 21 mirrored), b_p; edges of the pose split over 256
+// threads (fixed stride), block tree sum
+__global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
+  __shared__ double sm[27 * 4];
+  const int i = blockIdx.x, t = threadIdx.x;
+  double acc[27];
+#pragma unroll
+  for (int v = 0; v < 27; v++) acc[v] = 0.0;
+  for (int q = d.ps_ptr[i] + t; q < d.ps_ptr[i + 1]; q += kRedNT) {
+    const int e = d.ps_edges[q];
+    const double* jp = d.jp + 12 * e;
+    double j0[6], j1[6];
+#pragma unroll
+    for (int a = 0; a < 6; a++) { j0[a] = jp[a]; j1[a] = jp[6 + a]; }
+    const double w = d.w[e];
+    const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
+#pragma unroll
+    for (int v = 0; v < 21; v++) {
+      const int a = kUpper6[v][0], bb = kUpper6[v][1];
+      acc[v] += w * (j0[a] * j0[bb] + j1[a] * j1[bb]);
+    }
+#pragma unroll
+    for (int a = 0; a < 6; a++) acc[21 + a] += j0[a] * we0 + j1[a] * we1;
+  }
+  block_sum_vec<27>(acc, sm);
+  if (t < 21) {
+    const int a = kUpper6[t][0], bb = kUpper6[t][1];
+    const double h = sm[t * 4];
+    d.Hpp[36 * i + 6 * a + bb] = h;
+    d.Hpp[36 * i + 6 * bb + a] = h;
+    if (a == bb) d.red[d.nl + 6 * i + a] = fabs(h);
+  } else if (t < 27) {
+    d.bp[6 * i + t - 21] = sm[t * 4];
+  }
 }
 
 // per active point: D = Hll + lambda I -> Dinv (cofactors), db = Dinv b_l;
@@ -354,33 +391,100 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d, double lam) {
 }
 
 // reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lambda I)
-//   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T, in point/edge order;
+//   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T;
 // diagonal blocks also form bschur_i = b_i - sum_e Hpl_e db(point(e)).
-__global__ __launch_bounds__(64) void k_schur(Dev d, double lam) {
+// The pair list of a block is split over 256 threads (fixed stride) + block tree sum.
+__global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam) {
+  __shared__ double sm[42 * 4];
   const int blk = blockIdx.x, t = threadIdx.x;
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
   const int n = 6 * d.np;
-  if (t < 36) {
-    const int a = t / 6, b = t % 6;
-    double s = 0.0;
-    if (bi == bj) { s = d.Hpp[36 * bi + 6 * a + b]; if (a == b) s += lam; }
-    for (int q = d.pr_ptr[blk]; q < d.pr_ptr[blk + 1]; q++) {
-      const double* Y = d.y + 18 * d.pr_e1[q] + 3 * a;
-      const double* B = d.hpl + 18 * d.pr_e2[q] + 3 * b;
-      s -= Y[0] * B[0] + Y[1] * B[1] + Y[2] * B[2];
+  double acc[42];
+#pragma unroll
+  for (int v = 0; v < 42; v++) acc[v] = 0.0;
+  for (int q = d.pr_ptr[blk] + t; q < d.pr_ptr[blk + 1]; q += kRedNT) {
+    const double* Y = d.y + 18 * d.pr_e1[q];
+    const double* B = d.hpl + 18 * d.pr_e2[q];
+    double y[18], bb[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) { y[k] = Y[k]; bb[k] = B[k]; }
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+      for (int c = 0; c < 6; c++)
+        acc[6 * a + c] += y[3 * a] * bb[3 * c] + y[3 * a + 1] * bb[3 * c + 1] + y[3 * a + 2] * bb[3 * c + 2];
+  }
+  if (bi == bj) {
+    for (int q = d.ps_ptr[bi] + t; q < d.ps_ptr[bi + 1]; q += kRedNT) {
+      const int e = d.ps_edges[q];
+      const double* B = d.hpl + 18 * e;
+      const double* g = d.db + 3 * d.point_h[d.e_point[e]];
+      const double g0 = g[0], g1 = g[1], g2 = g[2];
+#pragma unroll
+      for (int a = 0; a < 6; a++) acc[36 + a] += B[3 * a] * g0 + B[3 * a + 1] * g1 + B[3 * a + 2] * g2;
     }
-    d.S[(6 * bi + a) * n + 6 * bj + b] = s;
+  }
+  block_sum_vec<42>(acc, sm);
+  if (t < 36) {
+    const int a = t / 6, c = t % 6;
+    double s0 = 0.0;
+    if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam; }
+    d.S[(6 * bi + a) * n + 6 * bj + c] = s0 - sm[t * 4];
   } else if (t < 42 && bi == bj) {
     const int a = t - 36;
-    double s = d.bp[6 * bi + a];
-    for (int q = d.ps_ptr[bi]; q < d.ps_ptr[bi + 1]; q++) {
-      const int e = d.ps_edges[q];
-      const double* B = d.hpl + 18 * e + 3 * a;
-      const double* g = d.db + 3 * d.point_h[d.e_point[e]];
-      s -= B[0] * g[0] + B[1] * g[1] + B[2] * g[2];
-    }
-    d.bs[6 * bi + a] = s;
+    d.bs[6 * bi + a] = d.bp[6 * bi + a] - sm[t * 4];
   }
+}
+
+// LDL^T of the reduced camera system held in LDS (n <= kLdsN), right-looking, no pivoting
+// (Eigen SimplicialLDLT only fails on an exact zero pivot), then the two triangular solves
+// column by column.  One workgroup; zero pivot -> flag = 1.
+constexpr int kLdsN = 88;   // n*n + n doubles <= 62.6 KB of LDS
+__global__ __launch_bounds__(256) void k_ldlt_lds(Dev d) {
+  extern __shared__ double A[];   // n*n lower (row-major), then x[n]
+  __shared__ int fail;
+  const int n = 6 * d.np, t = threadIdx.x;
+  double* x = A + n * n;
+  for (int idx = t; idx < n * n; idx += 256) {
+    const int i = idx / n, j = idx - i * n;
+    A[idx] = (j <= i) ? d.S[idx] : 0.0;
+  }
+  for (int i = t; i < n; i += 256) x[i] = d.bs[i];
+  if (t == 0) fail = 0;
+  __syncthreads();
+  for (int j = 0; j < n; j++) {
+    const double dj = A[j * n + j];
+    if (dj == 0.0) { if (t == 0) fail = 1; break; }   // uniform: every thread reads the same dj
+    for (int i = j + 1 + t; i < n; i += 256) A[i * n + j] /= dj;
+    __syncthreads();
+    // trailing update A[i][m] -= (L_ij L_mj) d_j for j < m <= i
+    const int r = n - 1 - j;
+    for (int idx = t; idx < r * r; idx += 256) {
+      const int ii = idx / r, mm = idx - ii * r;
+      if (mm > ii) continue;
+      const int i = j + 1 + ii, m = j + 1 + mm;
+      A[i * n + m] -= (A[i * n + j] * A[m * n + j]) * dj;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (fail) { if (t == 0) *d.flag = 1; return; }
+  // forward: L y = b (unit lower), column-oriented
+  for (int k = 0; k < n; k++) {
+    const double xk = x[k];
+    for (int i = k + 1 + t; i < n; i += 256) x[i] -= A[i * n + k] * xk;
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += 256) x[i] /= A[i * n + i];
+  __syncthreads();
+  // backward: L^T x = y
+  for (int k = n - 1; k >= 0; k--) {
+    const double xk = x[k];
+    for (int i = t; i < k; i += 256) x[i] -= A[k * n + i] * xk;
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += 256) d.x[i] = x[i];
+  if (t == 0) *d.flag = 0;
 }
 
 // LDL^T (no pivoting, lower, left-looking) + solve, one workgroup; zero pivot -> flag=1
@@ -473,16 +577,31 @@ using namespace mcs::ba;
 struct mcs_ba_ctx {
   int device = 0;
   hipStream_t st = nullptr;
+  // Device buffers are cached across calls: the driver requests them in the same order
+  // every call, so request k reuses slot k when it is large enough (grow-only).
   std::vector<void*> bufs;
+  std::vector<size_t> caps;
+  size_t next = 0;
+  double* pinned = nullptr;   // host-pinned readback scalars
+  int32_t* pinned_i = nullptr;
   void* alloc(size_t bytes) {
+    bytes += 64;
+    if (next < bufs.size() && caps[next] >= bytes) return bufs[next++];
     void* p = nullptr;
-    if (hipMalloc(&p, bytes + 64) != hipSuccess) return nullptr;
-    bufs.push_back(p);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (next < bufs.size()) {
+      (void)hipFree(bufs[next]);
+      bufs[next] = p; caps[next] = bytes;
+    } else {
+      bufs.push_back(p); caps.push_back(bytes);
+    }
+    next++;
     return p;
   }
-  void free_all() {
+  void free_all() { next = 0; }   // recycle (buffers stay allocated)
+  void release() {
     for (void* p : bufs) (void)hipFree(p);
-    bufs.clear();
+    bufs.clear(); caps.clear(); next = 0;
   }
 };
 
@@ -591,6 +710,8 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   if (!c) return MCS_ERR_ARG;
   c->device = device;
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocDefault));
   *out = c;
   return MCS_OK;
 }
@@ -598,7 +719,10 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
 void mcs_ba_destroy(mcs_ba_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  c->free_all();
+  (void)hipStreamSynchronize(c->st);
+  c->release();
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->pinned_i) (void)hipHostFree(c->pinned_i);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -667,8 +791,9 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
   auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
     hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
-    MCS_HIP_CHECK(hipMemcpyAsync(out, d_scalar, 8, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
     MCS_HIP_CHECK(hipStreamSynchronize(st));
+    *out = c->pinned[3];
     return MCS_OK;
   };
   auto copy_state = [&](double* dp, double* dl, const double* sp, const double* sl) -> int {
@@ -686,27 +811,33 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
     double lambda = 0, lastChi = 0;
     int ni = 2, nBad = 0, it = 0;
     bool ok = true;
+    double currentChi = chi0;
     for (int i = 0; i < o->max_iterations && !(*stop) && ok; i++) {
       // ---- OptimizationAlgorithmLevenberg::solve(i)
+      // The robust chi2 of the linearisation point equals the chi2 the previous iteration
+      // ended with (same kernel, same state: accepted trial or restored backup), so only
+      // the first iteration reads anything back (the max diagonal for lambda's init).
       hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
-      hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
       hipLaunchKernelGGL(k_points_build, dim3(gb(s.nl)), dim3(256), 0, st, d);
-      if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(64), 0, st, d);
-      hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl + 6 * s.np, d_scalar + 1);
-      double hs[2];
-      MCS_HIP_CHECK(hipMemcpyAsync(hs, d_scalar, 16, hipMemcpyDeviceToHost, st));
-      MCS_HIP_CHECK(hipStreamSynchronize(st));
-      double currentChi = hs[0];
+      if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
+      if (i == 0) {
+        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl + 6 * s.np, d_scalar + 1);
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 8, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipStreamSynchronize(st));
+        lambda = o->tau * c->pinned[1]; ni = 2; nBad = 0;
+      }
       const double iniChi = currentChi;
-      if (i == 0) { lambda = o->tau * hs[1]; ni = 2; nBad = 0; }
       double rho = 0;
       int qmax = 0;
       do {
         if ((rc = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc;  // push
         hipLaunchKernelGGL(k_point_trial, dim3(gb(s.nl)), dim3(256), 0, st, d, lambda);
         if (s.np) {
-          hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(64), 0, st, d, lambda);
-          hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), 0, st, d);
+          hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(kRedNT), 0, st, d, lambda);
+          if (n <= kLdsN)
+            hipLaunchKernelGGL(k_ldlt_lds, dim3(1), dim3(256), ((size_t)n * n + n) * 8, st, d);
+          else
+            hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), 0, st, d);
         } else {
           MCS_HIP_CHECK(hipMemsetAsync(d.flag, 0, 4, st));
         }
@@ -714,11 +845,11 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
         hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.red, nvar, d_scalar + 2);
         hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
         hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
-        double tr[3];
-        int fl = 0;
-        MCS_HIP_CHECK(hipMemcpyAsync(tr, d_scalar, 24, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipMemcpyAsync(&fl, d.flag, 4, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d.flag, 4, hipMemcpyDeviceToHost, st));
         MCS_HIP_CHECK(hipStreamSynchronize(st));
+        const double tr[3] = {c->pinned[0], c->pinned[1], c->pinned[2]};
+        const int fl = c->pinned_i[0];
         double tempChi = tr[0];
         if (fl) tempChi = std::numeric_limits<double>::max();
         rho = currentChi - tempChi;
@@ -747,9 +878,9 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
       }
       ok = (result == 0);
       ++it;
-      // ---- SparseOptimizerTerminateAction (post-iteration)
-      double cur;
-      if ((rc = chi_now(&cur))) return rc;
+      // ---- SparseOptimizerTerminateAction (post-iteration): activeRobustChi2 of the
+      // current state == currentChi (see above)
+      const double cur = currentChi;
       if (rep && rep->trace_chi2 && i < rep->trace_cap) rep->trace_chi2[i] = cur;
       if (i == 0) lastChi = cur;
       else {
@@ -766,8 +897,7 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
       if (rep) rep->lambda_final = lambda;
     }
     if (rep) rep->iterations = it;
-    double fin;
-    if ((rc = chi_now(&fin))) return rc;
+    const double fin = currentChi;
     if (rep) rep->chi2_final = fin;
   }
   if (rep) rep->stop_flag = *stop;

@@ -109,15 +109,16 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     }
     a.blur = h->d_blur + D.img_off; a.blur_fstride = pl.img_frame_bytes; a.bpitch = D.bpitch;
     a.dw = D.w; a.dh = D.h;
-    a.tiles_x = (D.w + 123) / 124; a.tiles_y = (D.h + 15) / 16;
+    pyr_strips(D.w, D.h, a);
     a.nframes = F;
     return a;
   };
   stage_mark(h, 0, st);
   // K1+K5: resize chain, each level blurred in the same pass
-  for (int l = 1; l < nl; l++) launch_pyr_blur(pyr_args(l), true, st);
+  const bool wide = pl.scale_factor > 1.5;
+  for (int l = 1; l < nl; l++) launch_pyr_blur(pyr_args(l), true, wide, st);
   stage_mark(h, 1, st);
-  launch_pyr_blur(pyr_args(0), false, st);  // blur of level 0 (the input frames)
+  launch_pyr_blur(pyr_args(0), false, false, st);  // blur of level 0 (the input frames)
   stage_mark(h, 2, st);
   // K2: FAST cells
   {
@@ -133,6 +134,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
     fa.nframes = F;
     fill_level_ptrs(pl, fa.lp);
+    fast_lds_layout(pl.max_win_w, pl.max_win_h, fa);
     launch_fast_cells(fa, st);
   }
   MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));

@@ -32,9 +32,19 @@ struct PyrArgs {
   int dw, dh;
   const int32_t* xofs; const int16_t* alpha; const int32_t* yofs; const int16_t* beta;
   int simd_end;
-  int tiles_x, tiles_y, nframes;
+  int tiles_x, tiles_y, nframes;   // tiles_x = column strips, tiles_y = row segments
+  int core, seg_rows;              // strip width (px, multiple of 4, <= 248), segment height
 };
-void launch_pyr_blur(const PyrArgs& a, bool resize, hipStream_t st);
+// strips of <= 248 columns (62 lanes x 4 px), segments of 48 rows
+inline void pyr_strips(int dw, int dh, PyrArgs& a) {
+  const int n = (dw + 247) / 248;
+  a.core = ((dw + n - 1) / n + 3) & ~3;
+  a.tiles_x = (dw + a.core - 1) / a.core;
+  a.seg_rows = 48;
+  a.tiles_y = (dh + a.seg_rows - 1) / a.seg_rows;
+}
+// wide: source tiles for scale factors in (1.5, 2.2] (larger LDS footprint)
+void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st);
 
 void launch_mask_pyramids(const Plan& pl, const uint8_t* d_masks, int n, uint8_t* dst,
                           hipStream_t st);
@@ -55,7 +65,17 @@ struct FastArgs {
   int threshold;
   int nframes;
   LevelPtrs lp;
+  // per-wave LDS layout (fast_lds_layout)
+  int tile_pitch, smap_off, surv_off, wave_lds;
 };
+// LDS layout of k_fast_cells for windows up to max_ww x max_wh
+inline void fast_lds_layout(int max_ww, int max_wh, FastArgs& a) {
+  auto al16 = [](int v) { return (v + 15) & ~15; };
+  a.tile_pitch = (max_ww + 6 + 3 + 3) & ~3;
+  a.smap_off = al16(a.tile_pitch * (max_wh + 6));
+  a.surv_off = a.smap_off + al16(max_ww * max_wh);
+  a.wave_lds = a.surv_off + 3 * 256 * 2;
+}
 void launch_fast_cells(const FastArgs& a, hipStream_t st);
 
 // ---- K3: octree

@@ -148,6 +148,8 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
         c.wx0 = (int16_t)((int)iniX + 3); c.wx1 = (int16_t)((int)maxX - 3);
         c.wy0 = (int16_t)((int)iniY + 3); c.wy1 = (int16_t)((int)maxY - 3);
         const int ww = std::max(0, c.wx1 - c.wx0), wh = std::max(0, c.wy1 - c.wy0);
+        pl.max_win_w = std::max(pl.max_win_w, ww);
+        pl.max_win_h = std::max(pl.max_win_h, wh);
         c.slot_off = slot;
         c.slot_cap = ((ww + 1) / 2) * ((wh + 1) / 2);
         slot += c.slot_cap;

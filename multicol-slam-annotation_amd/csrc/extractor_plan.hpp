@@ -61,6 +61,7 @@ struct Plan {
   int32_t cand_per_frame = 0;    // == slots_per_frame
   int32_t sel_per_frame = 0;     // sum of level sel caps == mcs_extractor_capacity
   int32_t max_cells_level = 0;
+  int32_t max_win_w = 0, max_win_h = 0;  // largest FAST window (LDS sizing)
   // resize tables (concatenated over levels 1..L-1)
   std::vector<int32_t> xofs, yofs;
   std::vector<int16_t> alpha, beta;

@@ -29,6 +29,27 @@ __device__ __forceinline__ int ham_dist_v(const uint32_t (&q)[W], const uint4* t
 }
 
 // Top-2 over one (query set, train set) pair; blockIdx.x = query tile, blockIdx.y = pair.
+// Each lane owns kQPT queries (descriptors in VGPRs) so one LDS broadcast read of a train
+// row feeds kQPT distances.  The running best/second-best are kept as packed keys
+// (dist << 16 | train index): trains are scanned in index order, so the strict-< rule of the
+// reference scans (first minimum wins, :2447) equals "two smallest keys", maintained with
+// v_min_u32 + v_med3_u32 (best <= second always).
+constexpr int kQPT = 2;
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// popcount-accumulate as one v_bcnt_u32_b32 (the compiler otherwise reassociates the sum
+// into bcnt(x, 0) + v_add3 chains, 25 % more VALU)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+  return r;
+}
+
 template <int W>
 __global__ __launch_bounds__(kHamThreads) void k_top2(
     const uint8_t* __restrict__ qbase, const uint8_t* __restrict__ tbase,
@@ -50,41 +71,73 @@ __global__ __launch_bounds__(kHamThreads) void k_top2(
   } else {
     Q = qbase; T = tbase; nq = nq_fixed; nt = nt_fixed;
   }
-  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
-  if (blockIdx.x * kHamThreads >= nq) return;  // uniform per block
-  uint32_t q[W];
-  if (qi < nq) {
-    const uint4* qp = reinterpret_cast<const uint4*>(Q + (int64_t)qi * W * 4);
+  const int q0 = blockIdx.x * (kHamThreads * kQPT);
+  if (q0 >= nq) return;  // uniform per block
+  uint32_t q[kQPT][W];
 #pragma unroll
-    for (int w4 = 0; w4 < W / 4; w4++) {
-      const uint4 v = qp[w4];
-      q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
+  for (int k = 0; k < kQPT; k++) {
+    const int qi = q0 + k * kHamThreads + threadIdx.x;
+    if (qi < nq) {
+      const uint4* qp = reinterpret_cast<const uint4*>(Q + (int64_t)qi * W * 4);
+#pragma unroll
+      for (int w4 = 0; w4 < W / 4; w4++) {
+        const uint4 v = qp[w4];
+        q[k][4 * w4] = v.x; q[k][4 * w4 + 1] = v.y; q[k][4 * w4 + 2] = v.z; q[k][4 * w4 + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; w++) q[k][w] = 0;
     }
-  } else {
-#pragma unroll
-    for (int w = 0; w < W; w++) q[w] = 0;
   }
-  int b1 = 0x7FFFFFFF, b2 = 0x7FFFFFFF, i1 = -1, i2 = -1;
+  uint32_t k1[kQPT], k2[kQPT];
+#pragma unroll
+  for (int k = 0; k < kQPT; k++) { k1[k] = 0xFFFFFFFFu; k2[k] = 0xFFFFFFFFu; }
   for (int t0 = 0; t0 < nt; t0 += kHamTile) {
     const int nt_tile = min(kHamTile, nt - t0);
     __syncthreads();
     const uint4* src = reinterpret_cast<const uint4*>(T + (int64_t)t0 * W * 4);
     for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
     __syncthreads();
-    for (int j = 0; j < nt_tile; j++) {
-      const int d = ham_dist_v<W>(q, &tile[j * (W / 4)]);
-      const int idx = t0 + j;
-      if (d < b1) { b2 = b1; i2 = i1; b1 = d; i1 = idx; }
-      else if (d < b2) { b2 = d; i2 = idx; }
-    }
+    auto body = [&](int j) {
+      const uint4* tr = &tile[j * (W / 4)];
+      const uint32_t idx = (uint32_t)(t0 + j);
+      uint32_t d[kQPT];
+#pragma unroll
+      for (int k = 0; k < kQPT; k++) d[k] = 0;
+#pragma unroll
+      for (int w4 = 0; w4 < W / 4; w4++) {
+        const uint4 v = tr[w4];
+#pragma unroll
+        for (int k = 0; k < kQPT; k++) {
+          d[k] = bcnt_acc(q[k][4 * w4 + 0] ^ v.x, d[k]);
+          d[k] = bcnt_acc(q[k][4 * w4 + 1] ^ v.y, d[k]);
+          d[k] = bcnt_acc(q[k][4 * w4 + 2] ^ v.z, d[k]);
+          d[k] = bcnt_acc(q[k][4 * w4 + 3] ^ v.w, d[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kQPT; k++) {
+        const uint32_t key = (d[k] << 16) | idx;
+        k2[k] = med3_u32(k1[k], key, k2[k]);
+        k1[k] = min(k1[k], key);
+      }
+    };
+    int j = 0;
+    for (; j + 4 <= nt_tile; j += 4) { body(j); body(j + 1); body(j + 2); body(j + 3); }
+    for (; j < nt_tile; j++) body(j);
   }
-  if (qi < nq) {
-    const int64_t o = (int64_t)p * cap_out + qi;
-    const int none = 8 * 4 * W + 1;
-    best_idx[o] = i1;
-    best_dist[o] = i1 < 0 ? none : b1;
-    second_idx[o] = i2;
-    second_dist[o] = i2 < 0 ? none : b2;
+  const int none = 8 * 4 * W + 1;
+#pragma unroll
+  for (int k = 0; k < kQPT; k++) {
+    const int qi = q0 + k * kHamThreads + threadIdx.x;
+    if (qi < nq) {
+      const int64_t o = (int64_t)p * cap_out + qi;
+      const bool h1 = k1[k] != 0xFFFFFFFFu, h2 = k2[k] != 0xFFFFFFFFu;
+      best_idx[o] = h1 ? (int)(k1[k] & 0xFFFF) : -1;
+      best_dist[o] = h1 ? (int)(k1[k] >> 16) : none;
+      second_idx[o] = h2 ? (int)(k2[k] & 0xFFFF) : -1;
+      second_dist[o] = h2 ? (int)(k2[k] >> 16) : none;
+    }
   }
 }
 
@@ -215,7 +268,8 @@ int mcs_hamming_top2_device(const uint8_t* d_q, int32_t nq, const uint8_t* d_t, 
   int rc = check_bytes(bytes);
   if (rc) return rc;
   if (nq <= 0) return MCS_OK;
-  dim3 g((nq + kHamThreads - 1) / kHamThreads, 1);
+  if (nt > 65535) { set_error("top2: at most 65535 train descriptors"); return MCS_ERR_ARG; }
+  dim3 g((nq + kHamThreads * kQPT - 1) / (kHamThreads * kQPT), 1);
   MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_q, d_t,
                  (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, nq, nt, nq,
                  d_best_idx, d_best_dist, d_second_idx, d_second_dist);
@@ -231,7 +285,8 @@ int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts
   if (rc) return rc;
   if (n_pairs <= 0) return MCS_OK;
   if (!d_desc || !d_counts || !d_pairs || cap <= 0) return MCS_ERR_ARG;
-  dim3 g((cap + kHamThreads - 1) / kHamThreads, n_pairs);
+  if (cap > 65535) { set_error("top2: capacity above 65535"); return MCS_ERR_ARG; }
+  dim3 g((cap + kHamThreads * kQPT - 1) / (kHamThreads * kQPT), n_pairs);
   MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_desc, d_desc,
                  d_counts, d_pairs, (int64_t)cap * bytes, 0, 0, cap, d_best_idx, d_best_dist,
                  d_second_idx, d_second_dist);

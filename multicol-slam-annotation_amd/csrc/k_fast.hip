@@ -20,25 +20,25 @@
 
 namespace mcs {
 
-constexpr int kFW = kMaxCellDim;            // max window side
-constexpr int kFTP = 76;                    // tile row pitch (>= kFW + 6 + 3 alignment slack)
-constexpr int kFTH = kFW + 6;
 constexpr int kChunk = 256;
 
-struct FastWaveLds {
-  uint8_t tile[kFTH * kFTP];
-  uint8_t smap[kFW * kFW];      // score + 1 for corners, 0 otherwise (window raster)
-  uint16_t surv[kChunk];
-  uint16_t corner[2][kChunk];
-};
-
+// Per-wave LDS carve-up, sized on the host from the largest FAST window of the plan (about
+// 31 x 31 px for 30 px cells) so a workgroup needs ~16 KB instead of a 64 px worst case:
+//   tile  [th_max][tp]      window + 3 px halo (+3 bytes alignment slack per row)
+//   smap  [ww*wh]           score + 1 for corners, 0 otherwise (window raster)
+//   surv  u16[kChunk]       compass-test survivors of the current chunk (y<<8 | x)
+//   corner u16[2][kChunk]   corners of the current / previous chunk
 __device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
 __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
-  __shared__ FastWaveLds lds_all[4];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  FastWaveLds& L = lds_all[wv];
+  const int kFTP = a.tile_pitch;
+  uint8_t* const tile = lds_dyn + wv * a.wave_lds;
+  uint8_t* const smap = tile + a.smap_off;
+  uint16_t* const surv = reinterpret_cast<uint16_t*>(tile + a.surv_off);
+  uint16_t* const corner_base = surv + kChunk;
   int f, item;
   const int cells_per_block_row = (a.ncells + 3) / 4;
   if (!xcd_frame_map(blockIdx.x, a.nframes, cells_per_block_row, &f, &item)) return;
@@ -62,18 +62,21 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
   const int ww = max(0, c.wx1 - c.wx0), wh = max(0, c.wy1 - c.wy0);
   const int npx = ww * wh;
   const int th = wh + 6, nd = (ww + 6 + 3) >> 2;
-  // ---- stage tile (window + 3px halo) with aligned dword loads + alignbyte
-  constexpr int kDW = kFTP / 4;  // 19 dword slots per tile row (constant divisor)
-  for (int i = lane; i < th * kDW; i += 64) {
-    const int r = i / kDW, j = i - r * kDW;
-    if (j >= nd) continue;
-    const uintptr_t g = (uintptr_t)(img + (int64_t)(c.wy0 - 3 + r) * pitch + (c.wx0 - 3) + 4 * j);
-    const uint32_t* ap = reinterpret_cast<const uint32_t*>(g & ~(uintptr_t)3);
-    const uint32_t d0 = ap[0], d1 = ap[1];
-    *reinterpret_cast<uint32_t*>(&L.tile[r * kFTP + 4 * j]) =
-        __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(g & 3));
+  // ---- stage tile (window + 3px halo) with aligned dword loads + alignbyte;
+  // row = i / nd by a multiply-high with the cell's magic (exact for i < 2^16)
+  {
+    const uint32_t magic = 0xFFFFFFFFu / (uint32_t)nd + 1u;
+    const uint8_t* gbase = img + (int64_t)(c.wy0 - 3) * pitch + (c.wx0 - 3);
+    for (int i = lane; i < th * nd; i += 64) {
+      const int r = (int)__umulhi((uint32_t)i, magic), j = i - r * nd;
+      const uintptr_t g = (uintptr_t)(gbase + (int64_t)r * pitch + 4 * j);
+      const uint32_t* ap = reinterpret_cast<const uint32_t*>(g & ~(uintptr_t)3);
+      const uint32_t d0 = ap[0], d1 = ap[1];
+      *reinterpret_cast<uint32_t*>(&tile[r * kFTP + 4 * j]) =
+          __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(g & 3));
+    }
   }
-  for (int i = lane; i < (npx + 3) / 4; i += 64) reinterpret_cast<uint32_t*>(L.smap)[i] = 0u;
+  for (int i = lane; i < (npx + 3) / 4; i += 64) reinterpret_cast<uint32_t*>(smap)[i] = 0u;
   dev::wave_sync();
 
   const int t = a.threshold;
@@ -89,9 +92,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
       bool keep = false;
       int x = 0, y = 0, s = 0;
       if (j < nc) {
-        const int pk = L.corner[buf][j];
+        const int pk = corner_base[buf * kChunk + j];
         y = pk >> 8; x = pk & 0xFF;
-        s = L.smap[y * ww + x] - 1;
+        s = smap[y * ww + x] - 1;
         keep = true;
 #pragma unroll
         for (int dy = -1; dy <= 1; dy++)
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
             const int xx = x + dx, yy = y + dy;
             int ns = 0;
             if (xx >= 0 && xx < ww && yy >= 0 && yy < wh) {
-              const int e = L.smap[yy * ww + xx];
+              const int e = smap[yy * ww + xx];
               ns = e ? e - 1 : 0;
             }
             keep = keep && (s > ns);
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
       if (px >= ww) { px -= ww; py++; }
       bool pass = false;
       if (i < npx) {
-        const uint8_t* p = &L.tile[(y + 3) * kFTP + x + 3];
+        const uint8_t* p = &tile[(y + 3) * kFTP + x + 3];
         const int v = p[0];
         const int q0 = p[3 * kFTP], q4 = p[3], q8 = p[-3 * kFTP], q12 = p[-3];
         const int lo = v - t, hi = v + t;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
                (b0 && b4) || (b4 && b8) || (b8 && b12) || (b12 && b0);
       }
       const uint64_t bal = __ballot(pass);
-      if (pass) L.surv[ns + __popcll(bal & dev::lanemask_lt())] = (uint16_t)((y << 8) | x);
+      if (pass) surv[ns + __popcll(bal & dev::lanemask_lt())] = (uint16_t)((y << 8) | x);
       ns += __popcll(bal);
     }
     dev::wave_sync();
@@ -155,9 +158,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
       bool corner = false;
       int idx = 0;
       if (j < ns) {
-        idx = L.surv[j];
+        idx = surv[j];
         const int y = idx >> 8, x = idx & 0xFF;
-        const uint8_t* p = &L.tile[(y + 3) * kFTP + x + 3];
+        const uint8_t* p = &tile[(y + 3) * kFTP + x + 3];
         const int v = p[0];
         int d[16];
         // circle (dx,dy): (0,3),(1,3),(2,2),(3,1),(3,0),(3,-1),(2,-2),(1,-3),(0,-3),(-1,-3),
@@ -184,11 +187,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         corner = dark > t || bright > t;
         if (corner) {
           const int score = max(max(t, dark), bright) - 1;
-          L.smap[y * ww + x] = (uint8_t)(score + 1);
+          smap[y * ww + x] = (uint8_t)(score + 1);
         }
       }
       const uint64_t bal = __ballot(corner);
-      if (corner) L.corner[cur_buf][ncorner + __popcll(bal & dev::lanemask_lt())] = (uint16_t)idx;
+      if (corner) corner_base[cur_buf * kChunk + ncorner + __popcll(bal & dev::lanemask_lt())] = (uint16_t)idx;
       ncorner += __popcll(bal);
     }
     dev::wave_sync();
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
 
 void launch_fast_cells(const FastArgs& a, hipStream_t st) {
   const unsigned g = xcd_grid(a.nframes, (a.ncells + 3) / 4);
-  hipLaunchKernelGGL(k_fast_cells, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_fast_cells, dim3(g), dim3(256), (size_t)4 * a.wave_lds, st, a);
 }
 
 }  // namespace mcs

@@ -14,11 +14,6 @@
 
 namespace mcs {
 
-constexpr int kPTW = 124, kPTH = 16, kPH = 2;   // core tile; halo tile = 128 x 20
-constexpr int kHH = kPTH + 2 * kPH;              // 20 halo rows = 5 per wave
-constexpr int kSrcMaxW = 288, kSrcMaxH = 48;     // source tile bound (scale <= 2.2, host-checked)
-constexpr int kLvlW = kPTW + 8;                  // level tile origin at x0-4 (aligned core)
-
 __device__ __forceinline__ int refl101(int p, int n) {
   p = p < 0 ? -p : p;
   return p >= n ? 2 * n - 2 - p : p;
@@ -39,133 +34,214 @@ __device__ __forceinline__ int vres(int s0, int s1, int b0, int b1, bool simd) {
   return max(0, min(255, v));
 }
 
-// One workgroup = 4 waves; wave w owns halo rows w, w+4, ...; lane owns halo columns
-// lane and lane+64 (their resize coefficients stay in registers, row coefficients are
-// wave-uniform scalars).
+// (2s + 25) / 50 for 2s + 25 <= 12775 (s = 5x5 sum of u8) by multiply-shift;
+// exact: 20972 / 2^20 - 1/50 < 4.6e-7 and 12775 * 4.6e-7 < 1/50 (checked on the host too)
+__device__ __forceinline__ uint32_t div50(uint32_t n) { return (n * 20972u) >> 20; }
+
+// Row-streaming pyramid level: one wave owns a strip of `core` (<= 248) output columns and a
+// segment of `seg_rows` rows.  Lane L holds 4 consecutive pixels [xs-4+4L, xs+4L); lane 0 and
+// the lane after the core are the +-2 px halo of the blur.  Rows are produced top to bottom
+// (with a 2-row halo above and below the segment), each row:
+//   RESIZE: the source rows it needs (yofs[r], yofs[r]+1) are streamed once per wave with
+//           aligned dword loads (one row prefetched ahead), horizontally resized per lane
+//           (coefficients in registers) and kept for the next output row;
+//   level 0: the input row is streamed the same way;
+// then the raw row is written out (RESIZE), horizontal 5-sums go into a per-wave LDS ring of
+// 8 rows, and once row r+2 exists the blurred row r is summed vertically and written.
+// No workgroup barriers: every wave works alone (wave-local LDS ordering only).
+constexpr int kStageDW = 192;    // staged source row (dwords), scale <= 2.2
+constexpr int kRowBufDW = 66;    // raw row bytes of px [xs-4, xs+260)
+constexpr int kRing = 8;
+
+struct PyrWaveLds {
+  uint32_t stage[kStageDW];
+  uint32_t row[kRowBufDW];
+  uint2 ring[kRing][64];
+};
+
 template <bool RESIZE>
-__global__ __launch_bounds__(256) void k_pyr_blur(PyrArgs a) {
-  __shared__ uint8_t s_src[RESIZE ? kSrcMaxH * kSrcMaxW : 4];
-  __shared__ __attribute__((aligned(16))) uint8_t s_lvl[kHH * kLvlW];
-  __shared__ uint16_t s_hs[kHH * kPTW];
+__global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
+  __shared__ PyrWaveLds lds_all[4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  PyrWaveLds& W = lds_all[wv];
   int f, item;
-  if (!xcd_frame_map(blockIdx.x, a.nframes, a.tiles_x * a.tiles_y, &f, &item)) return;
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int x0 = (item % a.tiles_x) * kPTW, y0 = (item / a.tiles_x) * kPTH;
-  const int dw = a.dw, dh = a.dh;
-  const int lrow0 = y0 - kPH;  // s_lvl row 0 <-> level row y0-2
-  const int lcol0 = x0 - 4;    // s_lvl col 0 <-> level col x0-4
+  const int units = a.tiles_x * a.tiles_y;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, (units + 3) / 4, &f, &item)) return;
+  const int unit = item * 4 + wv;
+  if (unit >= units) return;
+  const int strip = unit % a.tiles_x, seg = unit / a.tiles_x;
+  const int dw = a.dw, dh = a.dh, core = a.core;
+  const int xs = strip * core;
+  const int xcore1 = min(xs + core, dw);           // core px [xs, xcore1)
+  const int seg0 = seg * a.seg_rows, seg1 = min(dh, seg0 + a.seg_rows);
+  const int r_begin = max(0, seg0 - 2), r_end = min(dh, seg1 + 2);
+  const int xb = xs - 4 + 4 * lane;                // lane's first pixel
+  const bool core_lane = xb >= xs && xb < xcore1;
   const uint8_t* S = a.src + (int64_t)f * a.src_fstride;
-  const int ry0 = max(0, lrow0), ry1 = min(dh, y0 + kPTH + kPH);
-  const int rx0 = max(0, x0 - kPH), rx1 = min(dw, x0 + kPTW + kPH);
+  uint8_t* const rowb = reinterpret_cast<uint8_t*>(W.row);
+  const uint8_t* const stb = reinterpret_cast<const uint8_t*>(W.stage);
+
+  // source columns staged per row: [c_lo, c_hi]
+  int c_lo, c_hi;
+  int sx[4], sx1[4], a0[4], a1[4];
+  bool simd[4];
+  if (RESIZE) {
+    c_lo = a.xofs[max(xs - 4, 0)];
+    c_hi = min(a.xofs[min(xs + core + 3, dw - 1)] + 1, a.sw - 1);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int p = min(max(xb + k, 0), dw - 1);
+      sx[k] = a.xofs[p] - c_lo;
+      sx1[k] = min(a.xofs[p] + 1, a.sw - 1) - c_lo;
+      a0[k] = a.alpha[2 * p];
+      a1[k] = a.alpha[2 * p + 1];
+      simd[k] = p < a.simd_end;
+    }
+  } else {
+    c_lo = max(xs - 4, 0);
+    c_hi = min(xs + core + 3, dw - 1);
+  }
+  const int nbytes0 = c_hi - c_lo + 1;
+  const int sh = RESIZE ? a.sh : dh;
+
+  // ---- streamed source row: aligned dwords covering [c_lo, c_hi] of row sr
+  auto row_base = [&](int sr) -> const uint8_t* { return S + (int64_t)sr * a.spitch; };
+  auto load_row = [&](int sr, uint32_t (&v)[3]) {
+    const uintptr_t st = (uintptr_t)(row_base(sr) + c_lo);
+    const uint32_t* ap = reinterpret_cast<const uint32_t*>(st & ~(uintptr_t)3);
+    const int ndw = ((int)(st & 3) + nbytes0 + 3) >> 2;
+    const bool last = sr == sh - 1;
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+      const int j = lane + 64 * m;
+      v[m] = 0;
+      if (j < ndw) {
+        const uintptr_t q = (uintptr_t)(ap + j);
+        if (!last || q + 4 <= (uintptr_t)(row_base(sr) + (RESIZE ? a.sw : dw))) {
+          v[m] = ap[j];
+        } else {   // never read past the end of the last row (it may end the buffer)
+          const uintptr_t end = (uintptr_t)(row_base(sr) + (RESIZE ? a.sw : dw));
+          for (int k = 0; k < 4; k++)
+            if (q + k < end) v[m] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(q + k)) << (8 * k);
+        }
+      }
+    }
+  };
+  auto stage_row = [&](const uint32_t (&v)[3]) {
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+      const int j = lane + 64 * m;
+      if (j < kStageDW) W.stage[j] = v[m];
+    }
+  };
+
+  // ---- raw row -> store, horizontal 5-sums into the ring, blurred rows out
+  int next_emit = seg0;
+  uint8_t* const dstf = RESIZE ? a.dst + (int64_t)f * a.dst_fstride : nullptr;
+  uint8_t* const blrf = a.blur + (int64_t)f * a.blur_fstride;
+  auto push_row = [&](int r, uint32_t v) {
+    if (RESIZE && core_lane && r >= seg0 && r < seg1)
+      *reinterpret_cast<uint32_t*>(dstf + (int64_t)r * a.dpitch + xb) = v;
+    W.row[lane] = v;
+    dev::wave_sync();
+    // reflect-101 across the level's left / right border (px -1,-2 and dw, dw+1)
+    if (lane == 0 && xs == 0) { rowb[3] = rowb[5]; rowb[2] = rowb[6]; }
+    if (lane == 1 && xcore1 == dw) {
+      const int ib = dw - (xs - 4);
+      rowb[ib] = rowb[ib - 2];
+      rowb[ib + 1] = rowb[ib - 3];
+    }
+    dev::wave_sync();
+    if (lane >= 1 && lane < kRowBufDW - 1) {
+      const uint32_t L = W.row[lane - 1], C = W.row[lane], R = W.row[lane + 1];
+      const uint32_t sc = __builtin_amdgcn_sad_u8(C, 0u, 0u);
+      const uint32_t l2 = (L >> 16) & 0xFF, l3 = L >> 24, c0 = C & 0xFF, c3 = C >> 24;
+      const uint32_t r0 = R & 0xFF, r1 = (R >> 8) & 0xFF;
+      const uint32_t h0 = sc - c3 + l2 + l3, h1 = sc + l3, h2 = sc + r0, h3 = sc - c0 + r0 + r1;
+      W.ring[r & (kRing - 1)][lane] = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+    }
+    dev::wave_sync();
+    const int upto = (r == dh - 1) ? dh - 1 : r - 2;
+    for (; next_emit <= upto && next_emit < seg1; next_emit++) {
+      const int y = next_emit;
+      uint32_t s01 = 0, s23 = 0;
+#pragma unroll
+      for (int d = -2; d <= 2; d++) {
+        const uint2 h = W.ring[refl101(y + d, dh) & (kRing - 1)][lane];
+        s01 += h.x;   // two u16 lanes, no carry (5 * 1275 < 65536)
+        s23 += h.y;
+      }
+      if (core_lane) {
+        const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |
+                           (div50(2 * (s23 & 0xFFFF) + 25) << 16) | (div50(2 * (s23 >> 16) + 25) << 24);
+        *reinterpret_cast<uint32_t*>(blrf + (int64_t)y * a.bpitch + xb) = o;
+      }
+    }
+  };
 
   if (RESIZE) {
-    const int sh = a.sh, sw = a.sw;
-    const int sr0 = min(max(a.yofs[ry0], 0), sh - 1);
-    const int sr1 = min(max(a.yofs[ry1 - 1] + 1, 0), sh - 1) + 1;
-    const int sc0 = a.xofs[rx0], sc1 = min(a.xofs[rx1 - 1] + 1, sw - 1) + 1;
-    for (int r = wv; r < sr1 - sr0; r += 4) {
-      const uint8_t* srow = S + (int64_t)(sr0 + r) * a.spitch + sc0;
-      for (int c = lane; c < sc1 - sc0; c += 64) s_src[r * kSrcMaxW + c] = srow[c];
-    }
-    // per-lane column coefficients for halo columns lane, lane + 64
-    int sx[2], sx1[2], a0[2], a1[2];
-    bool simd[2], cval[2];
+    // source rows feeding output rows [r_begin, r_end)
+    auto lo_of = [&](int r) { return min(max(a.yofs[r], 0), sh - 1); };
+    auto hi_of = [&](int r) { return min(max(a.yofs[r] + 1, 0), sh - 1); };
+    const int sr0 = lo_of(r_begin), sr1 = hi_of(r_end - 1);
+    int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
+    uint32_t pf[3];
+    load_row(sr0, pf);
+    int r = r_begin;
+    for (int sr = sr0; sr <= sr1; sr++) {
+      uint32_t cur[3] = {pf[0], pf[1], pf[2]};
+      if (sr < sr1) load_row(sr + 1, pf);
+      const int shft = (int)(((uintptr_t)(row_base(sr) + c_lo)) & 3);
+      stage_row(cur);
+      dev::wave_sync();
 #pragma unroll
-    for (int m = 0; m < 2; m++) {
-      const int c = x0 - kPH + lane + 64 * m;
-      cval[m] = c >= rx0 && c < rx1;
-      const int cc = cval[m] ? c : rx0;
-      sx[m] = a.xofs[cc] - sc0;
-      sx1[m] = min(a.xofs[cc] + 1, sw - 1) - sc0;
-      a0[m] = a.alpha[2 * cc];
-      a1[m] = a.alpha[2 * cc + 1];
-      simd[m] = cc < a.simd_end;
-    }
-    __syncthreads();
-    for (int r = ry0 + wv; r < ry1; r += 4) {
-      const int sy = a.yofs[r];
-      const int b0 = a.beta[2 * r], b1 = a.beta[2 * r + 1];
-      const uint8_t* r0 = s_src + (min(max(sy, 0), sh - 1) - sr0) * kSrcMaxW;
-      const uint8_t* r1 = s_src + (min(max(sy + 1, 0), sh - 1) - sr0) * kSrcMaxW;
-      uint8_t* out = s_lvl + (r - lrow0) * kLvlW + (x0 - kPH - lcol0);
+      for (int k = 0; k < 4; k++) {
+        hprev[k] = hcur[k];
+        hcur[k] = stb[shft + sx[k]] * a0[k] + stb[shft + sx1[k]] * a1[k];
+      }
+      dev::wave_sync();
+      for (; r < r_end && hi_of(r) == sr; r++) {
+        const bool same = lo_of(r) == sr;
+        const int b0 = a.beta[2 * r], b1 = a.beta[2 * r + 1];
+        uint32_t v = 0;
 #pragma unroll
-      for (int m = 0; m < 2; m++) {
-        if (!cval[m]) continue;
-        const int s0 = r0[sx[m]] * a0[m] + r0[sx1[m]] * a1[m];
-        const int s1 = r1[sx[m]] * a0[m] + r1[sx1[m]] * a1[m];
-        out[lane + 64 * m] = (uint8_t)vres(s0, s1, b0, b1, simd[m]);
+        for (int k = 0; k < 4; k++) {
+          const int s0 = same ? hcur[k] : hprev[k];
+          v |= (uint32_t)vres(s0, hcur[k], b0, b1, simd[k]) << (8 * k);
+        }
+        push_row(r, v);
       }
     }
   } else {
-    for (int r = ry0 + wv; r < ry1; r += 4) {
-      const uint8_t* srow = S + (int64_t)r * a.spitch;
-      uint8_t* out = s_lvl + (r - lrow0) * kLvlW;
-#pragma unroll
-      for (int m = 0; m < 2; m++) {
-        const int c = x0 - kPH + lane + 64 * m;
-        if (c >= rx0 && c < rx1) out[c - lcol0] = srow[c];
+    uint32_t pf[3];
+    load_row(r_begin, pf);
+    for (int r = r_begin; r < r_end; r++) {
+      uint32_t cur[3] = {pf[0], pf[1], pf[2]};
+      if (r + 1 < r_end) load_row(r + 1, pf);
+      const int shft = (int)(((uintptr_t)(row_base(r) + c_lo)) & 3);
+      stage_row(cur);
+      dev::wave_sync();
+      // lane's 4 px [xb, xb+4) sit at staged byte shft + (xb - c_lo); px outside the level
+      // are replaced by the border reflection in push_row
+      const int o = shft + (xb - c_lo);
+      uint32_t v = 0;
+      if (o >= 0 && o + 4 <= 4 * kStageDW) {
+        const uint32_t w0 = W.stage[o >> 2], w1 = W.stage[min((o >> 2) + 1, kStageDW - 1)];
+        v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(o & 3));
       }
-    }
-  }
-  __syncthreads();
-  // raw level-l core tile -> HBM (aligned dwords: 31 per row, 16 rows)
-  if (RESIZE) {
-    for (int i = tid; i < kPTH * (kPTW / 4); i += 256) {
-      const int ty = i / (kPTW / 4), tx = (i % (kPTW / 4)) * 4;
-      const int y = y0 + ty;
-      if (y < dh && x0 + tx < dw) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(&s_lvl[(ty + kPH) * kLvlW + 4 + tx]);
-        *reinterpret_cast<uint32_t*>(a.dst + (int64_t)f * a.dst_fstride + (int64_t)y * a.dpitch + x0 + tx) = v;
-      }
-    }
-  }
-  // horizontal 5-sums (reflect-101 only at the level border), core columns
-  for (int r = ry0 + wv; r < ry1; r += 4) {
-    const uint8_t* row = s_lvl + (r - lrow0) * kLvlW;
-#pragma unroll
-    for (int m = 0; m < 2; m++) {
-      const int cl = lane + 64 * m;
-      if (cl >= kPTW) continue;
-      const int c = x0 + cl;
-      int s = 0;
-      if (c < dw) {
-        if (c >= 2 && c < dw - 2) {
-          const uint8_t* q = row + (c - lcol0);
-          s = q[-2] + q[-1] + q[0] + q[1] + q[2];
-        } else {
-#pragma unroll
-          for (int d = -2; d <= 2; d++) s += row[refl101(c + d, dw) - lcol0];
-        }
-      }
-      s_hs[(r - lrow0) * kPTW + cl] = (uint16_t)s;
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < kPTH * (kPTW / 4); i += 256) {
-    const int ty = i / (kPTW / 4), tx = (i % (kPTW / 4)) * 4;
-    const int y = y0 + ty;
-    if (y < dh && x0 + tx < dw) {
-      int rr[5];
-#pragma unroll
-      for (int d = -2; d <= 2; d++) rr[d + 2] = (refl101(y + d, dh) - lrow0) * kPTW;
-      uint32_t packed = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int s = s_hs[rr[0] + tx + k] + s_hs[rr[1] + tx + k] + s_hs[rr[2] + tx + k] +
-                      s_hs[rr[3] + tx + k] + s_hs[rr[4] + tx + k];
-        packed |= (uint32_t)((2 * s + 25) / 50) << (8 * k);
-      }
-      *reinterpret_cast<uint32_t*>(a.blur + (int64_t)f * a.blur_fstride + (int64_t)y * a.bpitch + x0 + tx) = packed;
+      dev::wave_sync();
+      push_row(r, v);
     }
   }
 }
 
-void launch_pyr_blur(const PyrArgs& a, bool resize, hipStream_t st) {
-  const unsigned g = xcd_grid(a.nframes, a.tiles_x * a.tiles_y);
+void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st) {
+  (void)wide;
+  const unsigned g = xcd_grid(a.nframes, (a.tiles_x * a.tiles_y + 3) / 4);
   if (resize)
-    hipLaunchKernelGGL(k_pyr_blur<true>, dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_pyr_rows<true>, dim3(g), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(k_pyr_blur<false>, dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_pyr_rows<false>, dim3(g), dim3(256), 0, st, a);
 }
 
 // ---------------------------------------------------------------------------

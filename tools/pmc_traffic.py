@@ -47,16 +47,19 @@ def main(fetch_csv, write_csv, out_json):
             "write": (sum(w) / len(w) * 1024) if w else None,
         }
     k = out["kernels"]
-    # per extractor call: 7 resize launches (one per level 1..7) + 1 FAST launch
-    rs = k.get("k_resize_linear")
+    # per extractor call (= one k_fast_cells launch): every k_pyr_blur<true> launch of the
+    # call (one per level 1..L-1: resize + fused blur) + the FAST launch
     fa = k.get("k_fast_cells")
-    if rs and fa:
-        nres = 7
-        rd = rs["fetch_raw"] * nres + fa["fetch_raw"]
-        rd2 = rs["fetch_x2"] * nres + fa["fetch_x2"]
-        wt = rs["write"] * nres + (fa["write"] or 0)
-        out["pyramid+fast_bytes_per_call"] = rd + wt
-        out["pyramid+fast_bytes_per_call_x2read"] = rd2 + wt
+    rs = next((v for n, v in k.items() if n.startswith(("k_pyr_blur<true", "k_pyr_rows<true"))), None)
+    if rs and fa and fa["launches"]:
+        per_call = rs["launches"] / fa["launches"]
+        rd = rs["fetch_raw"] * per_call + fa["fetch_raw"]
+        rd2 = rs["fetch_x2"] * per_call + fa["fetch_x2"]
+        wt = rs["write"] * per_call + (fa["write"] or 0)
+        out["pyr_launches_per_call"] = per_call
+        out["pyramid+fast_bytes_per_call_rawread"] = rd + wt
+        # reported figure: gfx950 x2 read correction (MI355X_MICROARCH.md "HBM")
+        out["pyramid+fast_bytes_per_call"] = rd2 + wt
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
