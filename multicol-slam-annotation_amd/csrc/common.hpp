@@ -33,6 +33,13 @@ namespace dev {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Round a byte pointer down to its dword.  Pointer arithmetic (not an integer round trip)
+// keeps the global address space, so loads stay global_load (a flat_load also counts on
+// lgkmcnt and every LDS wait would then wait for it).
+__device__ __forceinline__ const uint32_t* align_down4(const uint8_t* p) {
+  return reinterpret_cast<const uint32_t*>(p - ((uintptr_t)p & 3));
+}
+
 // LDS ordering between lanes of ONE wave (no cross-wave barrier)
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

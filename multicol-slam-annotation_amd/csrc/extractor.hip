@@ -109,7 +109,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     }
     a.blur = h->d_blur + D.img_off; a.blur_fstride = pl.img_frame_bytes; a.bpitch = D.bpitch;
     a.dw = D.w; a.dh = D.h;
-    pyr_strips(D.w, D.h, a);
+    pyr_strips(D.w, D.h, F, a);
     a.nframes = F;
     return a;
   };

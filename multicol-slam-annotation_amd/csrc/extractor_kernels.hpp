@@ -1,6 +1,7 @@
 // Kernel argument blocks and launch wrappers of the extractor pipeline (one .hip file per
 // stage; the host orchestration lives in extractor.hip).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "extractor_plan.hpp"
@@ -33,15 +34,22 @@ struct PyrArgs {
   const int32_t* xofs; const int16_t* alpha; const int32_t* yofs; const int16_t* beta;
   int simd_end;
   int tiles_x, tiles_y, nframes;   // tiles_x = column strips, tiles_y = row segments
-  int core, seg_rows;              // strip width (px, multiple of 4, <= 248), segment height
+  int core, seg_rows;              // strip width (px, multiple of 4, <= 244), segment height
 };
-// strips of <= 248 columns (62 lanes x 4 px), segments of 48 rows
-inline void pyr_strips(int dw, int dh, PyrArgs& a) {
-  const int n = (dw + 247) / 248;
+// strips of <= 244 columns (61 lanes x 4 px, so a level-0 strip + halo is <= 64 dwords);
+// segment height chosen so that a batch of F
+// frames gives ~16k waves (latency hiding), between 16 and 64 rows
+inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
+  const int n = (dw + 243) / 244;
   a.core = ((dw + n - 1) / n + 3) & ~3;
   a.tiles_x = (dw + a.core - 1) / a.core;
-  a.seg_rows = 48;
-  a.tiles_y = (dh + a.seg_rows - 1) / a.seg_rows;
+  const long target = 16384;
+  const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
+  const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
+  int rows = (dh + segs - 1) / segs;
+  rows = std::min(64, std::max(16, rows));
+  a.seg_rows = rows;
+  a.tiles_y = (dh + rows - 1) / rows;
 }
 // wide: source tiles for scale factors in (1.5, 2.2] (larger LDS footprint)
 void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st);

@@ -78,9 +78,8 @@ constexpr int kBlrW = 12;   // dwords per blurred patch row (43 bytes + alignmen
 constexpr int kBlrH = 43;
 
 __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
-  const uintptr_t u = (uintptr_t)g;
-  const uint32_t* ap = reinterpret_cast<const uint32_t*>(u & ~(uintptr_t)3);
-  return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)(u & 3));
+  const uint32_t* ap = dev::align_down4(g);
+  return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)((uintptr_t)g & 3));
 }
 
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {

@@ -69,11 +69,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     const uint8_t* gbase = img + (int64_t)(c.wy0 - 3) * pitch + (c.wx0 - 3);
     for (int i = lane; i < th * nd; i += 64) {
       const int r = (int)__umulhi((uint32_t)i, magic), j = i - r * nd;
-      const uintptr_t g = (uintptr_t)(gbase + (int64_t)r * pitch + 4 * j);
-      const uint32_t* ap = reinterpret_cast<const uint32_t*>(g & ~(uintptr_t)3);
+      const uint8_t* gp = gbase + (int64_t)r * pitch + 4 * j;
+      const uint32_t* ap = dev::align_down4(gp);
       const uint32_t d0 = ap[0], d1 = ap[1];
       *reinterpret_cast<uint32_t*>(&tile[r * kFTP + 4 * j]) =
-          __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(g & 3));
+          __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)((uintptr_t)gp & 3));
     }
   }
   for (int i = lane; i < (npx + 3) / 4; i += 64) reinterpret_cast<uint32_t*>(smap)[i] = 0u;

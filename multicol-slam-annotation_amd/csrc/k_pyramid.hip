@@ -38,32 +38,30 @@ __device__ __forceinline__ int vres(int s0, int s1, int b0, int b1, bool simd) {
 // exact: 20972 / 2^20 - 1/50 < 4.6e-7 and 12775 * 4.6e-7 < 1/50 (checked on the host too)
 __device__ __forceinline__ uint32_t div50(uint32_t n) { return (n * 20972u) >> 20; }
 
-// Row-streaming pyramid level: one wave owns a strip of `core` (<= 248) output columns and a
+// Row-streaming pyramid level: one wave owns a strip of `core` (<= 244) output columns and a
 // segment of `seg_rows` rows.  Lane L holds 4 consecutive pixels [xs-4+4L, xs+4L); lane 0 and
-// the lane after the core are the +-2 px halo of the blur.  Rows are produced top to bottom
-// (with a 2-row halo above and below the segment), each row:
-//   RESIZE: the source rows it needs (yofs[r], yofs[r]+1) are streamed once per wave with
-//           aligned dword loads (one row prefetched ahead), horizontally resized per lane
-//           (coefficients in registers) and kept for the next output row;
-//   level 0: the input row is streamed the same way;
-// then the raw row is written out (RESIZE), horizontal 5-sums go into a per-wave LDS ring of
-// 8 rows, and once row r+2 exists the blurred row r is summed vertically and written.
-// No workgroup barriers: every wave works alone (wave-local LDS ordering only).
+// the lane after the core are the +-2 px halo of the blur.  A pixel outside the level holds
+// the value of its BORDER_REFLECT_101 mirror (computed from the mirror's own coordinates),
+// so the horizontal 5-sum needs no border cases.  Rows are produced top to bottom with a
+// 2-row halo above and below the segment:
+//   RESIZE: every source row the segment needs is streamed once per wave with aligned dword
+//           loads (two rows in flight), staged in wave-private LDS, and horizontally resized
+//           per lane (coefficients in registers); an output row combines the last two;
+//   level 0: the input row is streamed the same way.
+// Each raw row is written out (RESIZE); its horizontal 5-sums (lane neighbours by shuffle)
+// enter a 5-row register window; once row r+2 exists the blurred row r is written.
+// No workgroup barriers: every wave works alone.
 constexpr int kStageDW = 192;    // staged source row (dwords), scale <= 2.2
-constexpr int kRowBufDW = 66;    // raw row bytes of px [xs-4, xs+260)
-constexpr int kRing = 8;
+constexpr int kPF = 4;           // source rows in flight per wave
 
-struct PyrWaveLds {
-  uint32_t stage[kStageDW];
-  uint32_t row[kRowBufDW];
-  uint2 ring[kRing][64];
-};
-
-template <bool RESIZE>
+// NDW = staged dwords per lane per source row: 1 (level 0, core <= 244), 2 (scale <= 1.5),
+// 3 (scale <= 2.2)
+template <bool RESIZE, int NDW>
 __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
-  __shared__ PyrWaveLds lds_all[4];
+  __shared__ uint32_t lds_stage[4][kStageDW];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  PyrWaveLds& W = lds_all[wv];
+  uint32_t* const stage = lds_stage[wv];
+  const uint8_t* const stb = reinterpret_cast<const uint8_t*>(stage);
   int f, item;
   const int units = a.tiles_x * a.tiles_y;
   if (!xcd_frame_map(blockIdx.x, a.nframes, (units + 3) / 4, &f, &item)) return;
@@ -78,170 +76,215 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
   const int xb = xs - 4 + 4 * lane;                // lane's first pixel
   const bool core_lane = xb >= xs && xb < xcore1;
   const uint8_t* S = a.src + (int64_t)f * a.src_fstride;
-  uint8_t* const rowb = reinterpret_cast<uint8_t*>(W.row);
-  const uint8_t* const stb = reinterpret_cast<const uint8_t*>(W.stage);
+  const int sh = RESIZE ? a.sh : dh, swid = RESIZE ? a.sw : dw;
 
-  // source columns staged per row: [c_lo, c_hi]
+  // staged source columns [c_lo, c_hi]; per pixel: the (mirrored) column(s) it reads
   int c_lo, c_hi;
   int sx[4], sx1[4], a0[4], a1[4];
   bool simd[4];
   if (RESIZE) {
+    // mirrors of the strip's pixels stay inside [xs-4, xs+core+4) clamped to the level
     c_lo = a.xofs[max(xs - 4, 0)];
     c_hi = min(a.xofs[min(xs + core + 3, dw - 1)] + 1, a.sw - 1);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const int p = min(max(xb + k, 0), dw - 1);
+      const int p = min(max(refl101(xb + k, dw), 0), dw - 1);
       sx[k] = a.xofs[p] - c_lo;
       sx1[k] = min(a.xofs[p] + 1, a.sw - 1) - c_lo;
       a0[k] = a.alpha[2 * p];
       a1[k] = a.alpha[2 * p + 1];
       simd[k] = p < a.simd_end;
+      // lanes outside the strip's halo read garbage, but always inside the staged row
+      sx[k] = min(max(sx[k], 0), c_hi - c_lo);
+      sx1[k] = min(max(sx1[k], 0), c_hi - c_lo);
     }
   } else {
     c_lo = max(xs - 4, 0);
     c_hi = min(xs + core + 3, dw - 1);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      sx[k] = min(max(min(max(refl101(xb + k, dw), 0), dw - 1) - c_lo, 0), c_hi - c_lo);
+      sx1[k] = 0; a0[k] = a1[k] = 0; simd[k] = false;
+    }
   }
   const int nbytes0 = c_hi - c_lo + 1;
-  const int sh = RESIZE ? a.sh : dh;
 
-  // ---- streamed source row: aligned dwords covering [c_lo, c_hi] of row sr
+  // ---- streamed source rows: aligned dwords covering [c_lo, c_hi]
   auto row_base = [&](int sr) -> const uint8_t* { return S + (int64_t)sr * a.spitch; };
-  auto load_row = [&](int sr, uint32_t (&v)[3]) {
-    const uintptr_t st = (uintptr_t)(row_base(sr) + c_lo);
-    const uint32_t* ap = reinterpret_cast<const uint32_t*>(st & ~(uintptr_t)3);
-    const int ndw = ((int)(st & 3) + nbytes0 + 3) >> 2;
+  auto load_row = [&](int sr, uint32_t (&v)[NDW]) {
+    const uint8_t* rb = row_base(sr);
+    const uint8_t* st = rb + c_lo;
+    const uint32_t* ap = dev::align_down4(st);
+    const int ndw = ((int)((uintptr_t)st & 3) + nbytes0 + 3) >> 2;
+    // the last row may end the buffer: only its fully valid dwords are loaded directly
+    // (indices clamped, so the loads are unconditional and stay in flight), the partial
+    // tail dword is assembled bytewise
     const bool last = sr == sh - 1;
+    const int lim = last ? (int)((rb + swid) - reinterpret_cast<const uint8_t*>(ap)) : 4 * ndw;
+    const int jfull = max(0, min(ndw, lim >> 2) - 1);
 #pragma unroll
-    for (int m = 0; m < 3; m++) {
-      const int j = lane + 64 * m;
-      v[m] = 0;
-      if (j < ndw) {
-        const uintptr_t q = (uintptr_t)(ap + j);
-        if (!last || q + 4 <= (uintptr_t)(row_base(sr) + (RESIZE ? a.sw : dw))) {
-          v[m] = ap[j];
-        } else {   // never read past the end of the last row (it may end the buffer)
-          const uintptr_t end = (uintptr_t)(row_base(sr) + (RESIZE ? a.sw : dw));
-          for (int k = 0; k < 4; k++)
-            if (q + k < end) v[m] |= (uint32_t)(*reinterpret_cast<const uint8_t*>(q + k)) << (8 * k);
+    for (int m = 0; m < NDW; m++) v[m] = ap[min(lane + 64 * m, jfull)];
+    if (last && (lim & 3)) {
+#pragma unroll
+      for (int m = 0; m < NDW; m++) {
+        const int j = lane + 64 * m;
+        if (j == (lim >> 2) && j < ndw) {
+          const uint8_t* q = reinterpret_cast<const uint8_t*>(ap + j);
+          uint32_t x = 0;
+          for (int k = 0; k < (lim & 3); k++) x |= (uint32_t)q[k] << (8 * k);
+          v[m] = x;
         }
       }
     }
   };
-  auto stage_row = [&](const uint32_t (&v)[3]) {
+  // stage a row and read this lane's 4 (mirrored) source bytes / resized values
+  auto stage_and_gather = [&](int sr, const uint32_t (&v)[NDW], int (&h)[4]) {
+    const int shft = (int)((uintptr_t)(row_base(sr) + c_lo) & 3);
 #pragma unroll
-    for (int m = 0; m < 3; m++) {
-      const int j = lane + 64 * m;
-      if (j < kStageDW) W.stage[j] = v[m];
+    for (int m = 0; m < NDW; m++) stage[lane + 64 * m] = v[m];
+    dev::wave_sync();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (RESIZE) h[k] = stb[shft + sx[k]] * a0[k] + stb[shft + sx1[k]] * a1[k];
+      else h[k] = stb[shft + sx[k]];
     }
+    dev::wave_sync();
   };
 
-  // ---- raw row -> store, horizontal 5-sums into the ring, blurred rows out
-  int next_emit = seg0;
+  // ---- raw row -> store, horizontal 5-sums, 5-row window, blurred rows out
   uint8_t* const dstf = RESIZE ? a.dst + (int64_t)f * a.dst_fstride : nullptr;
   uint8_t* const blrf = a.blur + (int64_t)f * a.blur_fstride;
+  uint32_t win[5][2];   // packed u16 5-sums of raw rows r-4..r (win[4] = newest)
+#pragma unroll
+  for (int i = 0; i < 5; i++) win[i][0] = win[i][1] = 0;
+  int next_emit = seg0;
+  auto emit = [&](int y, int r) {
+    uint32_t s01 = 0, s23 = 0;
+    if (y - 2 >= 0 && y + 2 <= dh - 1) {   // interior: window rows r-4..r == y-2..y+2
+#pragma unroll
+      for (int i = 0; i < 5; i++) { s01 += win[i][0]; s23 += win[i][1]; }
+    } else {
+#pragma unroll
+      for (int d = -2; d <= 2; d++) {
+        const int idx = refl101(y + d, dh) - (r - 4);
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+          if (i == idx) { s01 += win[i][0]; s23 += win[i][1]; }
+      }
+    }
+    if (core_lane) {
+      const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |
+                         (div50(2 * (s23 & 0xFFFF) + 25) << 16) | (div50(2 * (s23 >> 16) + 25) << 24);
+      *reinterpret_cast<uint32_t*>(blrf + (int64_t)y * a.bpitch + xb) = o;
+    }
+  };
   auto push_row = [&](int r, uint32_t v) {
     if (RESIZE && core_lane && r >= seg0 && r < seg1)
       *reinterpret_cast<uint32_t*>(dstf + (int64_t)r * a.dpitch + xb) = v;
-    W.row[lane] = v;
-    dev::wave_sync();
-    // reflect-101 across the level's left / right border (px -1,-2 and dw, dw+1)
-    if (lane == 0 && xs == 0) { rowb[3] = rowb[5]; rowb[2] = rowb[6]; }
-    if (lane == 1 && xcore1 == dw) {
-      const int ib = dw - (xs - 4);
-      rowb[ib] = rowb[ib - 2];
-      rowb[ib + 1] = rowb[ib - 3];
-    }
-    dev::wave_sync();
-    if (lane >= 1 && lane < kRowBufDW - 1) {
-      const uint32_t L = W.row[lane - 1], C = W.row[lane], R = W.row[lane + 1];
-      const uint32_t sc = __builtin_amdgcn_sad_u8(C, 0u, 0u);
-      const uint32_t l2 = (L >> 16) & 0xFF, l3 = L >> 24, c0 = C & 0xFF, c3 = C >> 24;
-      const uint32_t r0 = R & 0xFF, r1 = (R >> 8) & 0xFF;
-      const uint32_t h0 = sc - c3 + l2 + l3, h1 = sc + l3, h2 = sc + r0, h3 = sc - c0 + r0 + r1;
-      W.ring[r & (kRing - 1)][lane] = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
-    }
-    dev::wave_sync();
-    const int upto = (r == dh - 1) ? dh - 1 : r - 2;
-    for (; next_emit <= upto && next_emit < seg1; next_emit++) {
-      const int y = next_emit;
-      uint32_t s01 = 0, s23 = 0;
+    const uint32_t L = __shfl_up(v, 1), R = __shfl_down(v, 1);
+    const uint32_t sc = __builtin_amdgcn_sad_u8(v, 0u, 0u);
+    const uint32_t l2 = (L >> 16) & 0xFF, l3 = L >> 24, c0 = v & 0xFF, c3 = v >> 24;
+    const uint32_t r0 = R & 0xFF, r1 = (R >> 8) & 0xFF;
+    const uint32_t h0 = sc - c3 + l2 + l3, h1 = sc + l3, h2 = sc + r0, h3 = sc - c0 + r0 + r1;
 #pragma unroll
-      for (int d = -2; d <= 2; d++) {
-        const uint2 h = W.ring[refl101(y + d, dh) & (kRing - 1)][lane];
-        s01 += h.x;   // two u16 lanes, no carry (5 * 1275 < 65536)
-        s23 += h.y;
-      }
-      if (core_lane) {
-        const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |
-                           (div50(2 * (s23 & 0xFFFF) + 25) << 16) | (div50(2 * (s23 >> 16) + 25) << 24);
-        *reinterpret_cast<uint32_t*>(blrf + (int64_t)y * a.bpitch + xb) = o;
-      }
-    }
+    for (int i = 0; i < 4; i++) { win[i][0] = win[i + 1][0]; win[i][1] = win[i + 1][1]; }
+    win[4][0] = h0 | (h1 << 16);
+    win[4][1] = h2 | (h3 << 16);
+    const int upto = (r == dh - 1) ? dh - 1 : r - 2;
+    for (; next_emit <= upto && next_emit < seg1; next_emit++) emit(next_emit, r);
+  };
+  auto pack4 = [&](const int (&h)[4]) {
+    return (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
   };
 
+  uint32_t pf[kPF][NDW];
   if (RESIZE) {
-    // source rows feeding output rows [r_begin, r_end)
-    auto lo_of = [&](int r) { return min(max(a.yofs[r], 0), sh - 1); };
-    auto hi_of = [&](int r) { return min(max(a.yofs[r] + 1, 0), sh - 1); };
-    const int sr0 = lo_of(r_begin), sr1 = hi_of(r_end - 1);
+    // the segment's row tables (<= 68 rows) live in two VGPRs per lane and are read with
+    // v_readlane (wave-uniform row index): no scalar-memory round trip per output row
+    const int nrows = r_end - r_begin;
+    uint32_t tabA = 0, tabB = 0, betA = 0, betB = 0;
+    {
+      auto pack_rows = [&](int r) {
+        const int lo = min(max(a.yofs[r], 0), sh - 1), hi = min(max(a.yofs[r] + 1, 0), sh - 1);
+        return (uint32_t)lo | ((uint32_t)hi << 16);
+      };
+      auto pack_beta = [&](int r) {
+        return (uint32_t)(uint16_t)a.beta[2 * r] | ((uint32_t)(uint16_t)a.beta[2 * r + 1] << 16);
+      };
+      if (lane < nrows) { tabA = pack_rows(r_begin + lane); betA = pack_beta(r_begin + lane); }
+      if (lane + 64 < nrows) { tabB = pack_rows(r_begin + 64 + lane); betB = pack_beta(r_begin + 64 + lane); }
+    }
+    auto row_tab = [&](int r) -> uint32_t {
+      const int i = r - r_begin;
+      return i < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)tabA, i)
+                    : (uint32_t)__builtin_amdgcn_readlane((int)tabB, i - 64);
+    };
+    auto row_beta = [&](int r) -> uint32_t {
+      const int i = r - r_begin;
+      return i < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)betA, i)
+                    : (uint32_t)__builtin_amdgcn_readlane((int)betB, i - 64);
+    };
+    const int sr0 = (int)(row_tab(r_begin) & 0xFFFF), sr1 = (int)(row_tab(r_end - 1) >> 16);
     int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
-    uint32_t pf[3];
-    load_row(sr0, pf);
     int r = r_begin;
-    for (int sr = sr0; sr <= sr1; sr++) {
-      uint32_t cur[3] = {pf[0], pf[1], pf[2]};
-      if (sr < sr1) load_row(sr + 1, pf);
-      const int shft = (int)(((uintptr_t)(row_base(sr) + c_lo)) & 3);
-      stage_row(cur);
-      dev::wave_sync();
+    uint32_t t = row_tab(r);
+    auto consume = [&](int sr, const uint32_t (&v)[NDW]) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        hprev[k] = hcur[k];
-        hcur[k] = stb[shft + sx[k]] * a0[k] + stb[shft + sx1[k]] * a1[k];
+      for (int k = 0; k < 4; k++) hprev[k] = hcur[k];
+      stage_and_gather(sr, v, hcur);
+      while (r < r_end && (int)(t >> 16) == sr) {
+        const bool same = (int)(t & 0xFFFF) == sr;
+        const uint32_t bb = row_beta(r);
+        const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
+        int o[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, simd[k]);
+        push_row(r, pack4(o));
+        r++;
+        if (r < r_end) t = row_tab(r);
       }
-      dev::wave_sync();
-      for (; r < r_end && hi_of(r) == sr; r++) {
-        const bool same = lo_of(r) == sr;
-        const int b0 = a.beta[2 * r], b1 = a.beta[2 * r + 1];
-        uint32_t v = 0;
+    };
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int s0 = same ? hcur[k] : hprev[k];
-          v |= (uint32_t)vres(s0, hcur[k], b0, b1, simd[k]) << (8 * k);
+    for (int u = 0; u < kPF; u++)
+      if (sr0 + u <= sr1) load_row(sr0 + u, pf[u]);
+    for (int sr = sr0; sr <= sr1; sr += kPF) {   // kPF source rows in flight
+#pragma unroll
+      for (int u = 0; u < kPF; u++) {
+        if (sr + u <= sr1) {
+          consume(sr + u, pf[u]);
+          if (sr + u + kPF <= sr1) load_row(sr + u + kPF, pf[u]);
         }
-        push_row(r, v);
       }
     }
   } else {
-    uint32_t pf[3];
-    load_row(r_begin, pf);
-    for (int r = r_begin; r < r_end; r++) {
-      uint32_t cur[3] = {pf[0], pf[1], pf[2]};
-      if (r + 1 < r_end) load_row(r + 1, pf);
-      const int shft = (int)(((uintptr_t)(row_base(r) + c_lo)) & 3);
-      stage_row(cur);
-      dev::wave_sync();
-      // lane's 4 px [xb, xb+4) sit at staged byte shft + (xb - c_lo); px outside the level
-      // are replaced by the border reflection in push_row
-      const int o = shft + (xb - c_lo);
-      uint32_t v = 0;
-      if (o >= 0 && o + 4 <= 4 * kStageDW) {
-        const uint32_t w0 = W.stage[o >> 2], w1 = W.stage[min((o >> 2) + 1, kStageDW - 1)];
-        v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(o & 3));
+    auto consume = [&](int r, const uint32_t (&v)[NDW]) {
+      int h[4];
+      stage_and_gather(r, v, h);
+      push_row(r, pack4(h));
+    };
+#pragma unroll
+    for (int u = 0; u < kPF; u++)
+      if (r_begin + u < r_end) load_row(r_begin + u, pf[u]);
+    for (int r = r_begin; r < r_end; r += kPF) {
+#pragma unroll
+      for (int u = 0; u < kPF; u++) {
+        if (r + u < r_end) {
+          consume(r + u, pf[u]);
+          if (r + u + kPF < r_end) load_row(r + u + kPF, pf[u]);
+        }
       }
-      dev::wave_sync();
-      push_row(r, v);
     }
   }
 }
 
 void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st) {
-  (void)wide;
   const unsigned g = xcd_grid(a.nframes, (a.tiles_x * a.tiles_y + 3) / 4);
-  if (resize)
-    hipLaunchKernelGGL(k_pyr_rows<true>, dim3(g), dim3(256), 0, st, a);
+  if (!resize)
+    hipLaunchKernelGGL((k_pyr_rows<false, 1>), dim3(g), dim3(256), 0, st, a);
+  else if (!wide)
+    hipLaunchKernelGGL((k_pyr_rows<true, 2>), dim3(g), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(k_pyr_rows<false>, dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_pyr_rows<true, 3>), dim3(g), dim3(256), 0, st, a);
 }
 
 // ---------------------------------------------------------------------------
