@@ -52,6 +52,17 @@ typedef struct mcs_keypoint {
   int32_t octave, class_id;
 } mcs_keypoint;
 
+/* Scaramuzza omni camera model (cCamModelGeneral_, include/cam_model_omni.h:36-147,
+ * src/cam_model_omni.cpp:49-163), needed by the dBRIEF / mdBRIEF descriptors: keypoints are
+ * undistorted with ImgToWorld (undistortPointsOcam, scale p[0]) and the rotated pattern is
+ * re-distorted with WorldToImg at z = -p[0] (distortPointsOcam). */
+typedef struct mcs_cam_model {
+  double c, d, e, u0, v0;        /* affine parameters and principal point */
+  int32_t p_deg, invp_deg;       /* number of coefficients in p / invp (<= 16 each) */
+  double p[16];                  /* forward polynomial (ImgToWorld); p[0] = p1 */
+  double invp[16];               /* inverse polynomial (WorldToImg), Horner in theta */
+} mcs_cam_model;
+
 typedef struct mcs_extractor mcs_extractor;
 
 /* Fill *p with the reference constructor defaults (include/mdBRIEFextractorOct.h:339-351). */
@@ -92,6 +103,19 @@ int mcs_extractor_set_masks_device(mcs_extractor* h, const uint8_t* d_masks, int
 int mcs_extract_batch_device(mcs_extractor* h, const uint8_t* d_images, int32_t n_frames,
                              const int32_t* d_mask_index, mcs_keypoint* d_kps,
                              int32_t* d_counts, uint8_t* d_desc, void* stream);
+
+/* Camera models for the dBRIEF / mdBRIEF descriptors (do_dbrief / learn_masks), one per
+ * camera; a frame uses the model of its mask index (model 0 for mcs_extract).  Host memory,
+ * copied.  Required before extracting with do_dbrief or learn_masks set. */
+int mcs_extractor_set_cam_models(mcs_extractor* h, const mcs_cam_model* models, int32_t n);
+
+/* mcs_extract_batch_device with the descriptor masks of mdBRIEF (learn_masks; all-zero for
+ * ORB and dBRIEF, as the reference's Mat::zeros): d_desc_masks [n_frames][cap][desc_size]
+ * (nullable).  d_cam_index doubles as mask and camera-model index. */
+int mcs_extract_batch_device_ex(mcs_extractor* h, const uint8_t* d_images, int32_t n_frames,
+                                const int32_t* d_cam_index, mcs_keypoint* d_kps,
+                                int32_t* d_counts, uint8_t* d_desc, uint8_t* d_desc_masks,
+                                void* stream);
 
 /* Stage read-back for parity tests (synchronous; reads the workspace of the LAST batch
  * or single-frame call).  stage 0: pyramid level image (w*h bytes, row-major);

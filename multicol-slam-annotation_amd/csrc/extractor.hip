@@ -56,6 +56,9 @@ struct mcs_extractor {
   // single-frame staging
   uint8_t* d_in = nullptr;
   mcs_keypoint* d_kps = nullptr; uint8_t* d_desc = nullptr; int32_t* d_count = nullptr;
+  uint8_t* d_dmask = nullptr;
+  // camera models (dBRIEF / mdBRIEF)
+  mcs_cam_model* d_cams = nullptr; int n_cams = 0;
   // last call (for read_stage)
   const uint8_t* last_img0 = nullptr;
   int last_frames = 0;
@@ -86,7 +89,8 @@ static inline void stage_mark(mcs_extractor* h, int stage, hipStream_t st) {
 // Core batched pipeline on device buffers.
 static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uint8_t* mask_pyr,
                      const uint8_t* mask_flags, const int32_t* d_mask_index, mcs_keypoint* d_kps,
-                     int32_t* d_counts, uint8_t* d_desc, hipStream_t st) {
+                     int32_t* d_counts, uint8_t* d_desc, uint8_t* d_desc_masks,
+                     const int32_t* d_cam_index, hipStream_t st) {
   const Plan& pl = h->plan;
   const int nl = pl.nlevels;
   const int64_t img0_fs = (int64_t)pl.W * pl.H;
@@ -168,6 +172,16 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     da.sel_count = h->d_sel_count;
     da.kps = d_kps; da.desc = d_desc; da.cap = pl.sel_per_frame; da.desc_size = pl.p.desc_size;
     da.nframes = F;
+    da.mode = pl.p.learn_masks ? 2 : (pl.p.do_dbrief ? 1 : 0);
+    da.do_dbrief = pl.p.do_dbrief ? 1 : 0;
+    da.cams = h->d_cams; da.cam_index = d_cam_index;
+    da.desc_masks = d_desc_masks;
+    if (da.mode != 0 && !h->d_cams) {
+      set_error("dBRIEF / mdBRIEF need camera models (mcs_extractor_set_cam_models)");
+      return MCS_ERR_ARG;
+    }
+    if (d_desc_masks && da.mode != 2)   // Mat::zeros (:1213-1215)
+      MCS_HIP_CHECK(hipMemsetAsync(d_desc_masks, 0, (size_t)F * pl.sel_per_frame * pl.p.desc_size, st));
     launch_orient_desc(da, st);
   }
   stage_mark(h, 5, st);
@@ -245,6 +259,7 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
   ALLOC(h->d_kps, pl.sel_per_frame);
   ALLOC(h->d_desc, (size_t)pl.sel_per_frame * pl.p.desc_size);
   ALLOC(h->d_count, 1);
+  ALLOC(h->d_dmask, (size_t)pl.sel_per_frame * pl.p.desc_size);
 #undef ALLOC
   hipError_t e = hipSuccess;
   if (e == hipSuccess) e = hipMemcpy(h->d_xofs, pl.xofs.data(), pl.xofs.size() * 4, hipMemcpyHostToDevice);
@@ -267,7 +282,7 @@ void mcs_extractor_destroy(mcs_extractor* h) {
   void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_pyr, h->d_blur,
                   h->d_slots, h->d_cell_counts, h->d_cand, h->d_cnode, h->d_sel, h->d_sel_count,
                   h->d_mask_pyr, h->d_mask_flags, h->d_mask_single, h->d_flags_single, h->d_in,
-                  h->d_kps, h->d_desc, h->d_count};
+                  h->d_kps, h->d_desc, h->d_count, h->d_dmask, h->d_cams};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (h->ev) {
@@ -342,9 +357,29 @@ int mcs_extractor_set_masks_device(mcs_extractor* h, const uint8_t* d_masks, int
   return MCS_OK;
 }
 
-int mcs_extract_batch_device(mcs_extractor* h, const uint8_t* d_images, int32_t n_frames,
-                             const int32_t* d_mask_index, mcs_keypoint* d_kps,
-                             int32_t* d_counts, uint8_t* d_desc, void* stream) {
+int mcs_extractor_set_cam_models(mcs_extractor* h, const mcs_cam_model* models, int32_t n) {
+  if (!h || n < 0 || (n > 0 && !models)) return MCS_ERR_ARG;
+  for (int i = 0; i < n; i++)
+    if (models[i].p_deg < 1 || models[i].p_deg > 16 || models[i].invp_deg < 1 ||
+        models[i].invp_deg > 16) {
+      set_error("camera polynomial length must be 1..16");
+      return MCS_ERR_ARG;
+    }
+  MCS_HIP_CHECK(hipSetDevice(h->device));
+  if (h->d_cams) { MCS_HIP_CHECK(hipFree(h->d_cams)); h->d_cams = nullptr; }
+  h->n_cams = 0;
+  if (n == 0) return MCS_OK;
+  int rc = dalloc(&h->d_cams, (size_t)n);
+  if (rc) return rc;
+  MCS_HIP_CHECK(hipMemcpy(h->d_cams, models, sizeof(mcs_cam_model) * n, hipMemcpyHostToDevice));
+  h->n_cams = n;
+  return MCS_OK;
+}
+
+int mcs_extract_batch_device_ex(mcs_extractor* h, const uint8_t* d_images, int32_t n_frames,
+                                const int32_t* d_cam_index, mcs_keypoint* d_kps,
+                                int32_t* d_counts, uint8_t* d_desc, uint8_t* d_desc_masks,
+                                void* stream) {
   if (!h || !d_images || !d_kps || !d_counts || !d_desc || n_frames < 1) {
     set_error("null argument"); return MCS_ERR_ARG;
   }
@@ -352,8 +387,16 @@ int mcs_extract_batch_device(mcs_extractor* h, const uint8_t* d_images, int32_t 
   MCS_HIP_CHECK(hipSetDevice(h->device));
   const uint8_t* mp = h->n_masks > 0 ? h->d_mask_pyr : nullptr;
   const uint8_t* mf = h->n_masks > 0 ? h->d_mask_flags : nullptr;
-  return run_batch(h, d_images, n_frames, mp, mf, mp ? d_mask_index : nullptr, d_kps, d_counts,
-                   d_desc, (hipStream_t)stream);
+  return run_batch(h, d_images, n_frames, mp, mf, mp ? d_cam_index : nullptr, d_kps, d_counts,
+                   d_desc, d_desc_masks, h->n_cams > 1 ? d_cam_index : nullptr,
+                   (hipStream_t)stream);
+}
+
+int mcs_extract_batch_device(mcs_extractor* h, const uint8_t* d_images, int32_t n_frames,
+                             const int32_t* d_mask_index, mcs_keypoint* d_kps,
+                             int32_t* d_counts, uint8_t* d_desc, void* stream) {
+  return mcs_extract_batch_device_ex(h, d_images, n_frames, d_mask_index, d_kps, d_counts,
+                                     d_desc, nullptr, stream);
 }
 
 int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const uint8_t* mask,
@@ -379,7 +422,9 @@ int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const ui
     mp = h->d_mask_single;
     mf = h->d_flags_single;
   }
-  int rc = run_batch(h, h->d_in, 1, mp, mf, nullptr, h->d_kps, h->d_count, h->d_desc, st);
+  const bool learn = pl.p.learn_masks != 0;
+  int rc = run_batch(h, h->d_in, 1, mp, mf, nullptr, h->d_kps, h->d_count, h->d_desc,
+                     learn ? h->d_dmask : nullptr, nullptr, st);
   if (rc) return rc;
   int32_t n = 0;
   MCS_HIP_CHECK(hipMemcpy(&n, h->d_count, sizeof(n), hipMemcpyDeviceToHost));
@@ -388,7 +433,12 @@ int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const ui
   if (n > 0) {
     if (kps) MCS_HIP_CHECK(hipMemcpy(kps, h->d_kps, sizeof(mcs_keypoint) * n, hipMemcpyDeviceToHost));
     if (desc) MCS_HIP_CHECK(hipMemcpy(desc, h->d_desc, (size_t)n * pl.p.desc_size, hipMemcpyDeviceToHost));
-    if (desc_masks) std::memset(desc_masks, 0, (size_t)n * pl.p.desc_size);
+    if (desc_masks) {
+      if (learn)
+        MCS_HIP_CHECK(hipMemcpy(desc_masks, h->d_dmask, (size_t)n * pl.p.desc_size, hipMemcpyDeviceToHost));
+      else
+        std::memset(desc_masks, 0, (size_t)n * pl.p.desc_size);
+    }
   }
   return MCS_OK;
 }

@@ -111,6 +111,10 @@ struct DescArgs {
   const int32_t* sel_count;
   mcs_keypoint* kps; uint8_t* desc; int cap; int desc_size;
   int nframes;
+  // dBRIEF / mdBRIEF (mode 1 / 2; mode 0 = ORB)
+  int mode, do_dbrief;
+  const mcs_cam_model* cams; const int32_t* cam_index;
+  uint8_t* desc_masks;
 };
 void launch_orient_desc(const DescArgs& a, hipStream_t st);
 int upload_desc_constants();

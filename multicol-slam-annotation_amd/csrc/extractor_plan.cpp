@@ -54,10 +54,6 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     set_error("only FAST TYPE_9_16 (fastAgastType 2, useAgast 0) is implemented");
     return MCS_ERR_UNSUPPORTED;
   }
-  if (p.do_dbrief || p.learn_masks) {
-    set_error("dBRIEF / mdBRIEF descriptors are not implemented yet (ORB only)");
-    return MCS_ERR_UNSUPPORTED;
-  }
   pl.p = p;
   pl.W = W; pl.H = H; pl.nlevels = p.nlevels;
   pl.scale_factor = (double)p.scale_factor;

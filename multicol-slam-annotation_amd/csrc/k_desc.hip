@@ -8,6 +8,7 @@
 // spelled with _rn intrinsics so no FMA contraction can change a rounding.
 #include "common.hpp"
 #include "extractor_kernels.hpp"
+#include <algorithm>
 
 namespace mcs {
 
@@ -176,9 +177,233 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   }
 }
 
+// ===========================================================================
+// dBRIEF / mdBRIEF (src/mdBRIEFextractorOct.cpp:250-283 rotateAndDistortPattern, :356-408
+// compute_dBRIEF, :410-554 compute_mdBRIEF; keypoint undistortion :1304-1316) on the
+// Scaramuzza model (src/cam_model_omni.cpp:49-163).  One wave per keypoint: every lane
+// distorts npoints/64 pattern points in double precision (ImgToWorld / WorldToImg with the
+// reference's operation order, no FMA), the pattern mean is summed by one lane in point
+// order (the reference's sequential sum), and the tests sample the padded level buffer the
+// reference reads (blurred ROI, raw reflect-101 border of 25 px, linear wrap beyond).
+// ===========================================================================
+__device__ __forceinline__ double horner_d(const double* c, int s, double x) {
+  double r = 0.0;
+  for (int i = s - 1; i >= 0; i--) r = __dadd_rn(__dmul_rn(r, x), c[i]);
+  return r;
+}
+
+__device__ void img_to_world_d(const mcs_cam_model& m, double u, double v, double& x, double& y,
+                               double& z) {
+  const double invAffine = __dsub_rn(m.c, __dmul_rn(m.d, m.e));
+  const double u_t = __dsub_rn(u, m.u0), v_t = __dsub_rn(v, m.v0);
+  x = __ddiv_rn(__dsub_rn(u_t, __dmul_rn(m.d, v_t)), invAffine);
+  y = __ddiv_rn(__dadd_rn(__dmul_rn(-m.e, u_t), __dmul_rn(m.c, v_t)), invAffine);
+  const double X2 = __dmul_rn(x, x), Y2 = __dmul_rn(y, y);
+  z = -horner_d(m.p, m.p_deg, __dsqrt_rn(__dadd_rn(X2, Y2)));
+  const double norm = __dsqrt_rn(__dadd_rn(__dadd_rn(X2, Y2), __dmul_rn(z, z)));
+  x = __ddiv_rn(x, norm); y = __ddiv_rn(y, norm); z = __ddiv_rn(z, norm);
+}
+
+__device__ void world_to_img_d(const mcs_cam_model& m, double x, double y, double z, double& u,
+                               double& v) {
+  double norm = __dsqrt_rn(__dadd_rn(__dmul_rn(x, x), __dmul_rn(y, y)));
+  if (norm == 0.0) norm = 1e-14;
+  const double theta = atan(__ddiv_rn(-z, norm));
+  const double rho = horner_d(m.invp, m.invp_deg, theta);
+  const double uu = __dmul_rn(__ddiv_rn(x, norm), rho), vv = __dmul_rn(__ddiv_rn(y, norm), rho);
+  u = __dadd_rn(__dadd_rn(__dmul_rn(uu, m.c), __dmul_rn(vv, m.d)), m.u0);
+  v = __dadd_rn(__dadd_rn(__dmul_rn(uu, m.e), vv), m.v0);
+}
+
+__device__ __forceinline__ int refl101_d(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+// image.ptr(y)[x] of the reference's padded level buffer (see oracle padded_at)
+__device__ __forceinline__ int padded_at_dev(const uint8_t* blr, int bp, const uint8_t* raw, int rp,
+                                             int w, int h, int y, int x) {
+  if ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) return blr[(int64_t)y * bp + x];
+  int py = y, px = x;
+  if (x < -kEdgeThreshold || x >= w + kEdgeThreshold || y < -kEdgeThreshold ||
+      y >= h + kEdgeThreshold) {
+    const int64_t W2 = w + 2 * kEdgeThreshold, H2 = h + 2 * kEdgeThreshold;
+    int64_t L = (int64_t)(y + kEdgeThreshold) * W2 + (x + kEdgeThreshold);
+    L = L < 0 ? 0 : (L >= W2 * H2 ? W2 * H2 - 1 : L);
+    py = (int)(L / W2) - kEdgeThreshold;
+    px = (int)(L - (int64_t)(py + kEdgeThreshold) * W2) - kEdgeThreshold;
+    if ((unsigned)py < (unsigned)h && (unsigned)px < (unsigned)w) return blr[(int64_t)py * bp + px];
+  }
+  return raw[(int64_t)refl101_d(py, h) * rp + refl101_d(px, w)];
+}
+
+template <bool LEARN>
+__global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+  const int wpb = blockDim.x >> 6;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int npts = 16 * a.desc_size;
+  double* xs = reinterpret_cast<double*>(dlds + (size_t)wv * wave_lds);
+  double* ys = xs + npts;
+  int32_t* offs = reinterpret_cast<int32_t*>(ys + npts);   // [LEARN ? 3 : 1][npts]
+  int f, item;
+  const int chunks = (a.sel_per_frame + wpb - 1) / wpb;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, chunks, &f, &item)) return;
+  const int j = item * wpb + wv;
+  if (j >= a.sel_per_frame) return;
+  int l = 0;
+  while (l + 1 < a.nlevels && j >= a.lv[l + 1].sel_off) l++;
+  const LevelPlan& L = a.lv[l];
+  const int i = j - L.sel_off;
+  const int32_t* scount = a.sel_count + (int64_t)f * a.nlevels;
+  if (i >= scount[l]) return;
+  int outIdx = i;
+  for (int t = 0; t < l; t++) outIdx += scount[t];
+  const uint32_t pk = a.sel[(int64_t)f * a.sel_fstride + j];
+  const int cx = (int)(pk & 0xFFF) + kMinBorder, cy = (int)((pk >> 12) & 0xFFF) + kMinBorder;
+  const int score = (int)(pk >> 24);
+  const int pitch = L.pitch, bp = L.bpitch;
+  const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
+                                : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
+  const uint8_t* blr = a.blur + (int64_t)f * a.blur_fstride + L.img_off;
+  // ---- IC_Angle on the raw patch, staged in the (not yet used) xs area
+  {
+    uint32_t* rawp = reinterpret_cast<uint32_t*>(xs);
+    const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
+    for (int q = lane; q < kRawH * kRawW; q += 64) {
+      const int r = q / kRawW, c = q - r * kRawW;
+      rawp[q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+    }
+  }
+  dev::wave_sync();
+  float angle;
+  {
+    const uint8_t* raw = reinterpret_cast<const uint8_t*>(xs);
+    int m10 = 0, m01 = 0;
+#pragma unroll
+    for (int t = 0; t < 18; t++) {
+      const int e = c_icpatch[t * 64 + lane];
+      const int u = (e & 0xFF) - 16, v = ((e >> 8) & 0xFF) - 16;
+      const int w = (e >> 16) & 1;
+      const int I = raw[(v + 16) * (4 * kRawW) + (u + 16)];
+      m10 += w * u * I;
+      m01 += w * v * I;
+    }
+    m10 = dev::wave_sum(m10);
+    m01 = dev::wave_sum(m01);
+    angle = fast_atan2_dev((float)m01, (float)m10);
+  }
+  dev::wave_sync();
+  // ---- undistorted keypoint (zero unless do_dBrief, :1304-1316)
+  const mcs_cam_model& m = a.cams[a.cam_index ? a.cam_index[f] : 0];
+  double ux = 0.0, uy = 0.0;
+  if (a.do_dbrief) {
+    const float fx = (l != 0) ? __fmul_rn((float)cx, L.scale) : (float)cx;
+    const float fy = (l != 0) ? __fmul_rn((float)cy, L.scale) : (float)cy;
+    double x, y, z;
+    img_to_world_d(m, (double)fx, (double)fy, x, y, z);
+    ux = __dmul_rn(__ddiv_rn(-x, z), m.p[0]);
+    uy = __dmul_rn(__ddiv_rn(-y, z), m.p[0]);
+  }
+  // ---- rotateAndDistortPattern
+  auto build = [&](double ang, int32_t* out) {
+    double ax, ay;
+    sincos(ang, &ay, &ax);
+    for (int p = lane; p < npts; p += 64) {
+      const double px = c_pattern[2 * p], py = c_pattern[2 * p + 1];
+      const double xr = __dadd_rn(__dsub_rn(__dmul_rn(px, ax), __dmul_rn(py, ay)), ux);
+      const double yr = __dadd_rn(__dadd_rn(__dmul_rn(px, ay), __dmul_rn(py, ax)), uy);
+      double u, v;
+      world_to_img_d(m, xr, yr, -m.p[0], u, v);
+      xs[p] = u;
+      ys[p] = v;
+    }
+    dev::wave_sync();
+    double sx = 0.0, sy = 0.0;
+    if (lane == 0) {   // the reference's running sum, in point order
+      for (int p = 0; p < npts; p++) { sx = __dadd_rn(sx, xs[p]); sy = __dadd_rn(sy, ys[p]); }
+    }
+    sx = __shfl(sx, 0);
+    sy = __shfl(sy, 0);
+    const double mx = __ddiv_rn(sx, (double)npts), my = __ddiv_rn(sy, (double)npts);
+    for (int p = lane; p < npts; p += 64) {
+      const int ox = (int)rint(__dsub_rn(xs[p], mx)), oy = (int)rint(__dsub_rn(ys[p], my));
+      out[p] = (ox & 0xFFFF) | (oy << 16);
+    }
+    dev::wave_sync();
+  };
+  if (LEARN) {
+    const float RHOf = 180.0f / 3.1415926535897932384626f;
+    const double RHOd = 180.0 / 3.1415926535897932384626433832795028841971693993;
+    const double rot = 20.0 / RHOd;
+    const double ang = (double)__fdiv_rn(angle, RHOf);
+    build(ang, offs);
+    build(__dadd_rn(ang, rot), offs + npts);
+    build(__dsub_rn(ang, rot), offs + 2 * npts);
+  } else {
+    const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
+    build((double)__fmul_rn(angle, DEG2RADf), offs);
+  }
+  // ---- tests
+  auto sample = [&](int32_t o) {
+    const int ox = (int)(int16_t)(o & 0xFFFF), oy = o >> 16;
+    return padded_at_dev(blr, bp, img, pitch, L.w, L.h, cy + oy, cx + ox);
+  };
+  const int nwords = a.desc_size / 8;
+  uint64_t words[8], mwords[8];
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    words[r] = mwords[r] = 0;
+    if (r < nwords) {
+      const int t = r * 64 + lane;
+      const int bit = sample(offs[2 * t]) < sample(offs[2 * t + 1]);
+      words[r] = __ballot(bit);
+      if (LEARN) {
+        const int s1 = (sample(offs[npts + 2 * t]) < sample(offs[npts + 2 * t + 1])) ^ bit;
+        const int s2 = (sample(offs[2 * npts + 2 * t]) < sample(offs[2 * npts + 2 * t + 1])) ^ bit;
+        mwords[r] = __ballot(s1 + s2 == 0);
+      }
+    }
+  }
+  uint8_t* dptr = a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size;
+  if (lane < nwords) {
+    uint64_t w = words[0], mw = mwords[0];
+#pragma unroll
+    for (int r = 1; r < 8; r++)
+      if (lane == r) { w = words[r]; mw = mwords[r]; }
+    reinterpret_cast<uint64_t*>(dptr)[lane] = w;
+    if (a.desc_masks)
+      reinterpret_cast<uint64_t*>(a.desc_masks + ((int64_t)f * a.cap + outIdx) * a.desc_size)[lane] = mw;
+  }
+  if (lane == 0) {
+    mcs_keypoint kp;
+    kp.x = (float)cx; kp.y = (float)cy;
+    if (l != 0) { kp.x = __fmul_rn((float)cx, L.scale); kp.y = __fmul_rn((float)cy, L.scale); }
+    kp.size = (float)L.patch_size_scaled;
+    kp.angle = angle;
+    kp.response = (float)score;
+    kp.octave = l;
+    kp.class_id = -1;
+    a.kps[(int64_t)f * a.cap + outIdx] = kp;
+  }
+}
+
 void launch_orient_desc(const DescArgs& a, hipStream_t st) {
-  const unsigned g = xcd_grid(a.nframes, (a.sel_per_frame + 3) / 4);
-  hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(256), 0, st, a);
+  if (a.mode == 0) {
+    const unsigned g = xcd_grid(a.nframes, (a.sel_per_frame + 3) / 4);
+    hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(256), 0, st, a);
+    return;
+  }
+  const int npts = 16 * a.desc_size;
+  const int npat = a.mode == 2 ? 3 : 1;
+  const int wave_lds = (npts * 16 + npat * npts * 4 + 15) & ~15;
+  const int wpb = std::max(1, std::min(4, 65536 / wave_lds));
+  const unsigned g = xcd_grid(a.nframes, (a.sel_per_frame + wpb - 1) / wpb);
+  if (a.mode == 2)
+    hipLaunchKernelGGL(k_dbrief<true>, dim3(g), dim3(64 * wpb), (size_t)wpb * wave_lds, st, a, wave_lds);
+  else
+    hipLaunchKernelGGL(k_dbrief<false>, dim3(g), dim3(64 * wpb), (size_t)wpb * wave_lds, st, a, wave_lds);
 }
 
 }  // namespace mcs

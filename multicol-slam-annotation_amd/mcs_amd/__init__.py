@@ -54,6 +54,27 @@ class ExtractorParams(ctypes.Structure):
                          do_dbrief, learn_masks, desc_size)
 
 
+class CamModel(ctypes.Structure):
+    """Mirror of mcs_cam_model (include/mcs_extractor.h): cCamModelGeneral_ parameters."""
+    _fields_ = [("c", ctypes.c_double), ("d", ctypes.c_double), ("e", ctypes.c_double),
+                ("u0", ctypes.c_double), ("v0", ctypes.c_double),
+                ("p_deg", ctypes.c_int32), ("invp_deg", ctypes.c_int32),
+                ("p", ctypes.c_double * 16), ("invp", ctypes.c_double * 16)]
+
+    @classmethod
+    def from_dict(cls, cam):
+        """From a Lafida-style calibration dict (c, d, e, u0, v0, a = p, pol = invP)."""
+        m = cls()
+        m.c, m.d, m.e, m.u0, m.v0 = (float(cam[k]) for k in ("c", "d", "e", "u0", "v0"))
+        a, pol = list(cam["a"]), list(cam["pol"])
+        m.p_deg, m.invp_deg = len(a), len(pol)
+        for i, v in enumerate(a):
+            m.p[i] = float(v)
+        for i, v in enumerate(pol):
+            m.invp[i] = float(v)
+        return m
+
+
 # numpy view of mcs_keypoint / cv::KeyPoint
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -76,6 +97,8 @@ SIGNATURES = {
     "mcs_extractor_set_masks_device": (ctypes.c_int, [_P, _P, _I32, _P]),
     "mcs_extract_batch_device": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_extractor_read_stage": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _I64, _P]),
+    "mcs_extractor_set_cam_models": (ctypes.c_int, [_P, _P, _I32]),
+    "mcs_extract_batch_device_ex": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "mcs_extractor_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mcs_extractor_read_timing": (ctypes.c_int, [_P, _P, _P, _I32]),
     # matcher (include/mcs_matcher.h)
@@ -168,6 +191,33 @@ class Extractor:
         _check(lib().mcs_extractor_levels(self._h, ctypes.byref(n), _ptr(wh), _ptr(nf)))
         k = n.value
         return wh[:2 * k].reshape(k, 2), nf[:k]
+
+    def set_cam_models(self, models):
+        """Camera models (list of CamModel or calibration dicts) for dBRIEF / mdBRIEF."""
+        arr = (CamModel * len(models))(*[m if isinstance(m, CamModel) else CamModel.from_dict(m)
+                                         for m in models])
+        _check(lib().mcs_extractor_set_cam_models(self._h, arr, len(models)))
+
+    def extract_with_masks(self, image, mask=None):
+        """operator() -> (kps, desc, descMasks) (masks all-zero unless learn_masks)."""
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        assert image.shape == (self.height, self.width)
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            assert mask.shape == image.shape
+        kps = np.zeros(self.capacity, KEYPOINT_DTYPE)
+        desc = np.zeros((self.capacity, self.desc_size), np.uint8)
+        dm = np.zeros((self.capacity, self.desc_size), np.uint8)
+        n = ctypes.c_int32()
+        _check(lib().mcs_extract(self._h, _ptr(image), self.width, _ptr(mask), self.width,
+                                 _ptr(kps), self.capacity, ctypes.byref(n), _ptr(desc), _ptr(dm)))
+        k = n.value
+        return kps[:k].copy(), desc[:k].copy(), dm[:k].copy()
+
+    def extract_batch_device_ex(self, d_images, n_frames, d_cam_index, d_kps, d_counts, d_desc,
+                                d_desc_masks, stream=None):
+        _check(lib().mcs_extract_batch_device_ex(self._h, d_images, int(n_frames), d_cam_index,
+                                                 d_kps, d_counts, d_desc, d_desc_masks, stream))
 
     def extract(self, image, mask=None):
         """operator()(image, mask, kps, camModel, desc, descMasks) -> (kps, desc)."""

@@ -35,6 +35,8 @@
 #include <vector>
 #include <utility>
 
+#include "../include/mcs_extractor.h"
+
 namespace {
 
 const int kPatternFull[2048] = {
@@ -464,6 +466,106 @@ void orb_descriptor(const Img& blurred, float kx, float ky, float angle_deg, int
   }
 }
 
+// ---- dBRIEF / mdBRIEF (:250-283, :356-554) on the Scaramuzza model (cam_model_omni) ----
+double horner(const double* c, int s, double x) {  // include/misc.h:117-124
+  double r = 0.0;
+  for (int i = s - 1; i >= 0; i--) r = r * x + c[i];
+  return r;
+}
+// ImgToWorld (src/cam_model_omni.cpp:49-66)
+void img_to_world(const mcs_cam_model& m, double u, double v, double& x, double& y, double& z) {
+  const double invAffine = m.c - m.d * m.e;
+  const double u_t = u - m.u0, v_t = v - m.v0;
+  x = (u_t - m.d * v_t) / invAffine;
+  y = (-m.e * u_t + m.c * v_t) / invAffine;
+  const double X2 = x * x, Y2 = y * y;
+  z = -horner(m.p, m.p_deg, std::sqrt(X2 + Y2));
+  const double norm = std::sqrt(X2 + Y2 + z * z);
+  x /= norm; y /= norm; z /= norm;
+}
+// WorldToImg(x, y, z, u, v) (:147-163)
+void world_to_img(const mcs_cam_model& m, double x, double y, double z, double& u, double& v) {
+  double norm = std::sqrt(x * x + y * y);
+  if (norm == 0.0) norm = 1e-14;
+  const double theta = std::atan(-z / norm);
+  const double rho = horner(m.invp, m.invp_deg, theta);
+  const double uu = x / norm * rho, vv = y / norm * rho;
+  u = uu * m.c + vv * m.d + m.u0;
+  v = uu * m.e + vv + m.v0;
+}
+// rotateAndDistortPattern (:250-283): rotate around the undistorted keypoint, distort with
+// distortPointsOcam (WorldToImg at z = -p1), subtract the mean (summed in point order), round
+void rotate_distort_pattern(const mcs_cam_model& m, double ux, double uy, int npoints, double ax,
+                            double ay, int* out) {
+  std::vector<double> xc(npoints), yc(npoints);
+  double sumX = 0.0, sumY = 0.0;
+  for (int p = 0; p < npoints; ++p) {
+    const int px = kPatternFull[2 * p], py = kPatternFull[2 * p + 1];
+    const double xr = px * ax - py * ay + ux;
+    const double yr = px * ay + py * ax + uy;
+    world_to_img(m, xr, yr, -m.p[0], xc[p], yc[p]);
+    sumX += xc[p];
+    sumY += yc[p];
+  }
+  const double meanX = sumX / (double)npoints, meanY = sumY / (double)npoints;
+  for (int p = 0; p < npoints; ++p) {
+    out[2 * p] = cvRound(xc[p] - meanX);
+    out[2 * p + 1] = cvRound(yc[p] - meanY);
+  }
+}
+// The reference samples image.ptr(row+iy)[col+ix] on the blurred level, a ROI at (+25,+25)
+// of a (w+50)x(h+50) buffer whose border holds the RAW level reflected (copyMakeBorder,
+// :1166-1199; the in-place boxFilter only rewrites the ROI).  Offsets past the 25 px border
+// wrap through the buffer's linear layout exactly as the pointer arithmetic does; outside
+// the buffer the reference is undefined -- clamped to the buffer here (and on the GPU).
+int padded_at(const Img& blurred, const Img& raw, int y, int x) {
+  const long W2 = raw.w + 2 * EDGE_THRESHOLD, H2 = raw.h + 2 * EDGE_THRESHOLD;
+  long L = (long)(y + EDGE_THRESHOLD) * W2 + (x + EDGE_THRESHOLD);
+  L = std::min(std::max(L, 0L), W2 * H2 - 1);
+  const int py = (int)(L / W2) - EDGE_THRESHOLD, px = (int)(L % W2) - EDGE_THRESHOLD;
+  if (py >= 0 && py < raw.h && px >= 0 && px < raw.w) return blurred.at(py, px);
+  return raw.at(reflect101(py, raw.h), reflect101(px, raw.w));
+}
+// compute_dBRIEF (:356-408) and compute_mdBRIEF (:410-554)
+void dbrief_descriptor(const Img& blurred, const Img& raw, const mcs_cam_model& m, float kx,
+                       float ky, float angle_deg, double ux, double uy, int descsize,
+                       bool learn, uint8_t* desc, uint8_t* dmask) {
+  const int npoints = 2 * 8 * descsize;
+  std::vector<int> pat(2 * npoints), pm1, pm2;
+  if (learn) {
+    const float RHOf = 180.0f / 3.1415926535897932384626f;       // include/misc.h:38-42
+    const double RHOd = 180.0 / 3.1415926535897932384626433832795028841971693993;
+    const double rot = 20.0 / RHOd;
+    const double angle = static_cast<double>(angle_deg / RHOf);
+    const double a1 = angle + rot, a2 = angle - rot;
+    pm1.resize(2 * npoints); pm2.resize(2 * npoints);
+    rotate_distort_pattern(m, ux, uy, npoints, std::cos(angle), std::sin(angle), pat.data());
+    rotate_distort_pattern(m, ux, uy, npoints, std::cos(a1), std::sin(a1), pm1.data());
+    rotate_distort_pattern(m, ux, uy, npoints, std::cos(a2), std::sin(a2), pm2.data());
+  } else {
+    const double angle = static_cast<double>(angle_deg * DEG2RADf);
+    rotate_distort_pattern(m, ux, uy, npoints, std::cos(angle), std::sin(angle), pat.data());
+  }
+  const int row = cvRoundf(ky), col = cvRoundf(kx);
+  auto get = [&](const std::vector<int>& pt, int idx) {
+    return padded_at(blurred, raw, row + pt[2 * idx + 1], col + pt[2 * idx]);
+  };
+  for (int i = 0; i < descsize; ++i) {
+    int val = 0, maskVal = 0;
+    for (int k = 0; k < 8; k++) {
+      const int p0 = 16 * i + 2 * k;
+      const int t = get(pat, p0) < get(pat, p0 + 1);
+      val |= t << k;
+      if (learn) {
+        int stable = ((get(pm1, p0) < get(pm1, p0 + 1)) ^ t) + ((get(pm2, p0) < get(pm2, p0 + 1)) ^ t);
+        maskVal |= (stable == 0) << k;
+      }
+    }
+    desc[i] = (uint8_t)val;
+    if (dmask) dmask[i] = (uint8_t)maskVal;
+  }
+}
+
 struct Params {
   int nfeatures; float scale_factor; int nlevels; int fast_threshold; int desc_size; int vresize_mode;
 };
@@ -608,16 +710,20 @@ float oracle_ic_angle(const uint8_t* img, int w, int h, int cx, int cy, int* m01
   return ic_angle(im, cx, cy, umax, m01, m10);
 }
 
-// Full extractor: mdBRIEFextractorOct::operator() ORB path (:1244-1337).
-// kps/desc caller-allocated (cap keypoints).  Returns 0, or -1 if cap too small.
-int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
-                   float scale_factor, int nlevels, int fast_threshold, int desc_size,
-                   int vresize_mode, oracle_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+// Full extractor: mdBRIEFextractorOct::operator() (:1244-1337).  ORB when cam == nullptr
+// (do_dbrief = learn_masks = 0); dBRIEF / mdBRIEF otherwise.  kps/desc/desc_masks
+// caller-allocated (cap keypoints; desc_masks nullable).  Returns 0, or -1 if cap too small.
+int oracle_extract_ex(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
+                      float scale_factor, int nlevels, int fast_threshold, int desc_size,
+                      int vresize_mode, int do_dbrief, int learn_masks, const mcs_cam_model* cam,
+                      oracle_keypoint* kps, uint8_t* desc, uint8_t* desc_masks, int cap,
+                      int* n_out) {
   Params p{nfeatures, scale_factor, nlevels, fast_threshold, desc_size, vresize_mode};
   std::vector<Level> lv; std::vector<double> sf, isf;
   level_sizes(W, H, p, lv, sf, isf);
   auto nPerLevel = features_per_level(p);
   auto umax = make_umax();
+  if ((do_dbrief || learn_masks) && !cam) return -2;
   // ComputePyramid (:1158-1201)
   std::vector<Img> pyr(nlevels), mpyr(nlevels);
   pyr[0].create(W, H); std::memcpy(pyr[0].d.data(), image, (size_t)W * H);
@@ -640,6 +746,7 @@ int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int 
   for (int l = 0; l < nlevels; l++) total += (int)all[l].size();
   *n_out = total;
   if (total > cap) return -1;
+  const double scaleF = cam ? cam->p[0] : 0.0;   // camModel.Get_P().at<double>(0) (:1283)
   int off = 0;
   for (int l = 0; l < nlevels; l++) {
     const int scaledPatchSize = (int)(PATCH_SIZE * sf[l]);
@@ -652,7 +759,22 @@ int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int 
     float scale = (float)sf[l];
     for (size_t i = 0; i < all[l].size(); i++) {
       const KP& k = all[l][i];
-      orb_descriptor(blurred, k.x, k.y, ang[i], desc_size, desc + (size_t)(off + i) * desc_size);
+      uint8_t* d = desc + (size_t)(off + i) * desc_size;
+      uint8_t* dm = desc_masks ? desc_masks + (size_t)(off + i) * desc_size : nullptr;
+      if (dm) std::memset(dm, 0, desc_size);
+      if (learn_masks || do_dbrief) {
+        double ux = 0.0, uy = 0.0;   // zero unless do_dBrief (:1304-1316)
+        if (do_dbrief) {
+          double x, y, z;   // undistortPointsOcam (include/cam_model_omni.h:129-140)
+          img_to_world(*cam, static_cast<double>(k.x * scale), static_cast<double>(k.y * scale), x, y, z);
+          ux = -x / z * scaleF;
+          uy = -y / z * scaleF;
+        }
+        dbrief_descriptor(blurred, pyr[l], *cam, k.x, k.y, ang[i], ux, uy, desc_size,
+                          learn_masks != 0, d, dm);
+      } else {
+        orb_descriptor(blurred, k.x, k.y, ang[i], desc_size, d);
+      }
       oracle_keypoint& o = kps[off + i];
       o.x = k.x; o.y = k.y;
       if (l != 0) { o.x = k.x * scale; o.y = k.y * scale; }
@@ -661,6 +783,23 @@ int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int 
     }
     off += (int)all[l].size();
   }
+  return 0;
+}
+
+int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
+                   float scale_factor, int nlevels, int fast_threshold, int desc_size,
+                   int vresize_mode, oracle_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+  return oracle_extract_ex(image, W, H, mask, nfeatures, scale_factor, nlevels, fast_threshold,
+                           desc_size, vresize_mode, 0, 0, nullptr, kps, desc, nullptr, cap, n_out);
+}
+
+// single-point camera-model helpers (tests)
+int oracle_cam_world_to_img(const mcs_cam_model* m, double x, double y, double z, double* uv) {
+  world_to_img(*m, x, y, z, uv[0], uv[1]);
+  return 0;
+}
+int oracle_cam_img_to_world(const mcs_cam_model* m, double u, double v, double* xyz) {
+  img_to_world(*m, u, v, xyz[0], xyz[1], xyz[2]);
   return 0;
 }
 

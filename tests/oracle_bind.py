@@ -31,6 +31,9 @@ _SIGS = {
     "oracle_octree": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P]),
     "oracle_ic_angle": (_F, [_P, _I, _I, _I, _I, _P, _P]),
     "oracle_extract": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "oracle_extract_ex": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
+    "oracle_cam_world_to_img": (_I, [_P, _D, _D, _D, _P]),
+    "oracle_cam_img_to_world": (_I, [_P, _D, _D, _P]),
     # matcher oracle
     "oracle_descriptor_distance64": (_I, [_P, _P, _I]),
     "oracle_descriptor_distance64_masked": (_I, [_P, _P, _P, _P, _I]),
@@ -162,6 +165,37 @@ def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, de
                               desc_size, mode, _p(kps), _p(desc), cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def extract_ex(img, cam, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20,
+               desc_size=32, do_dbrief=1, learn_masks=0, mode=1):
+    """dBRIEF / mdBRIEF oracle: -> (kps, desc, desc_masks).  cam: mcs_amd.CamModel."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    cap = nfeatures * 2 + 64 * nlevels
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, desc_size), np.uint8)
+    dm = np.zeros((cap, desc_size), np.uint8)
+    n = ctypes.c_int()
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    rc = lib().oracle_extract_ex(_p(img), W, H, _p(m), nfeatures, scale, nlevels, fast_th,
+                                 desc_size, mode, do_dbrief, learn_masks, ctypes.byref(cam),
+                                 _p(kps), _p(desc), _p(dm), cap, ctypes.byref(n))
+    assert rc == 0, rc
+    k = n.value
+    return kps[:k].copy(), desc[:k].copy(), dm[:k].copy()
+
+
+def cam_world_to_img(cam, x, y, z):
+    uv = np.zeros(2)
+    lib().oracle_cam_world_to_img(ctypes.byref(cam), x, y, z, _p(uv))
+    return uv
+
+
+def cam_img_to_world(cam, u, v):
+    xyz = np.zeros(3)
+    lib().oracle_cam_img_to_world(ctypes.byref(cam), u, v, _p(xyz))
+    return xyz
 
 
 # ---------------------------------------------------------------------------
