@@ -141,6 +141,135 @@ __global__ __launch_bounds__(kHamThreads) void k_top2(
   }
 }
 
+// ---------------------------------------------------------------------------
+// 32-byte descriptors on the int8 matrix cores: with bits mapped to +-1 bytes,
+// dot(a, b) = 256 - 2 * Hamming(a, b), exactly (i32 accumulation of +-1 products).
+// v_mfma_i32_32x32x32_i8: A = 32 train rows, B = 32 query columns, K = 32 bits per
+// instruction, 8 instructions per 256-bit descriptor.  A workgroup (4 waves) owns 256
+// queries of one pair; each wave keeps the expanded bits of its 64 queries in registers
+// (B operands of both 32-column groups) and streams 64-train tiles, expanded once per
+// workgroup into LDS.  The accumulator puts one query column on each lane and 16 train rows
+// in its registers, so the running best/second-best keys (dist << 16 | train) are updated
+// lane-locally; the two lane halves (different train rows) are merged at the end.
+// ---------------------------------------------------------------------------
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// 4 bits -> 4 bytes of +1 (bit set) / -1 (bit clear)
+__device__ __forceinline__ uint32_t expand4(uint32_t nib) {
+  const uint32_t m = (nib * 0x00204081u) & 0x01010101u;
+  return ~(m * 0xFEu);
+}
+// 16 bits -> 16 bytes (element j <-> bit j)
+__device__ __forceinline__ v4i expand16(uint32_t bits) {
+  v4i r;
+  r.x = (int)expand4(bits & 0xF);
+  r.y = (int)expand4((bits >> 4) & 0xF);
+  r.z = (int)expand4((bits >> 8) & 0xF);
+  r.w = (int)expand4((bits >> 12) & 0xF);
+  return r;
+}
+
+constexpr int kMfTileT = 64;            // trains per LDS tile
+constexpr int kMfPitch = 256 + 16;      // expanded train row (bytes), padded against bank conflicts
+
+__global__ __launch_bounds__(256) void k_top2_mfma32(
+    const uint8_t* __restrict__ qbase, const uint8_t* __restrict__ tbase,
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ pairs, int64_t set_stride,
+    int nq_fixed, int nt_fixed, int cap_out, int32_t* __restrict__ best_idx,
+    int32_t* __restrict__ best_dist, int32_t* __restrict__ second_idx,
+    int32_t* __restrict__ second_dist) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_t[kMfTileT * kMfPitch];
+  const int p = blockIdx.y;
+  const uint8_t* Q;
+  const uint8_t* T;
+  int nq, nt;
+  if (pairs) {
+    const int qs = pairs[2 * p], ts = pairs[2 * p + 1];
+    Q = qbase + (int64_t)qs * set_stride;
+    T = tbase + (int64_t)ts * set_stride;
+    nq = counts[qs];
+    nt = counts[ts];
+  } else {
+    Q = qbase; T = tbase; nq = nq_fixed; nt = nt_fixed;
+  }
+  const int q_blk = blockIdx.x * 256;
+  if (q_blk >= nq) return;   // uniform per block
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int h = lane >> 5, col = lane & 31;
+  // ---- B operands: this wave's 64 queries (2 column groups x 8 k-steps)
+  v4i bq[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const int qi = q_blk + wv * 64 + c * 32 + col;
+    const uint32_t* qd = reinterpret_cast<const uint32_t*>(Q + (int64_t)min(qi, max(nq - 1, 0)) * 32);
+    uint32_t w[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) w[s] = qd[s];
+#pragma unroll
+    for (int s = 0; s < 8; s++) bq[c][s] = expand16((w[s] >> (16 * h)) & 0xFFFF);
+  }
+  uint32_t k1[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, k2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  for (int t0 = 0; t0 < nt; t0 += kMfTileT) {
+    const int ntile = min(kMfTileT, nt - t0);
+    __syncthreads();
+    // ---- expand the tile: 64 trains x 8 dwords; each thread 2 dwords -> 2 x 32 bytes
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int e = tid + 256 * r;          // 0..511
+      const int tr = e >> 3, dw = e & 7;
+      const uint32_t bits = tr < ntile ? reinterpret_cast<const uint32_t*>(T + (int64_t)(t0 + tr) * 32)[dw] : 0u;
+      uint8_t* dst = s_t + tr * kMfPitch + dw * 32;
+      const v4i lo = expand16(bits & 0xFFFF), hi = expand16(bits >> 16);
+      *reinterpret_cast<v4i*>(dst) = lo;
+      *reinterpret_cast<v4i*>(dst + 16) = hi;
+    }
+    __syncthreads();
+    // ---- two 32-train sub-tiles
+#pragma unroll
+    for (int st = 0; st < 2; st++) {
+      if (st * 32 >= ntile) break;
+      v16i acc0 = {0}, acc1 = {0};
+      const uint8_t* arow = s_t + (st * 32 + col) * kMfPitch + 16 * h;
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        const v4i a = *reinterpret_cast<const v4i*>(arow + 32 * s);
+        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[0][s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[1][s], acc1, 0, 0, 0);
+      }
+      const int tb = t0 + st * 32 + 4 * h;
+      const bool full = st * 32 + 32 <= ntile;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int trow = tb + (r & 3) + 8 * (r >> 2);
+        const uint32_t d0 = (uint32_t)(256 - acc0[r]) >> 1, d1 = (uint32_t)(256 - acc1[r]) >> 1;
+        uint32_t key0 = (d0 << 16) | (uint32_t)trow, key1 = (d1 << 16) | (uint32_t)trow;
+        if (!full && trow >= nt) { key0 = 0xFFFFFFFFu; key1 = 0xFFFFFFFFu; }
+        k2[0] = med3_u32(k1[0], key0, k2[0]);
+        k1[0] = min(k1[0], key0);
+        k2[1] = med3_u32(k1[1], key1, k2[1]);
+        k1[1] = min(k1[1], key1);
+      }
+    }
+  }
+  // ---- merge the two lane halves (same query, disjoint train rows) and write
+  const int none = 8 * 32 + 1;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint32_t o1 = __shfl_xor(k1[c], 32), o2 = __shfl_xor(k2[c], 32);
+    const uint32_t b1 = min(k1[c], o1), b2 = min(max(k1[c], o1), min(k2[c], o2));
+    const int qi = q_blk + wv * 64 + c * 32 + col;
+    if (h == 0 && qi < nq) {
+      const int64_t o = (int64_t)p * cap_out + qi;
+      const bool h1 = b1 != 0xFFFFFFFFu, h2 = b2 != 0xFFFFFFFFu;
+      best_idx[o] = h1 ? (int)(b1 & 0xFFFF) : -1;
+      best_dist[o] = h1 ? (int)(b1 >> 16) : none;
+      second_idx[o] = h2 ? (int)(b2 & 0xFFFF) : -1;
+      second_dist[o] = h2 ? (int)(b2 >> 16) : none;
+    }
+  }
+}
+
 template <int W>
 __global__ __launch_bounds__(kHamThreads) void k_dense(const uint8_t* __restrict__ A, int na,
                                                        const uint8_t* __restrict__ B, int nb,
@@ -269,6 +398,13 @@ int mcs_hamming_top2_device(const uint8_t* d_q, int32_t nq, const uint8_t* d_t, 
   if (rc) return rc;
   if (nq <= 0) return MCS_OK;
   if (nt > 65535) { set_error("top2: at most 65535 train descriptors"); return MCS_ERR_ARG; }
+  if (bytes == 32) {
+    hipLaunchKernelGGL(k_top2_mfma32, dim3((nq + 255) / 256, 1), dim3(256), 0, (hipStream_t)stream,
+                       d_q, d_t, (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, nq,
+                       nt, nq, d_best_idx, d_best_dist, d_second_idx, d_second_dist);
+    MCS_HIP_CHECK(hipGetLastError());
+    return MCS_OK;
+  }
   dim3 g((nq + kHamThreads * kQPT - 1) / (kHamThreads * kQPT), 1);
   MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_q, d_t,
                  (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, nq, nt, nq,
@@ -286,6 +422,14 @@ int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts
   if (n_pairs <= 0) return MCS_OK;
   if (!d_desc || !d_counts || !d_pairs || cap <= 0) return MCS_ERR_ARG;
   if (cap > 65535) { set_error("top2: capacity above 65535"); return MCS_ERR_ARG; }
+  if (bytes == 32) {
+    hipLaunchKernelGGL(k_top2_mfma32, dim3((cap + 255) / 256, n_pairs), dim3(256), 0,
+                       (hipStream_t)stream, d_desc, d_desc, d_counts, d_pairs,
+                       (int64_t)cap * bytes, 0, 0, cap, d_best_idx, d_best_dist, d_second_idx,
+                       d_second_dist);
+    MCS_HIP_CHECK(hipGetLastError());
+    return MCS_OK;
+  }
   dim3 g((cap + kHamThreads * kQPT - 1) / (kHamThreads * kQPT), n_pairs);
   MCS_DISPATCH_W(bytes, k_top2, g, dim3(kHamThreads), 0, (hipStream_t)stream, d_desc, d_desc,
                  d_counts, d_pairs, (int64_t)cap * bytes, 0, 0, cap, d_best_idx, d_best_dist,
