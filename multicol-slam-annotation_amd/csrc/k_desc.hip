@@ -15,9 +15,13 @@ namespace mcs {
 __constant__ int c_pattern[2048] = {
 #include "pattern_orb64.inc"
 };
-// IC_Angle patch: 33x33 square scanned as 18 slots of 64 lanes; entry = (u+16) | (v+16)<<8
-// | inside<<16 (inside <=> |u| <= umax[|v|], the circular r=16 patch of the reference)
-__constant__ int c_icpatch[18 * 64];
+// IC_Angle's circular r=16 patch (inside <=> |u| <= umax[|v|]) per staged raw-patch dword (33 rows x 9 dwords, byte k of dword (r, cw) is
+// u = 4cw + k - 16, v = r - 16): packed u8 weights (u+16 inside, 0 outside) and inside flags,
+// so the moments are two v_dot4_u32_u8 per dword:  m10 = sum (u+16) I - 16 S, m01 = sum (v+16) I
+// - 16 S, S = sum I (exact integers, identical to the reference's loops).
+__constant__ uint32_t c_icw[2][33 * 9];
+// pattern as doubles (the rotation runs in double, :290-300)
+__constant__ double c_pattern_d[2048];
 
 int upload_desc_constants() {
   int umax[kHalfPatch + 1];
@@ -30,14 +34,26 @@ int upload_desc_constants() {
     umax[v] = v0;
     ++v0;
   }
-  int tab[18 * 64];
-  for (int i = 0; i < 18 * 64; i++) {
-    if (i >= 33 * 33) { tab[i] = 16 | (16 << 8); continue; }  // centre, weight 0 (outside)
-    const int vv = i / 33 - kHalfPatch, uu = i % 33 - kHalfPatch;
-    const bool in = std::abs(uu) <= umax[std::abs(vv)];
-    tab[i] = (uu + 16) | ((vv + 16) << 8) | ((in ? 1 : 0) << 16);
+  uint32_t icw[2][33 * 9];
+  for (int q = 0; q < 33 * 9; q++) {
+    const int r = q / 9, cw = q % 9;
+    uint32_t W = 0, M = 0;
+    for (int k = 0; k < 4; k++) {
+      const int c = 4 * cw + k, uu = c - kHalfPatch, vv = r - kHalfPatch;
+      const bool in = c < 33 && std::abs(uu) <= umax[std::abs(vv)];
+      W |= (uint32_t)(in ? c : 0) << (8 * k);
+      M |= (uint32_t)(in ? 1 : 0) << (8 * k);
+    }
+    icw[0][q] = W;
+    icw[1][q] = M;
   }
-  MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_icpatch), tab, sizeof(tab)));
+  MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_icw), icw, sizeof(icw)));
+  static const int pat[2048] = {
+#include "pattern_orb64.inc"
+  };
+  double patd[2048];
+  for (int i = 0; i < 2048; i++) patd[i] = (double)pat[i];
+  MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern_d), patd, sizeof(patd)));
   return MCS_OK;
 }
 
@@ -75,7 +91,6 @@ __device__ __forceinline__ int rot_round(double px, double py, double ca, double
 // gather batch.
 constexpr int kRawW = 9;    // dwords per raw patch row (33 bytes + alignment -> 36)
 constexpr int kRawH = 33;
-constexpr int kBlrW = 12;   // dwords per blurred patch row (43 bytes + alignment -> 48)
 constexpr int kBlrH = 43;
 
 __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
@@ -83,9 +98,38 @@ __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
   return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)((uintptr_t)g & 3));
 }
 
+// Blurred patch (+-21 around the keypoint) staged with 16-byte loads: blurred levels have a
+// 64-byte-aligned pitch, so every row shares the misalignment mis = (cx - 21) & 15 and
+// 4 aligned chunks of 16 bytes cover the 43 bytes of a row.
+constexpr int kBlrRow = 64;
+
+// IC moments of the raw patch staged in LDS (see c_icw)
+__device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int lane) {
+  uint32_t a10 = 0, aS = 0, a01 = 0;
+  int r = lane / kRawW, c = lane - kRawW * (lane / kRawW);
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const int q = lane + 64 * k;
+    if (q < kRawH * kRawW) {
+      const uint32_t px = rawp[q];
+      const uint32_t d1 = __builtin_amdgcn_udot4(c_icw[0][q], px, 0u, false);
+      const uint32_t d0 = __builtin_amdgcn_udot4(c_icw[1][q], px, 0u, false);
+      a10 += d1;
+      aS += d0;
+      a01 += (uint32_t)r * d0;
+    }
+    r += 7; c += 1;                       // q += 64 = 7 rows + 1 dword
+    if (c >= kRawW) { c -= kRawW; r++; }
+  }
+  const int S = dev::wave_sum((int)aS);
+  const int m10 = dev::wave_sum((int)a10) - kHalfPatch * S;
+  const int m01 = dev::wave_sum((int)a01) - kHalfPatch * S;
+  return fast_atan2_dev((float)m01, (float)m10);
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   __shared__ uint32_t s_raw[4][kRawH * kRawW];
-  __shared__ uint32_t s_blr[4][kBlrH * kBlrW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blr[4][kBlrH * kBlrRow];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int f, item;
   const int chunks = (a.sel_per_frame + 3) / 4;
@@ -108,52 +152,47 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
                                 : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
   const uint8_t* blr = a.blur + (int64_t)f * a.blur_fstride + L.img_off;
   // ---- stage both patches (independent loads, issued together)
+  const int mis = (cx - 21) & 15;
   {
     const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
-    for (int q = lane; q < kRawH * kRawW; q += 64) {
-      const int r = q / kRawW, c = q - r * kRawW;
-      s_raw[wv][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+    int r = lane / kRawW, c = lane - kRawW * (lane / kRawW);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int q = lane + 64 * k;
+      if (q < kRawH * kRawW) s_raw[wv][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+      r += 7; c += 1;
+      if (c >= kRawW) { c -= kRawW; r++; }
     }
-    const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21);
-    for (int q = lane; q < kBlrH * kBlrW; q += 64) {
-      const int r = q / kBlrW, c = q - r * kBlrW;
-      s_blr[wv][q] = load_aligned_dword(b0 + (int64_t)r * bp + 4 * c);
+    const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21 - mis);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int q = lane + 64 * k;        // chunk q: row q >> 2, 16-byte chunk q & 3
+      if (q < kBlrH * 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(b0 + (int64_t)(q >> 2) * bp + 16 * (q & 3));
+        *reinterpret_cast<uint4*>(&s_blr[wv][(q >> 2) * kBlrRow + 16 * (q & 3)]) = v;
+      }
     }
   }
   dev::wave_sync();
-  const uint8_t* raw = reinterpret_cast<const uint8_t*>(s_raw[wv]);
-  const uint8_t* bl = reinterpret_cast<const uint8_t*>(s_blr[wv]);
   // ---- IC_Angle: integer moments over the circular r=16 patch
-  int m10 = 0, m01 = 0;
-#pragma unroll
-  for (int t = 0; t < 18; t++) {
-    const int e = c_icpatch[t * 64 + lane];
-    const int u = (e & 0xFF) - 16, v = ((e >> 8) & 0xFF) - 16;
-    const int w = (e >> 16) & 1;
-    const int I = raw[(v + 16) * (4 * kRawW) + (u + 16)];
-    m10 += w * u * I;
-    m01 += w * v * I;
-  }
-  m10 = dev::wave_sum(m10);
-  m01 = dev::wave_sum(m01);
-  const float angle = fast_atan2_dev((float)m01, (float)m10);
+  const float angle = ic_angle_lds(s_raw[wv], lane);
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
-  const double ca = cos(theta), sa = sin(theta);
+  double ca, sa;
+  sincos(theta, &sa, &ca);
   const int nwords = a.desc_size / 8;
   uint8_t* dptr = a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size;
-  constexpr int BW = 4 * kBlrW;
-  const uint8_t* bc = bl + 21 * BW + 21;
+  const uint8_t* bc = &s_blr[wv][21 * kBlrRow + 21 + mis];
   uint64_t words[8];
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     if (r < nwords) {
       const int t = r * 64 + lane;  // test t: byte t/8, bit t%8
-      const double px0 = c_pattern[4 * t], py0 = c_pattern[4 * t + 1];
-      const double px1 = c_pattern[4 * t + 2], py1 = c_pattern[4 * t + 3];
-      const int o0 = rot_round(px0, py0, ca, sa, false) * BW + rot_round(px0, py0, ca, sa, true);
-      const int o1 = rot_round(px1, py1, ca, sa, false) * BW + rot_round(px1, py1, ca, sa, true);
+      const double px0 = c_pattern_d[4 * t], py0 = c_pattern_d[4 * t + 1];
+      const double px1 = c_pattern_d[4 * t + 2], py1 = c_pattern_d[4 * t + 3];
+      const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
+      const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
       words[r] = __ballot(bc[o0] < bc[o1]);
     }
   }
@@ -277,23 +316,7 @@ __global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
     }
   }
   dev::wave_sync();
-  float angle;
-  {
-    const uint8_t* raw = reinterpret_cast<const uint8_t*>(xs);
-    int m10 = 0, m01 = 0;
-#pragma unroll
-    for (int t = 0; t < 18; t++) {
-      const int e = c_icpatch[t * 64 + lane];
-      const int u = (e & 0xFF) - 16, v = ((e >> 8) & 0xFF) - 16;
-      const int w = (e >> 16) & 1;
-      const int I = raw[(v + 16) * (4 * kRawW) + (u + 16)];
-      m10 += w * u * I;
-      m01 += w * v * I;
-    }
-    m10 = dev::wave_sum(m10);
-    m01 = dev::wave_sum(m01);
-    angle = fast_atan2_dev((float)m01, (float)m10);
-  }
+  const float angle = ic_angle_lds(reinterpret_cast<const uint32_t*>(xs), lane);
   dev::wave_sync();
   // ---- undistorted keypoint (zero unless do_dBrief, :1304-1316)
   const mcs_cam_model& m = a.cams[a.cam_index ? a.cam_index[f] : 0];
@@ -311,7 +334,7 @@ __global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
     double ax, ay;
     sincos(ang, &ay, &ax);
     for (int p = lane; p < npts; p += 64) {
-      const double px = c_pattern[2 * p], py = c_pattern[2 * p + 1];
+      const double px = c_pattern_d[2 * p], py = c_pattern_d[2 * p + 1];
       const double xr = __dadd_rn(__dsub_rn(__dmul_rn(px, ax), __dmul_rn(py, ay)), ux);
       const double yr = __dadd_rn(__dadd_rn(__dmul_rn(px, ay), __dmul_rn(py, ax)), uy);
       double u, v;
