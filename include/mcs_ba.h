@@ -94,6 +94,57 @@ int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* 
 int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double* jac_pose,
                      double* jac_point);
 
+/* ---- Global BA and point-sharded BA (config E) ------------------------------------------
+ * cOptimizer::GlobalBundleAdjustment / BundleAdjustment (src/cOptimizer.cpp:59-261): every
+ * MultiKeyFrame and map point, information = I (:209), Huber delta = sqrt(5.991) (:161),
+ * keyframe mnId 0 fixed (:119-120, the caller sets pose_fixed), Mc / IO fixed, one
+ * optimize(15) (:241; the nIterations argument is ignored by the reference), poseOnly fixes
+ * every point (:178), results always written back (:244-261).
+ *
+ * Sharding: each rank holds a subset of the points with ALL of their edges;
+ * poses are replicated.  Per LM trial every rank forms its partial Schur complement
+ * S_r = Hpp_r - sum_{own points} Hpl Hll^-1 Hpl^T (lambda added by rank 0 only) and the
+ * partial rhs; one in-place SUM all-reduce of [S tiles | b_schur] gives every rank the same
+ * reduced camera system, which each rank factors redundantly (identical bits, no broadcast).
+ * Points are back-substituted locally; chi2 and the model-decrease terms are all-reduced as
+ * three scalars, so every rank takes the same LM decisions (lock step).
+ *
+ * The library never talks to the interconnect itself: `allreduce` (e.g. torch.distributed /
+ * RCCL on the caller's side) reduces xchg[offset, offset + count) in place across ranks and
+ * returns 0 when done.  The library synchronises its stream before every call and reads the
+ * buffer only after the callback returned. */
+enum { MCS_REDUCE_SUM = 0, MCS_REDUCE_MAX = 1 };
+typedef int32_t (*mcs_ba_allreduce_fn)(void* user, int32_t op, int64_t offset, int64_t count);
+typedef struct mcs_ba_shard {
+  int32_t rank, world;
+  double* xchg;                  /* device buffer of >= mcs_ba_xchg_doubles(n_poses) doubles */
+  int64_t xchg_cap;              /* its size in doubles */
+  mcs_ba_allreduce_fn allreduce;
+  void* user;
+} mcs_ba_shard;
+
+/* Exchange-buffer size (doubles) for problems with up to n_poses pose vertices. */
+int64_t mcs_ba_xchg_doubles(int32_t n_poses);
+
+/* mcs_ba_optimize over this rank's shard (shard == NULL or world == 1: single GPU). */
+int mcs_ba_optimize_sharded(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o,
+                            double* poses, double* points, const uint8_t* edge_level,
+                            double* edge_chi2, volatile int32_t* stop_flag, mcs_ba_report* rep,
+                            const mcs_ba_shard* shard);
+
+/* cOptimizer::BundleAdjustment after graph construction: optimize(15) with the terminate
+ * action (gain 1e-6, max 15), pose_only = 1 fixes every point.  p->huber_delta and
+ * p->edge_info are taken as given (the reference uses sqrt(5.991) and 1). */
+int mcs_global_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, int32_t pose_only, double* poses,
+                  double* points, volatile int32_t* stop_flag, mcs_ba_report* rep,
+                  const mcs_ba_shard* shard);
+
+/* Test hook for the dense reduced-camera solve (LinearSolverEigen::solve,
+ * ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126): S is n x n row-major (lower
+ * triangle read), b and x length n.  *zero_pivot = 1 when the LDL^T meets an exact zero. */
+int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
+                         int32_t* zero_pivot);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@
 // (robust chi2, model decrease), read back by the host driver.
 #include "common.hpp"
 #include "../../include/mcs_ba.h"
+#include "ldlt.hpp"
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -220,16 +221,17 @@ struct Dev {
   const int32_t* ps_ptr; const int32_t* ps_edges;     // CSR active poses  -> active edges
   const int32_t* blk_i; const int32_t* blk_j;         // lower pose blocks (i >= j)
   const int32_t* pr_ptr; const int32_t* pr_e1; const int32_t* pr_e2;  // edge pairs per block
+  int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
   double* err; double* w; double* jp; double* jl; double* hpl; double* y; double* chi; double* rchi;
   // system
   double* Hpp; double* bp; double* Hll; double* bl; double* Dinv; double* db;
-  double* S; double* bs; double* x;   // S: n x n row-major (lower triangle used)
+  double* S; double* bs; double* xp;   // S: lower 64x64 tiles (ldlt.hpp), bs / xp: 64 T
+  double* hdiag; double* bpf;          // [6 np] Hpp diagonal and b_p (all-reduced when sharded)
   double* red;                         // reduction scratch
-  int* flag;
 };
 
-// per active edge: error (+ robust chi2) and optionally Jacobians / weight
+// per active edge: error (+ robust chi2) and optionally Jacobians / weight / Hpl = w Jp^T Jl
 __global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= d.nae) return;
@@ -250,15 +252,21 @@ __global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
     edge_jac(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, jp, jl);
     for (int i = 0; i < 12; i++) d.jp[12 * e + i] = jp[i];
     for (int i = 0; i < 6; i++) d.jl[6 * e + i] = jl[i];
-    d.w[e] = r1 * d.e_info[e];
+    const double w = r1 * d.e_info[e];
+    d.w[e] = w;
+    if (d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
+      for (int a = 0; a < 6; a++)
+        for (int bb = 0; bb < 3; bb++)
+          d.hpl[18 * e + 3 * a + bb] = w * (jp[a] * jl[bb] + jp[6 + a] * jl[3 + bb]);
+    }
   }
 }
 
-// deterministic single-workgroup sum / max of n doubles -> out[0]
+// deterministic single-workgroup sum / max|.| of n doubles -> out[0]
 template <bool MAX>
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, int n, double* out) {
   __shared__ double s[1024];
-  double acc = MAX ? 0.0 : 0.0;
+  double acc = 0.0;
   for (int i = threadIdx.x; i < n; i += 1024) acc = MAX ? fmax(acc, fabs(v[i])) : acc + v[i];
   s[threadIdx.x] = acc;
   __syncthreads();
@@ -317,7 +325,7 @@ constexpr int kUpper6[21][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, 
                                 {2, 5}, {3, 3}, {3, 4}, {3, 5}, {4, 4}, {4, 5}, {5, 5}};
 
 // per active pose: Hpp (6x6, upper 21 mirrored), b_p; edges of the pose split over 256
-// threads (fixed stride), block tree sum
+// threads (fixed stride), block tree sum.  Also the diagonal and b_p into the exchange area.
 __global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
   __shared__ double sm[27 * 4];
   const int i = blockIdx.x, t = threadIdx.x;
@@ -346,17 +354,24 @@ __global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
     const double h = sm[t * 4];
     d.Hpp[36 * i + 6 * a + bb] = h;
     d.Hpp[36 * i + 6 * bb + a] = h;
-    if (a == bb) d.red[d.nl + 6 * i + a] = fabs(h);
+    if (a == bb) d.hdiag[6 * i + a] = h;
   } else if (t < 27) {
     d.bp[6 * i + t - 21] = sm[t * 4];
+    d.bpf[6 * i + t - 21] = sm[t * 4];
   }
 }
 
-// per active point: D = Hll + lambda I -> Dinv (cofactors), db = Dinv b_l;
-// per edge with a non-fixed pose: Hpl_e = w Jp^T Jl, Y_e = Hpl_e Dinv
+// One thread per (point, edge) entry of the point CSR: D = Hll + lambda I -> Dinv (cofactors,
+// recomputed per entry: identical bits), Y_e = Hpl_e Dinv; the first entry of each point
+// also stores Dinv and db = Dinv b_l.
 __global__ __launch_bounds__(256) void k_point_trial(Dev d, double lam) {
-  const int l = blockIdx.x * 256 + threadIdx.x;
-  if (l >= d.nl) return;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= d.npe) return;
+  const int e = d.pt_edges[q];
+  const int l = d.point_h[d.e_point[e]];
+  const bool first = (q == d.pt_ptr[l]);
+  const bool pose_act = d.pose_h[d.e_pose[e]] >= 0;
+  if (!first && !pose_act) return;
   double D[9];
   for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * l + k];
   D[0] += lam; D[4] += lam; D[8] += lam;
@@ -371,34 +386,30 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d, double lam) {
   Di[2] = (D[1] * D[5] - D[2] * D[4]) * id;
   Di[5] = (D[2] * D[3] - D[0] * D[5]) * id;
   Di[8] = (D[0] * D[4] - D[1] * D[3]) * id;
-  for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
-  const double* b = d.bl + 3 * l;
-  for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
-  for (int q = d.pt_ptr[l]; q < d.pt_ptr[l + 1]; q++) {
-    const int e = d.pt_edges[q];
-    if (d.pose_h[d.e_pose[e]] < 0) continue;
-    const double* jp = d.jp + 12 * e;
-    const double* jl = d.jl + 6 * e;
-    const double w = d.w[e];
-    double B[18];
+  if (first) {
+    for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
+    const double* b = d.bl + 3 * l;
+    for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
+  }
+  if (pose_act) {
+    const double* B = d.hpl + 18 * e;
+    double bb[18];
+    for (int k = 0; k < 18; k++) bb[k] = B[k];
     for (int a = 0; a < 6; a++)
-      for (int bb = 0; bb < 3; bb++) B[3 * a + bb] = w * (jp[a] * jl[bb] + jp[6 + a] * jl[3 + bb]);
-    for (int k = 0; k < 18; k++) d.hpl[18 * e + k] = B[k];
-    for (int a = 0; a < 6; a++)
-      for (int bb = 0; bb < 3; bb++)
-        d.y[18 * e + 3 * a + bb] = B[3 * a] * Di[bb] + B[3 * a + 1] * Di[3 + bb] + B[3 * a + 2] * Di[6 + bb];
+      for (int c = 0; c < 3; c++)
+        d.y[18 * e + 3 * a + c] = bb[3 * a] * Di[c] + bb[3 * a + 1] * Di[3 + c] + bb[3 * a + 2] * Di[6 + c];
   }
 }
 
-// reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lambda I)
+// reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lam0 I)
 //   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T;
 // diagonal blocks also form bschur_i = b_i - sum_e Hpl_e db(point(e)).
 // The pair list of a block is split over 256 threads (fixed stride) + block tree sum.
-__global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam) {
+// lam0 = lambda on rank 0 and 0 elsewhere (the sharded sum then holds lambda once).
+__global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam0) {
   __shared__ double sm[42 * 4];
   const int blk = blockIdx.x, t = threadIdx.x;
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
-  const int n = 6 * d.np;
   double acc[42];
 #pragma unroll
   for (int v = 0; v < 42; v++) acc[v] = 0.0;
@@ -417,8 +428,10 @@ __global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam) {
   if (bi == bj) {
     for (int q = d.ps_ptr[bi] + t; q < d.ps_ptr[bi + 1]; q += kRedNT) {
       const int e = d.ps_edges[q];
+      const int lh = d.point_h[d.e_point[e]];
+      if (lh < 0) continue;   // fixed point (pose-only BA): no Schur term
       const double* B = d.hpl + 18 * e;
-      const double* g = d.db + 3 * d.point_h[d.e_point[e]];
+      const double* g = d.db + 3 * lh;
       const double g0 = g[0], g1 = g[1], g2 = g[2];
 #pragma unroll
       for (int a = 0; a < 6; a++) acc[36 + a] += B[3 * a] * g0 + B[3 * a + 1] * g1 + B[3 * a + 2] * g2;
@@ -427,114 +440,21 @@ __global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam) {
   block_sum_vec<42>(acc, sm);
   if (t < 36) {
     const int a = t / 6, c = t % 6;
+    if (bi == bj && c > a) return;   // lower triangle of the diagonal block only
     double s0 = 0.0;
-    if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam; }
-    d.S[(6 * bi + a) * n + 6 * bj + c] = s0 - sm[t * 4];
+    if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam0; }
+    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - sm[t * 4];
   } else if (t < 42 && bi == bj) {
     const int a = t - 36;
     d.bs[6 * bi + a] = d.bp[6 * bi + a] - sm[t * 4];
   }
 }
 
-// LDL^T of the reduced camera system held in LDS (n <= kLdsN), right-looking, no pivoting
-// (Eigen SimplicialLDLT only fails on an exact zero pivot), then the two triangular solves
-// column by column.  One workgroup; zero pivot -> flag = 1.
-constexpr int kLdsN = 88;   // n*n + n doubles <= 62.6 KB of LDS
-__global__ __launch_bounds__(256) void k_ldlt_lds(Dev d) {
-  extern __shared__ double A[];   // n*n lower (row-major), then x[n]
-  __shared__ int fail;
-  const int n = 6 * d.np, t = threadIdx.x;
-  double* x = A + n * n;
-  for (int idx = t; idx < n * n; idx += 256) {
-    const int i = idx / n, j = idx - i * n;
-    A[idx] = (j <= i) ? d.S[idx] : 0.0;
-  }
-  for (int i = t; i < n; i += 256) x[i] = d.bs[i];
-  if (t == 0) fail = 0;
-  __syncthreads();
-  for (int j = 0; j < n; j++) {
-    const double dj = A[j * n + j];
-    if (dj == 0.0) { if (t == 0) fail = 1; break; }   // uniform: every thread reads the same dj
-    for (int i = j + 1 + t; i < n; i += 256) A[i * n + j] /= dj;
-    __syncthreads();
-    // trailing update A[i][m] -= (L_ij L_mj) d_j for j < m <= i
-    const int r = n - 1 - j;
-    for (int idx = t; idx < r * r; idx += 256) {
-      const int ii = idx / r, mm = idx - ii * r;
-      if (mm > ii) continue;
-      const int i = j + 1 + ii, m = j + 1 + mm;
-      A[i * n + m] -= (A[i * n + j] * A[m * n + j]) * dj;
-    }
-    __syncthreads();
-  }
-  __syncthreads();
-  if (fail) { if (t == 0) *d.flag = 1; return; }
-  // forward: L y = b (unit lower), column-oriented
-  for (int k = 0; k < n; k++) {
-    const double xk = x[k];
-    for (int i = k + 1 + t; i < n; i += 256) x[i] -= A[i * n + k] * xk;
-    __syncthreads();
-  }
-  for (int i = t; i < n; i += 256) x[i] /= A[i * n + i];
-  __syncthreads();
-  // backward: L^T x = y
-  for (int k = n - 1; k >= 0; k--) {
-    const double xk = x[k];
-    for (int i = t; i < k; i += 256) x[i] -= A[k * n + i] * xk;
-    __syncthreads();
-  }
-  for (int i = t; i < n; i += 256) d.x[i] = x[i];
-  if (t == 0) *d.flag = 0;
-}
-
-// LDL^T (no pivoting, lower, left-looking) + solve, one workgroup; zero pivot -> flag=1
-__global__ __launch_bounds__(256) void k_ldlt(Dev d) {
-  const int n = 6 * d.np, t = threadIdx.x;
-  double* S = d.S;  // overwritten with L (strictly lower) and D (diagonal)
-  __shared__ int fail;
-  if (t == 0) fail = 0;
-  __syncthreads();
-  for (int j = 0; j < n; j++) {
-    // d_j = S_jj - sum_k L_jk^2 D_k  (single thread, fixed order)
-    if (t == 0) {
-      double dj = S[j * n + j];
-      for (int k = 0; k < j; k++) dj -= S[j * n + k] * S[j * n + k] * S[k * n + k];
-      if (dj == 0.0) fail = 1;
-      S[j * n + j] = dj;
-    }
-    __syncthreads();
-    if (fail) break;
-    const double dj = S[j * n + j];
-    for (int i = j + 1 + t; i < n; i += 256) {
-      double s = S[i * n + j];
-      for (int k = 0; k < j; k++) s -= S[i * n + k] * S[j * n + k] * S[k * n + k];
-      S[i * n + j] = s / dj;
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    *d.flag = fail;
-    if (!fail) {
-      double* x = d.x;
-      for (int i = 0; i < n; i++) {
-        double s = d.bs[i];
-        for (int k = 0; k < i; k++) s -= S[i * n + k] * x[k];
-        x[i] = s;
-      }
-      for (int i = 0; i < n; i++) x[i] /= S[i * n + i];
-      for (int i = n - 1; i >= 0; i--) {
-        double s = x[i];
-        for (int k = i + 1; k < n; k++) s -= S[k * n + i] * x[k];
-        x[i] = s;
-      }
-    }
-  }
-}
-
-// x_l = Dinv (b_l - sum_e Hpl_e^T x_p); point = backup + x_l; per-point model decrease term
+// x_l = Dinv (b_l - sum_e Hpl_e^T x_p); point = backup + x_l; model-decrease terms:
+// red[k] (points, k < nl) and red[nl + i] (poses) summed separately (poses are replicated
+// across shards, points are not).
 __global__ __launch_bounds__(256) void k_update(Dev d, double lam) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  const int n = 6 * d.np;
   if (k < d.nl) {
     double c[3] = {d.bl[3 * k], d.bl[3 * k + 1], d.bl[3 * k + 2]};
     for (int q = d.pt_ptr[k]; q < d.pt_ptr[k + 1]; q++) {
@@ -543,14 +463,13 @@ __global__ __launch_bounds__(256) void k_update(Dev d, double lam) {
       if (i1 < 0) continue;
       const double* B = d.hpl + 18 * e;
       for (int b = 0; b < 3; b++)
-        for (int a = 0; a < 6; a++) c[b] -= B[3 * a + b] * d.x[6 * i1 + a];
+        for (int a = 0; a < 6; a++) c[b] -= B[3 * a + b] * d.xp[6 * i1 + a];
     }
     const double* Di = d.Dinv + 9 * k;
     double s = 0;
     const int v = d.hpt_vtx[k];
     for (int a = 0; a < 3; a++) {
       const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
-      d.x[n + 3 * k + a] = xa;
       d.points[3 * v + a] = d.points_bk[3 * v + a] + xa;
       s += xa * (lam * xa + d.bl[3 * k + a]);
     }
@@ -560,9 +479,9 @@ __global__ __launch_bounds__(256) void k_update(Dev d, double lam) {
     const int v = d.hpose_vtx[i];
     double s = 0;
     for (int a = 0; a < 6; a++) {
-      const double xa = d.x[6 * i + a];
+      const double xa = d.xp[6 * i + a];
       d.poses[6 * v + a] = d.poses_bk[6 * v + a] + xa;
-      s += xa * (lam * xa + d.bp[6 * i + a]);
+      s += xa * (lam * xa + d.bpf[6 * i + a]);
     }
     d.red[k] = s;
   }
@@ -613,59 +532,83 @@ struct HostStruct {
   int np = 0, nl = 0;
 };
 
-void build_structure(const mcs_ba_problem& p, const uint8_t* level, HostStruct& s) {
+// SparseOptimizer::initializeOptimization(0) + buildIndexMapping + BlockSolver::buildStructure
+// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295): active edges (level 0), active
+// non-fixed poses in vertex order (pose_cnt: number of active edges per pose over ALL shards),
+// active points in vertex order, CSR lists and the per-block edge pairs of the Schur
+// complement, all by counting sorts in edge order (deterministic).
+void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
+                     const std::vector<double>& pose_cnt, HostStruct& s) {
   s.aedge.clear();
-  for (int e = 0; e < p.n_edges; e++)
-    if (!level || level[e] == 0) s.aedge.push_back(e);
-  std::vector<int> ph(p.n_poses, 0), lh(p.n_points, 0);
-  for (int e : s.aedge) { ph[p.edge_pose[e]] = 1; lh[p.edge_point[e]] = 1; }
+  s.aedge.reserve(p.n_edges);
+  for (int e = 0; e < p.n_edges; e++)   // level 0 and not allVerticesFixed (:206-267)
+    if ((!level || level[e] == 0) && !(points_fixed && p.pose_fixed[p.edge_pose[e]])) s.aedge.push_back(e);
+  std::vector<char> lh(p.n_points, 0);
+  if (!points_fixed)
+    for (int e : s.aedge) lh[p.edge_point[e]] = 1;
   s.pose_h.assign(p.n_poses, -1);
   s.point_h.assign(p.n_points, -1);
   s.hpose_vtx.clear(); s.hpt_vtx.clear();
   s.np = s.nl = 0;
   for (int i = 0; i < p.n_poses; i++)
-    if (ph[i] && !p.pose_fixed[i]) { s.pose_h[i] = s.np++; s.hpose_vtx.push_back(i); }
+    if (pose_cnt[i] > 0 && !p.pose_fixed[i]) { s.pose_h[i] = s.np++; s.hpose_vtx.push_back(i); }
   for (int i = 0; i < p.n_points; i++)
     if (lh[i]) { s.point_h[i] = s.nl++; s.hpt_vtx.push_back(i); }
-  std::vector<std::vector<int>> pe(s.nl), se(s.np);
+  // CSR point -> edges, pose -> edges (counting sort, stable in edge order)
+  s.pt_ptr.assign(s.nl + 1, 0);
+  s.ps_ptr.assign(s.np + 1, 0);
   for (int e : s.aedge) {
-    pe[s.point_h[p.edge_point[e]]].push_back(e);
+    const int l = s.point_h[p.edge_point[e]];
+    if (l >= 0) s.pt_ptr[l + 1]++;
     const int h = s.pose_h[p.edge_pose[e]];
-    if (h >= 0) se[h].push_back(e);
+    if (h >= 0) s.ps_ptr[h + 1]++;
   }
-  s.pt_ptr.assign(1, 0); s.pt_edges.clear();
-  for (int l = 0; l < s.nl; l++) {
-    for (int e : pe[l]) s.pt_edges.push_back(e);
-    s.pt_ptr.push_back((int)s.pt_edges.size());
+  for (int l = 0; l < s.nl; l++) s.pt_ptr[l + 1] += s.pt_ptr[l];
+  for (int h = 0; h < s.np; h++) s.ps_ptr[h + 1] += s.ps_ptr[h];
+  s.pt_edges.assign(s.pt_ptr[s.nl], 0);
+  s.ps_edges.assign(s.ps_ptr[s.np], 0);
+  {
+    std::vector<int32_t> fp(s.pt_ptr.begin(), s.pt_ptr.end() - 1), fs(s.ps_ptr.begin(), s.ps_ptr.end() - 1);
+    for (int e : s.aedge) {
+      const int l = s.point_h[p.edge_point[e]];
+      if (l >= 0) s.pt_edges[fp[l]++] = e;
+      const int h = s.pose_h[p.edge_pose[e]];
+      if (h >= 0) s.ps_edges[fs[h]++] = e;
+    }
   }
-  s.ps_ptr.assign(1, 0); s.ps_edges.clear();
-  for (int i = 0; i < s.np; i++) {
-    for (int e : se[i]) s.ps_edges.push_back(e);
-    s.ps_ptr.push_back((int)s.ps_edges.size());
-  }
-  // lower pose blocks (i >= j) and their edge pairs, in (point, e1, e2) order
-  std::vector<std::vector<int>> pairs((size_t)s.np * s.np);
-  for (int l = 0; l < s.nl; l++)
-    for (int e1 : pe[l]) {
-      const int i1 = s.pose_h[p.edge_pose[e1]];
-      if (i1 < 0) continue;
-      for (int e2 : pe[l]) {
-        const int i2 = s.pose_h[p.edge_pose[e2]];
-        if (i2 < 0 || i2 > i1) continue;
-        auto& v = pairs[(size_t)i1 * s.np + i2];
-        v.push_back(e1);
-        v.push_back(e2);
+  // lower pose blocks (i >= j), block id i(i+1)/2 + j, and their edge pairs in
+  // (point, e1, e2) order
+  const size_t nblk = (size_t)s.np * (s.np + 1) / 2;
+  s.blk_i.resize(nblk); s.blk_j.resize(nblk);
+  for (int i = 0, b = 0; i < s.np; i++)
+    for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
+  s.pr_ptr.assign(nblk + 1, 0);
+  auto for_pairs = [&](auto&& f) {
+    for (int l = 0; l < s.nl; l++) {
+      const int q0 = s.pt_ptr[l], q1 = s.pt_ptr[l + 1];
+      for (int a = q0; a < q1; a++) {
+        const int e1 = s.pt_edges[a];
+        const int i1 = s.pose_h[p.edge_pose[e1]];
+        if (i1 < 0) continue;
+        for (int b = q0; b < q1; b++) {
+          const int e2 = s.pt_edges[b];
+          const int i2 = s.pose_h[p.edge_pose[e2]];
+          if (i2 < 0 || i2 > i1) continue;
+          f((size_t)i1 * (i1 + 1) / 2 + i2, e1, e2);
+        }
       }
     }
-  s.blk_i.clear(); s.blk_j.clear(); s.pr_ptr.assign(1, 0); s.pr_e1.clear(); s.pr_e2.clear();
-  for (int i = 0; i < s.np; i++)
-    for (int j = 0; j <= i; j++) {
-      s.blk_i.push_back(i);
-      s.blk_j.push_back(j);
-      auto& v = pairs[(size_t)i * s.np + j];
-      for (size_t q = 0; q < v.size(); q += 2) { s.pr_e1.push_back(v[q]); s.pr_e2.push_back(v[q + 1]); }
-      s.pr_ptr.push_back((int)s.pr_e1.size());
-    }
+  };
+  for_pairs([&](size_t blk, int, int) { s.pr_ptr[blk + 1]++; });
+  for (size_t b = 0; b < nblk; b++) s.pr_ptr[b + 1] += s.pr_ptr[b];
+  s.pr_e1.assign(s.pr_ptr[nblk], 0);
+  s.pr_e2.assign(s.pr_ptr[nblk], 0);
+  std::vector<int32_t> fill(s.pr_ptr.begin(), s.pr_ptr.end() - 1);
+  for_pairs([&](size_t blk, int e1, int e2) {
+    const int q = fill[blk]++;
+    s.pr_e1[q] = e1;
+    s.pr_e2[q] = e2;
+  });
 }
 
 template <typename T>
@@ -685,6 +628,312 @@ T* up_raw(mcs_ba_ctx* c, const T* src, size_t n, hipError_t& e) {
 }
 
 unsigned gb(int n) { return (unsigned)std::max(1, (n + 255) / 256); }
+
+// Exchange-buffer layout (offsets in doubles) for T tiles and np active poses; the head of
+// the buffer is reused for the structure exchange (pose activity counts) before T is known.
+struct XLayout {
+  size_t S, bs, hdiag, bpf, sc, total;
+  XLayout(int T, int np) {
+    S = 0;
+    bs = ldlt::tile_doubles(T);
+    hdiag = bs + (size_t)ldlt::TB * T;
+    bpf = hdiag + 6 * (size_t)np;
+    sc = bpf + 6 * (size_t)np;
+    total = sc + 16;
+  }
+};
+
+int64_t xchg_doubles(int32_t n_poses) {
+  const int np = std::max(0, n_poses);
+  const XLayout x(ldlt::tiles_for(std::max(1, 6 * np)), np);
+  return (int64_t)std::max<size_t>(x.total, (size_t)np + 16);
+}
+
+struct Shard {
+  int rank = 0, world = 1;
+  double* xchg = nullptr;
+  mcs_ba_allreduce_fn fn = nullptr;
+  void* user = nullptr;
+};
+
+int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
+                  double* points, const uint8_t* edge_level, double* edge_chi2,
+                  volatile int32_t* stop_flag, mcs_ba_report* rep, const mcs_ba_shard* shard_in,
+                  bool points_fixed) {
+  if (!c || !p || !o || !poses || !points) return MCS_ERR_ARG;
+  if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
+  for (int e = 0; e < p->n_edges; e++) {
+    if (p->edge_pose[e] < 0 || p->edge_pose[e] >= p->n_poses || p->edge_point[e] < 0 ||
+        p->edge_point[e] >= p->n_points || p->edge_cam[e] < 0 || p->edge_cam[e] >= p->n_cams) {
+      set_error("edge vertex index out of range");
+      return MCS_ERR_ARG;
+    }
+  }
+  MCS_HIP_CHECK(hipSetDevice(c->device));
+  Shard sh;
+  if (shard_in && shard_in->world > 1) {
+    if (!shard_in->xchg || !shard_in->allreduce || shard_in->rank < 0 || shard_in->rank >= shard_in->world ||
+        shard_in->xchg_cap < xchg_doubles(p->n_poses)) {
+      set_error("invalid mcs_ba_shard (exchange buffer too small or no allreduce callback)");
+      return MCS_ERR_ARG;
+    }
+    sh.rank = shard_in->rank; sh.world = shard_in->world; sh.xchg = shard_in->xchg;
+    sh.fn = shard_in->allreduce; sh.user = shard_in->user;
+  }
+  const bool sharded = sh.world > 1;
+  hipStream_t st = c->st;
+  c->free_all();
+  hipError_t he = hipSuccess;
+  if (!sharded) {
+    sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
+    if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+  }
+  // collective over xchg[off, off+cnt) (stream drained first); no-op on one rank
+  auto allreduce = [&](int op, size_t off, size_t cnt) -> int {
+    if (!sharded || cnt == 0) return MCS_OK;
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    if (sh.fn(sh.user, op, (int64_t)off, (int64_t)cnt) != 0) {
+      set_error("BA: allreduce callback failed");
+      return MCS_ERR_HIP;
+    }
+    return MCS_OK;
+  };
+  // all-reduce host scalars through the tail of the exchange buffer
+  auto allreduce_host = [&](double* v, int cnt, int op, size_t off) -> int {
+    if (!sharded) return MCS_OK;
+    MCS_HIP_CHECK(hipMemcpyAsync(sh.xchg + off, v, 8 * (size_t)cnt, hipMemcpyHostToDevice, st));
+    int rc = allreduce(op, off, cnt);
+    if (rc) return rc;
+    MCS_HIP_CHECK(hipMemcpyAsync(v, sh.xchg + off, 8 * (size_t)cnt, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    return MCS_OK;
+  };
+
+  // ---- structure: global pose activity (+ active point / edge counts)
+  int rc;
+  std::vector<double> cnt((size_t)p->n_poses + 2, 0.0);
+  {
+    int nae_l = 0;
+    std::vector<char> pt_seen(points_fixed ? 0 : p->n_points, 0);
+    int nl_l = 0;
+    for (int e = 0; e < p->n_edges; e++) {
+      if (edge_level && edge_level[e]) continue;
+      if (points_fixed && p->pose_fixed[p->edge_pose[e]]) continue;   // all vertices fixed
+      cnt[p->edge_pose[e]] += 1.0;
+      nae_l++;
+      if (!points_fixed && !pt_seen[p->edge_point[e]]) { pt_seen[p->edge_point[e]] = 1; nl_l++; }
+    }
+    cnt[p->n_poses] = nl_l;
+    cnt[p->n_poses + 1] = nae_l;
+    if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
+  }
+  HostStruct s;
+  build_structure(*p, edge_level, points_fixed, cnt, s);
+  const int nl_glob = (int)cnt[p->n_poses], nae_glob = (int)cnt[p->n_poses + 1];
+  if (rep) {
+    rep->n_active_edges = nae_glob;
+    rep->n_active_poses = s.np;
+    rep->n_active_points = nl_glob;
+    rep->iterations = 0;
+  }
+  const int n = 6 * s.np;
+  const int T = ldlt::tiles_for(std::max(1, n));
+  if ((size_t)T * ldlt::TB * 8 > 96 * 1024) {
+    set_error("more than 2048 active poses: exceeds the backward-solve LDS budget");
+    return MCS_ERR_UNSUPPORTED;
+  }
+  const XLayout X(T, s.np);
+  Dev d;
+  std::memset(&d, 0, sizeof(d));
+  const int NE = p->n_edges;
+  d.mc = up_raw(c, p->mc, 6 * (size_t)p->n_cams, he);
+  d.cam = up_raw(c, p->cam, 17 * (size_t)p->n_cams, he);
+  d.e_pose = up_raw(c, p->edge_pose, NE, he);
+  d.e_point = up_raw(c, p->edge_point, NE, he);
+  d.e_cam = up_raw(c, p->edge_cam, NE, he);
+  d.e_meas = up_raw(c, p->edge_meas, 2 * (size_t)NE, he);
+  d.e_info = up_raw(c, p->edge_info, NE, he);
+  d.delta = p->huber_delta;
+  d.dsqr = p->huber_delta * p->huber_delta;
+  double* d_poses = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
+  double* d_points = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
+  double* d_poses_bk = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
+  double* d_points_bk = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
+  d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
+  d.aedge = up(c, s.aedge, he); d.nae = (int)s.aedge.size();
+  d.pose_h = up(c, s.pose_h, he); d.point_h = up(c, s.point_h, he);
+  d.hpose_vtx = up(c, s.hpose_vtx, he); d.hpt_vtx = up(c, s.hpt_vtx, he);
+  d.np = s.np; d.nl = s.nl;
+  d.pt_ptr = up(c, s.pt_ptr, he); d.pt_edges = up(c, s.pt_edges, he);
+  d.npe = (int)s.pt_edges.size();
+  d.ps_ptr = up(c, s.ps_ptr, he); d.ps_edges = up(c, s.ps_edges, he);
+  d.blk_i = up(c, s.blk_i, he); d.blk_j = up(c, s.blk_j, he);
+  d.pr_ptr = up(c, s.pr_ptr, he); d.pr_e1 = up(c, s.pr_e1, he); d.pr_e2 = up(c, s.pr_e2, he);
+  auto dz = [&](size_t cnt_) { double* q = (double*)c->alloc(std::max<size_t>(1, cnt_) * 8); if (!q) he = hipErrorOutOfMemory; return q; };
+  d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
+  d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
+  d.Hpp = dz(36 * (size_t)s.np); d.bp = dz(6 * (size_t)s.np);
+  d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
+  d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
+  d.S = sh.xchg + X.S; d.bs = sh.xchg + X.bs; d.hdiag = sh.xchg + X.hdiag; d.bpf = sh.xchg + X.bpf;
+  d.xp = dz((size_t)ldlt::TB * T);
+  d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
+  ldlt::Work lw;
+  lw.L = dz(ldlt::tile_doubles(T));
+  lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
+  lw.z = dz((size_t)ldlt::TB * T);
+  double* d_scalar = dz(8);
+  int* d_flag = (int*)c->alloc(16);
+  if (he != hipSuccess || !d_flag) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
+
+  // control state agreed by all ranks: the caller's stop flag is folded into every scalar
+  // exchange, so no rank leaves the LM loop alone
+  volatile int32_t aux = 0;
+  volatile int32_t* stop = stop_flag ? stop_flag : &aux;
+  int agreed_stop = 0;
+  const size_t sc = X.sc;
+
+  auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate (all ranks)
+    hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
+    hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
+    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    double v[2] = {c->pinned[3], (double)(*stop != 0)};
+    int r = allreduce_host(v, 2, MCS_REDUCE_SUM, sc);
+    if (r) return r;
+    *out = v[0];
+    agreed_stop = v[1] > 0;
+    return MCS_OK;
+  };
+  auto copy_state = [&](double* dp, double* dl, const double* sp, const double* sl) -> int {
+    MCS_HIP_CHECK(hipMemcpyAsync(dp, sp, 48 * (size_t)p->n_poses, hipMemcpyDeviceToDevice, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(dl, sl, 24 * (size_t)p->n_points, hipMemcpyDeviceToDevice, st));
+    return MCS_OK;
+  };
+  double chi0 = 0;
+  if ((s.np + nl_glob) == 0 || nae_glob == 0) {
+    if (rep) rep->chi2_initial = rep->chi2_final = 0;
+  } else {
+    if ((rc = chi_now(&chi0))) return rc;
+    if (rep) rep->chi2_initial = chi0;
+    double lambda = 0, lastChi = 0;
+    int ni = 2, nBad = 0, it = 0;
+    bool ok = true;
+    double currentChi = chi0;
+    for (int i = 0; i < o->max_iterations && !agreed_stop && ok; i++) {
+      // ---- OptimizationAlgorithmLevenberg::solve(i)
+      // The robust chi2 of the linearisation point equals the chi2 the previous iteration
+      // ended with (same kernel, same state: accepted trial or restored backup), so only
+      // the first iteration reads anything back (the max diagonal for lambda's init).
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
+      hipLaunchKernelGGL(k_points_build, dim3(gb(s.nl)), dim3(256), 0, st, d);
+      if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
+      if ((rc = allreduce(MCS_REDUCE_SUM, X.hdiag, 12 * (size_t)s.np))) return rc;   // hdiag | bpf
+      if (i == 0) {
+        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
+        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.hdiag, 6 * s.np, d_scalar + 2);
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 16, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipStreamSynchronize(st));
+        double mx = std::max(c->pinned[1], c->pinned[2]);
+        if ((rc = allreduce_host(&mx, 1, MCS_REDUCE_MAX, sc))) return rc;
+        lambda = o->tau * mx; ni = 2; nBad = 0;
+      }
+      const double iniChi = currentChi;
+      double rho = 0;
+      int qmax = 0;
+      do {
+        if ((rc = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc;  // push
+        hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d, lambda);
+        MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
+        if (s.np) {
+          hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(kRedNT), 0, st, d,
+                             sh.rank == 0 ? lambda : 0.0);
+          MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
+          if ((rc = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc;   // S tiles | bs
+          MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
+        }
+        hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d, lambda);
+        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
+        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)(d.red + s.nl), s.np, d_scalar + 2);
+        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
+        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipStreamSynchronize(st));
+        double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
+        const double scale_pose = c->pinned[2];
+        const int fl = c->pinned_i[0];   // identical on every rank (same reduced system)
+        if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
+        agreed_stop = tr[2] > 0;
+        double tempChi = tr[0];
+        if (fl) tempChi = std::numeric_limits<double>::max();
+        rho = currentChi - tempChi;
+        double scale = scale_pose + tr[1];
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && std::isfinite(tempChi)) {
+          double alpha = 1. - std::pow((2 * rho - 1), 3);
+          alpha = std::min(alpha, 2. / 3.);
+          lambda *= std::max(1. / 3., alpha);
+          ni = 2;
+          currentChi = tempChi;
+        } else {
+          lambda *= ni;
+          ni *= 2;
+          if ((rc = copy_state(d_poses, d_points, d_poses_bk, d_points_bk))) return rc;  // pop
+        }
+        qmax++;
+      } while (rho < 0 && qmax < o->max_trials && !agreed_stop);
+      int result = 0;
+      if (qmax == o->max_trials || rho == 0) result = 1;
+      else {
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+        else nBad = 0;
+        if (nBad >= 3) result = 1;
+      }
+      ok = (result == 0);
+      ++it;
+      // ---- SparseOptimizerTerminateAction (post-iteration): activeRobustChi2 of the
+      // current state == currentChi (see above); identical on every rank
+      const double cur = currentChi;
+      if (rep && rep->trace_chi2 && i < rep->trace_cap) rep->trace_chi2[i] = cur;
+      if (i == 0) lastChi = cur;
+      else {
+        bool stopOpt = false;
+        if (i < o->terminate_max_iter) {
+          const double gain = (lastChi - cur) / cur;
+          lastChi = cur;
+          if (gain >= 0 && gain < o->gain_threshold) stopOpt = true;
+        } else {
+          stopOpt = true;
+        }
+        if (stopOpt) { *stop = 1; agreed_stop = 1; }
+      }
+      if (rep) rep->lambda_final = lambda;
+    }
+    if (rep) rep->iterations = it;
+    if (rep) rep->chi2_final = currentChi;
+  }
+  if (rep) rep->stop_flag = *stop;
+  MCS_HIP_CHECK(hipMemcpyAsync(poses, d_poses, 48 * (size_t)p->n_poses, hipMemcpyDeviceToHost, st));
+  MCS_HIP_CHECK(hipMemcpyAsync(points, d_points, 24 * (size_t)p->n_points, hipMemcpyDeviceToHost, st));
+  if (edge_chi2) {
+    // chi2 of every edge (active or not) at the final estimate
+    std::vector<int32_t> all(NE);
+    for (int e = 0; e < NE; e++) all[e] = e;
+    int32_t* d_all = up(c, all, he);
+    if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
+    Dev d2 = d;
+    d2.aedge = d_all;
+    d2.nae = NE;
+    d2.rchi = dz(NE);
+    hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
+    MCS_HIP_CHECK(hipMemcpyAsync(edge_chi2, d.chi, 8 * (size_t)NE, hipMemcpyDeviceToHost, st));
+  }
+  MCS_HIP_CHECK(hipStreamSynchronize(st));
+  MCS_HIP_CHECK(hipGetLastError());
+  return MCS_OK;
+}
 
 }  // namespace
 
@@ -730,195 +979,25 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
 int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o,
                     double* poses, double* points, const uint8_t* edge_level, double* edge_chi2,
                     volatile int32_t* stop_flag, mcs_ba_report* rep) {
-  if (!c || !p || !o || !poses || !points) return MCS_ERR_ARG;
-  if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
-  MCS_HIP_CHECK(hipSetDevice(c->device));
-  volatile int32_t aux = 0;
-  volatile int32_t* stop = stop_flag ? stop_flag : &aux;
-  HostStruct s;
-  build_structure(*p, edge_level, s);
-  if (rep) {
-    rep->n_active_edges = (int)s.aedge.size();
-    rep->n_active_poses = s.np;
-    rep->n_active_points = s.nl;
-    rep->iterations = 0;
-  }
-  const int n = 6 * s.np;
-  if (n > 6 * 256) {
-    set_error("more than 256 active poses: the dense LDL^T path is sized for LocalBA");
-    return MCS_ERR_UNSUPPORTED;
-  }
-  c->free_all();
-  hipError_t he = hipSuccess;
-  Dev d;
-  const int NE = p->n_edges;
-  d.mc = up_raw(c, p->mc, 6 * (size_t)p->n_cams, he);
-  d.cam = up_raw(c, p->cam, 17 * (size_t)p->n_cams, he);
-  d.e_pose = up_raw(c, p->edge_pose, NE, he);
-  d.e_point = up_raw(c, p->edge_point, NE, he);
-  d.e_cam = up_raw(c, p->edge_cam, NE, he);
-  d.e_meas = up_raw(c, p->edge_meas, 2 * (size_t)NE, he);
-  d.e_info = up_raw(c, p->edge_info, NE, he);
-  d.delta = p->huber_delta;
-  d.dsqr = p->huber_delta * p->huber_delta;
-  double* d_poses = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
-  double* d_points = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
-  double* d_poses_bk = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
-  double* d_points_bk = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
-  d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
-  d.aedge = up(c, s.aedge, he); d.nae = (int)s.aedge.size();
-  d.pose_h = up(c, s.pose_h, he); d.point_h = up(c, s.point_h, he);
-  d.hpose_vtx = up(c, s.hpose_vtx, he); d.hpt_vtx = up(c, s.hpt_vtx, he);
-  d.np = s.np; d.nl = s.nl;
-  d.pt_ptr = up(c, s.pt_ptr, he); d.pt_edges = up(c, s.pt_edges, he);
-  d.ps_ptr = up(c, s.ps_ptr, he); d.ps_edges = up(c, s.ps_edges, he);
-  d.blk_i = up(c, s.blk_i, he); d.blk_j = up(c, s.blk_j, he);
-  d.pr_ptr = up(c, s.pr_ptr, he); d.pr_e1 = up(c, s.pr_e1, he); d.pr_e2 = up(c, s.pr_e2, he);
-  auto dz = [&](size_t cnt) { double* q = (double*)c->alloc(std::max<size_t>(1, cnt) * 8); if (!q) he = hipErrorOutOfMemory; return q; };
-  d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
-  d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
-  d.Hpp = dz(36 * (size_t)s.np); d.bp = dz(6 * (size_t)s.np);
-  d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
-  d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
-  d.S = dz((size_t)n * n); d.bs = dz(n); d.x = dz(n + 3 * (size_t)s.nl);
-  d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
-  double* d_scalar = dz(4);
-  d.flag = (int*)c->alloc(16);
-  if (he != hipSuccess || !d.flag) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
-  hipStream_t st = c->st;
-  const int nvar = s.np + s.nl;
+  return optimize_impl(c, p, o, poses, points, edge_level, edge_chi2, stop_flag, rep, nullptr, false);
+}
 
-  auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate
-    hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
-    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
-    MCS_HIP_CHECK(hipStreamSynchronize(st));
-    *out = c->pinned[3];
-    return MCS_OK;
-  };
-  auto copy_state = [&](double* dp, double* dl, const double* sp, const double* sl) -> int {
-    MCS_HIP_CHECK(hipMemcpyAsync(dp, sp, 48 * (size_t)p->n_poses, hipMemcpyDeviceToDevice, st));
-    MCS_HIP_CHECK(hipMemcpyAsync(dl, sl, 24 * (size_t)p->n_points, hipMemcpyDeviceToDevice, st));
-    return MCS_OK;
-  };
-  int rc;
-  double chi0 = 0;
-  if (nvar == 0 || d.nae == 0) {
-    if (rep) rep->chi2_initial = rep->chi2_final = 0;
-  } else {
-    if ((rc = chi_now(&chi0))) return rc;
-    if (rep) rep->chi2_initial = chi0;
-    double lambda = 0, lastChi = 0;
-    int ni = 2, nBad = 0, it = 0;
-    bool ok = true;
-    double currentChi = chi0;
-    for (int i = 0; i < o->max_iterations && !(*stop) && ok; i++) {
-      // ---- OptimizationAlgorithmLevenberg::solve(i)
-      // The robust chi2 of the linearisation point equals the chi2 the previous iteration
-      // ended with (same kernel, same state: accepted trial or restored backup), so only
-      // the first iteration reads anything back (the max diagonal for lambda's init).
-      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
-      hipLaunchKernelGGL(k_points_build, dim3(gb(s.nl)), dim3(256), 0, st, d);
-      if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
-      if (i == 0) {
-        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl + 6 * s.np, d_scalar + 1);
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 8, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipStreamSynchronize(st));
-        lambda = o->tau * c->pinned[1]; ni = 2; nBad = 0;
-      }
-      const double iniChi = currentChi;
-      double rho = 0;
-      int qmax = 0;
-      do {
-        if ((rc = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc;  // push
-        hipLaunchKernelGGL(k_point_trial, dim3(gb(s.nl)), dim3(256), 0, st, d, lambda);
-        if (s.np) {
-          hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(kRedNT), 0, st, d, lambda);
-          if (n <= kLdsN)
-            hipLaunchKernelGGL(k_ldlt_lds, dim3(1), dim3(256), ((size_t)n * n + n) * 8, st, d);
-          else
-            hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), 0, st, d);
-        } else {
-          MCS_HIP_CHECK(hipMemsetAsync(d.flag, 0, 4, st));
-        }
-        hipLaunchKernelGGL(k_update, dim3(gb(nvar)), dim3(256), 0, st, d, lambda);
-        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.red, nvar, d_scalar + 2);
-        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d.flag, 4, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipStreamSynchronize(st));
-        const double tr[3] = {c->pinned[0], c->pinned[1], c->pinned[2]};
-        const int fl = c->pinned_i[0];
-        double tempChi = tr[0];
-        if (fl) tempChi = std::numeric_limits<double>::max();
-        rho = currentChi - tempChi;
-        double scale = tr[2];
-        scale += 1e-3;
-        rho /= scale;
-        if (rho > 0 && std::isfinite(tempChi)) {
-          double alpha = 1. - std::pow((2 * rho - 1), 3);
-          alpha = std::min(alpha, 2. / 3.);
-          lambda *= std::max(1. / 3., alpha);
-          ni = 2;
-          currentChi = tempChi;
-        } else {
-          lambda *= ni;
-          ni *= 2;
-          if ((rc = copy_state(d_poses, d_points, d_poses_bk, d_points_bk))) return rc;  // pop
-        }
-        qmax++;
-      } while (rho < 0 && qmax < o->max_trials && !(*stop));
-      int result = 0;
-      if (qmax == o->max_trials || rho == 0) result = 1;
-      else {
-        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-        else nBad = 0;
-        if (nBad >= 3) result = 1;
-      }
-      ok = (result == 0);
-      ++it;
-      // ---- SparseOptimizerTerminateAction (post-iteration): activeRobustChi2 of the
-      // current state == currentChi (see above)
-      const double cur = currentChi;
-      if (rep && rep->trace_chi2 && i < rep->trace_cap) rep->trace_chi2[i] = cur;
-      if (i == 0) lastChi = cur;
-      else {
-        bool stopOpt = false;
-        if (i < o->terminate_max_iter) {
-          const double gain = (lastChi - cur) / cur;
-          lastChi = cur;
-          if (gain >= 0 && gain < o->gain_threshold) stopOpt = true;
-        } else {
-          stopOpt = true;
-        }
-        if (stopOpt) *stop = 1;
-      }
-      if (rep) rep->lambda_final = lambda;
-    }
-    if (rep) rep->iterations = it;
-    const double fin = currentChi;
-    if (rep) rep->chi2_final = fin;
-  }
-  if (rep) rep->stop_flag = *stop;
-  MCS_HIP_CHECK(hipMemcpyAsync(poses, d_poses, 48 * (size_t)p->n_poses, hipMemcpyDeviceToHost, st));
-  MCS_HIP_CHECK(hipMemcpyAsync(points, d_points, 24 * (size_t)p->n_points, hipMemcpyDeviceToHost, st));
-  if (edge_chi2) {
-    // chi2 of every edge (active or not) at the final estimate
-    std::vector<int32_t> all(NE);
-    for (int e = 0; e < NE; e++) all[e] = e;
-    int32_t* d_all = up(c, all, he);
-    if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
-    Dev d2 = d;
-    d2.aedge = d_all;
-    d2.nae = NE;
-    d2.rchi = dz(NE);
-    hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
-    MCS_HIP_CHECK(hipMemcpyAsync(edge_chi2, d.chi, 8 * (size_t)NE, hipMemcpyDeviceToHost, st));
-  }
-  MCS_HIP_CHECK(hipStreamSynchronize(st));
-  MCS_HIP_CHECK(hipGetLastError());
-  return MCS_OK;
+int64_t mcs_ba_xchg_doubles(int32_t n_poses) { return xchg_doubles(n_poses); }
+
+int mcs_ba_optimize_sharded(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o,
+                            double* poses, double* points, const uint8_t* edge_level,
+                            double* edge_chi2, volatile int32_t* stop_flag, mcs_ba_report* rep,
+                            const mcs_ba_shard* shard) {
+  return optimize_impl(c, p, o, poses, points, edge_level, edge_chi2, stop_flag, rep, shard, false);
+}
+
+int mcs_global_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, int32_t pose_only, double* poses,
+                  double* points, volatile int32_t* stop_flag, mcs_ba_report* rep,
+                  const mcs_ba_shard* shard) {
+  mcs_ba_options o;
+  mcs_ba_default_options(&o);
+  o.max_iterations = 15;   // optimizer.optimize(15) (src/cOptimizer.cpp:241)
+  return optimize_impl(c, p, &o, poses, points, nullptr, nullptr, stop_flag, rep, shard, pose_only != 0);
 }
 
 int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* points,
@@ -980,6 +1059,55 @@ int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double
   MCS_HIP_CHECK(hipMemcpyAsync(jac_point, d.jl, 48 * (size_t)NE, hipMemcpyDeviceToHost, c->st));
   MCS_HIP_CHECK(hipStreamSynchronize(c->st));
   return MCS_OK;
+}
+
+int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
+                         int32_t* zero_pivot) {
+  if (!S || !b || !x || n < 1) return MCS_ERR_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device visible (no CPU fallback)");
+    return MCS_ERR_NO_DEVICE;
+  }
+  MCS_HIP_CHECK(hipSetDevice(device));
+  const int T = ldlt::tiles_for(n);
+  if ((size_t)T * ldlt::TB * 8 > 96 * 1024) return MCS_ERR_UNSUPPORTED;
+  const size_t NT = ldlt::tile_doubles(T), Np = (size_t)ldlt::TB * T;
+  std::vector<double> hA(NT, 0.0), hb(Np, 0.0);
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c <= r; c++) hA[ldlt::sidx(r, c)] = S[(size_t)r * n + c];
+  for (int r = 0; r < n; r++) hb[r] = b[r];
+  double *dA = nullptr, *db = nullptr, *dx = nullptr, *dL = nullptr, *dI = nullptr, *dz = nullptr;
+  int* dflag = nullptr;
+  hipStream_t st = nullptr;
+  int rc = MCS_OK;
+  auto chk = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && rc == MCS_OK) { set_hip_error(e, what, __FILE__, __LINE__); rc = MCS_ERR_HIP; }
+  };
+  chk(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+  chk(hipMalloc(&dA, NT * 8), "malloc"); chk(hipMalloc(&dL, NT * 8), "malloc");
+  chk(hipMalloc(&dI, (size_t)T * 4096 * 8), "malloc");
+  chk(hipMalloc(&db, Np * 8), "malloc"); chk(hipMalloc(&dx, Np * 8), "malloc"); chk(hipMalloc(&dz, Np * 8), "malloc");
+  chk(hipMalloc(&dflag, 16), "malloc");
+  if (rc == MCS_OK) {
+    chk(hipMemcpyAsync(dA, hA.data(), NT * 8, hipMemcpyHostToDevice, st), "h2d");
+    chk(hipMemcpyAsync(db, hb.data(), Np * 8, hipMemcpyHostToDevice, st), "h2d");
+    chk(hipMemsetAsync(dflag, 0, 4, st), "memset");
+    chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
+    ldlt::Work w{dL, dI, dz};
+    chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
+    std::vector<double> hx(Np);
+    int32_t fl = 0;
+    chk(hipMemcpyAsync(hx.data(), dx, Np * 8, hipMemcpyDeviceToHost, st), "d2h");
+    chk(hipMemcpyAsync(&fl, dflag, 4, hipMemcpyDeviceToHost, st), "d2h");
+    chk(hipStreamSynchronize(st), "sync");
+    for (int r = 0; r < n; r++) x[r] = hx[r];
+    if (zero_pivot) *zero_pivot = fl;
+  }
+  for (void* q : {(void*)dA, (void*)dL, (void*)dI, (void*)db, (void*)dx, (void*)dz, (void*)dflag})
+    if (q) (void)hipFree(q);
+  if (st) (void)hipStreamDestroy(st);
+  return rc;
 }
 
 }  // extern "C"

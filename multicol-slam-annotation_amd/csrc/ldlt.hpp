@@ -1,0 +1,44 @@
+// Dense LDL^T factor + solve of the reduced camera system on gfx950 (FP64 matrix cores).
+//
+// Replaces LinearSolverEigen::solve (ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126,
+// Eigen SimplicialLDLT without pivoting; an exact zero pivot fails the solve) for the Schur
+// complement produced by BlockSolver<6,3>::solve (block_solver.hpp:354-486).
+//
+// Storage: the symmetric matrix is held as its lower 64x64 tiles, tile (I, J) (I >= J) at
+// toff(I, J), each tile row-major.  n is padded to Np = 64 T with an identity block (zero
+// right-hand side), which leaves the solution of the leading n x n system unchanged.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+
+namespace mcs {
+namespace ldlt {
+
+constexpr int TB = 64;
+
+__host__ __device__ inline size_t toff(int I, int J) {
+  return ((size_t)I * (I + 1) / 2 + J) * (TB * TB);
+}
+// element (r, c) with r >= c (callers never address the strict upper triangle of a
+// diagonal tile through this)
+__host__ __device__ inline size_t sidx(int r, int c) {
+  return toff(r / TB, c / TB) + (size_t)(r % TB) * TB + (c % TB);
+}
+inline int tiles_for(int n) { return (n + TB - 1) / TB; }
+inline size_t tile_doubles(int T) { return (size_t)T * (T + 1) / 2 * TB * TB; }
+
+struct Work {
+  double* L;      // tile_doubles(T): off-diagonal L blocks (I > J)
+  double* Linv;   // T * 64 * 64: inverse of each unit-lower diagonal L block
+  double* z;      // 64 T: D^-1 L^-1 b
+};
+
+// A: tiles (destroyed), b: 64 T (destroyed), x: 64 T (out).  *flag (device) = 1 on an
+// exact zero pivot, else left untouched (callers clear it).  All launches on st.
+hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st);
+
+// Padding rows/columns [n, 64T): diagonal = diag_value, rest 0; b[n..64T) = 0.
+hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st);
+
+}  // namespace ldlt
+}  // namespace mcs

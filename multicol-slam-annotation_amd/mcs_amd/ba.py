@@ -274,3 +274,248 @@ class Solver:
         jl = np.zeros((n, 2, 3))
         _check(self._lib.mcs_ba_linearize(self._h, ctypes.byref(s), _p(err), _p(jp), _p(jl)))
         return err, jp, jl
+
+
+# ---------------------------------------------------------------------------
+# Global BA (config E) and point sharding
+# ---------------------------------------------------------------------------
+HUBER_GLOBAL = float(np.sqrt(5.991))     # cOptimizer::BundleAdjustment thHuber (src/cOptimizer.cpp:161)
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                ctypes.c_int64)
+
+
+class BAShard(ctypes.Structure):
+    """Mirror of mcs_ba_shard (include/mcs_ba.h)."""
+    _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32), ("xchg", ctypes.c_void_p),
+                ("xchg_cap", ctypes.c_int64), ("allreduce", ALLREDUCE_FN),
+                ("user", ctypes.c_void_p)]
+
+
+def ring_rig(ncams=8, size=1024, radius=0.12, phase_deg=10.0):
+    """Config D/E rig: `ncams` Lafida-polynomial fisheyes scaled to size x size, optical axes
+    horizontal and evenly spread in yaw, mounted on a ring of the given radius."""
+    cam = synth.scaled_cam(synth.LAFIDA_CAMS[0], size, size)
+    cams, mcs = [], []
+    for c in range(ncams):
+        ph = np.deg2rad(phase_deg + 360.0 * c / ncams)
+        ax = np.array([np.cos(ph), np.sin(ph), 0.0])
+        xc = np.array([-np.sin(ph), np.cos(ph), 0.0])
+        yc = np.array([0.0, 0.0, -1.0])
+        R = np.stack([xc, yc, -ax], 1)           # columns: camera axes in the body frame
+        mcs.append(np.concatenate([rot2cay(R), radius * ax]))
+        cams.append(dict(cam))
+    return cams, np.array(mcs)
+
+
+def make_global_problem(n_kf=200, n_points=50000, target_edges=400000, ncams=8, size=1024,
+                        seed=0, outlier_frac=0.02, noise_scale=0.5, pose_noise=(0.003, 0.01),
+                        point_noise=0.05, step=0.15, max_range=8.0):
+    """Config E: GlobalBA over n_kf MultiKeyFrames of an ncams ring rig, ~n_points points and
+    ~target_edges observations (vectorised generator).  BundleAdjustment semantics:
+    information = I (:209), Huber sqrt(5.991) (:161), keyframe 0 fixed (:119-120)."""
+    rng = np.random.default_rng(seed)
+    cams, mcs = ring_rig(ncams, size)
+    camv = np.stack([cam_vec(c) for c in cams])
+    cam = cams[0]
+    mask = synth.mirror_mask(cam)
+    # smooth planar trajectory (slow yaw drift), body z up
+    k = np.arange(n_kf)
+    yaw = 0.6 * np.sin(k / 40.0)
+    gt_poses = np.zeros((n_kf, 6))
+    pos = np.zeros(3)
+    for i in range(n_kf):
+        R = np.array([[np.cos(yaw[i]), -np.sin(yaw[i]), 0], [np.sin(yaw[i]), np.cos(yaw[i]), 0],
+                      [0, 0, 1]])
+        gt_poses[i, :3] = rot2cay(R)
+        gt_poses[i, 3:] = pos
+        pos = pos + step * np.array([np.cos(yaw[i]), np.sin(yaw[i]), 0.02 * np.sin(i / 7.0)])
+    # points on rays of random (kf, cam, pixel inside the mirror mask)
+    ys, xs = np.nonzero(mask[40:-40, 40:-40])
+    pick = rng.integers(len(xs), size=n_points)
+    u = xs[pick] + 40 + rng.uniform(0, 1, n_points)
+    v = ys[pick] + 40 + rng.uniform(0, 1, n_points)
+    rx, ry, rz = synth.img_to_world(cam, u, v)
+    depth = rng.uniform(1.5, max_range, n_points)
+    kk = rng.integers(n_kf, size=n_points)
+    cc = rng.integers(ncams, size=n_points)
+    Xc = np.stack([rx, ry, rz], 1) * depth[:, None]
+    Rt = cay2rot(gt_poses[kk, :3])
+    Rc = cay2rot(mcs[cc, :3])
+    Rw = Rt @ Rc
+    tw = np.einsum("nij,nj->ni", Rt, mcs[cc, 3:]) + gt_poses[kk, 3:]
+    pts = np.einsum("nij,nj->ni", Rw, Xc) + tw
+    # visibility of every point in every (kf, cam): in range, inside the mask, ray-consistent
+    rows, cols, uvs = [], [], []
+    for i in range(n_kf):
+        near = np.nonzero(np.linalg.norm(pts - gt_poses[i, 3:], axis=1) < max_range)[0]
+        if len(near) == 0:
+            continue
+        for c in range(ncams):
+            uv, Xc_ = project(gt_poses[i], mcs[c], camv[c], pts[near])
+            ok = np.isfinite(uv).all(-1)
+            ui = np.round(np.nan_to_num(uv[:, 0], nan=-1e6)).astype(np.int64)
+            vi = np.round(np.nan_to_num(uv[:, 1], nan=-1e6)).astype(np.int64)
+            ok &= (ui > 30) & (vi > 30) & (ui < size - 30) & (vi < size - 30)
+            idx = np.nonzero(ok)[0]
+            if len(idx) == 0:
+                continue
+            ok2 = mask[vi[idx], ui[idx]] > 0
+            rx, ry, rz = synth.img_to_world(cam, uv[idx, 0], uv[idx, 1])
+            d = Xc_[idx] / np.linalg.norm(Xc_[idx], axis=1, keepdims=True)
+            ok2 &= (rx * d[:, 0] + ry * d[:, 1] + rz * d[:, 2]) > 0.9999
+            idx = idx[ok2]
+            rows.append(near[idx])
+            cols.append(np.full(len(idx), i * ncams + c))
+            uvs.append(uv[idx])
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    uvs = np.concatenate(uvs)
+    # subsample observations towards the target (keep >= 2 per point when possible)
+    order = np.argsort(rows, kind="stable")
+    rows, cols, uvs = rows[order], cols[order], uvs[order]
+    cnt_all = np.bincount(rows, minlength=n_points)
+    forced = 2 * int((cnt_all >= 2).sum())
+    keep = rng.random(len(rows)) < min(1.0, max(0, target_edges - forced) / max(1, len(rows) - forced))
+    start = np.concatenate([[0], np.cumsum(cnt_all)[:-1]])
+    for j in (0, 1):   # force the first two observations of points that have >= 2
+        sel = cnt_all >= 2
+        keep[start[sel] + j] = True
+    rows, cols, uvs = rows[keep], cols[keep], uvs[keep]
+    cnt = np.bincount(rows, minlength=n_points)
+    good = cnt >= 2
+    m = good[rows]
+    rows, cols, uvs = rows[m], cols[m], uvs[m]
+    new_id = -np.ones(n_points, np.int64)
+    new_id[good] = np.arange(good.sum())
+    ne = len(rows)
+    lev = np.array([869, 724, 603, 503, 419, 349, 291, 242], np.float64)
+    octv = rng.choice(8, size=ne, p=lev / lev.sum())
+    meas = uvs + rng.normal(0, 1, (ne, 2)) * (noise_scale * 1.2 ** octv)[:, None]
+    out = rng.random(ne) < outlier_frac
+    meas[out] = rng.uniform(60, size - 60, (int(out.sum()), 2))
+    poses0 = gt_poses.copy()
+    pose_fixed = np.zeros(n_kf, np.uint8)
+    pose_fixed[0] = 1
+    poses0[1:, :3] += rng.normal(0, pose_noise[0], (n_kf - 1, 3))
+    poses0[1:, 3:] += rng.normal(0, pose_noise[1], (n_kf - 1, 3))
+    gt_pts = pts[good]
+    pts0 = gt_pts + rng.normal(0, point_noise, gt_pts.shape)
+    return dict(poses=poses0, pose_fixed=pose_fixed, points=pts0, mc=mcs, cam=camv,
+                edge_pose=(cols // ncams).astype(np.int32), edge_point=new_id[rows].astype(np.int32),
+                edge_cam=(cols % ncams).astype(np.int32), edge_meas=meas,
+                edge_info=np.ones(ne), huber_delta=HUBER_GLOBAL, gt_poses=gt_poses,
+                gt_points=gt_pts)
+
+
+def shard_points(pr, world):
+    """Contiguous point ranges with balanced edge counts -> list of (point_lo, point_hi)."""
+    npts = len(pr["points"])
+    cnt = np.bincount(pr["edge_point"], minlength=npts)
+    cum = np.cumsum(cnt)
+    tot = cum[-1] if npts else 0
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(np.searchsorted(cum, tot * r / world, side="left")) + 1 if npts else 0)
+    bounds.append(npts)
+    bounds = np.maximum.accumulate(np.minimum(np.array(bounds), npts))
+    return [(int(bounds[r]), int(bounds[r + 1])) for r in range(world)]
+
+
+def shard_problem(pr, rank, world):
+    """This rank's BA shard: the points [lo, hi) with ALL their edges (edge order kept),
+    every pose (replicated).  Returns (sub_problem, (lo, hi), edge_ids)."""
+    lo, hi = shard_points(pr, world)[rank]
+    ep = np.asarray(pr["edge_point"])
+    eids = np.nonzero((ep >= lo) & (ep < hi))[0]
+    sub = dict(pr)
+    sub["points"] = np.ascontiguousarray(pr["points"][lo:hi])
+    for k in ("edge_pose", "edge_cam", "edge_meas", "edge_info"):
+        sub[k] = np.ascontiguousarray(np.asarray(pr[k])[eids])
+    sub["edge_point"] = np.ascontiguousarray(ep[eids] - lo, dtype=np.int32)
+    return sub, (lo, hi), eids
+
+
+class TorchExchange:
+    """mcs_ba_shard backed by torch.distributed: the exchange buffer is a torch tensor on the
+    rank's GPU and the callback all-reduces a slice of it (backend "nccl" = RCCL over xGMI).
+    The library drains its stream before calling; the callback returns after the collective
+    has completed on the device."""
+
+    def __init__(self, n_poses, device, group=None):
+        import torch
+        import torch.distributed as dist
+        from . import lib
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        cap = int(lib().mcs_ba_xchg_doubles(int(n_poses)))
+        self.buf = torch.zeros(cap, dtype=torch.float64, device=device)
+        self._cb = ALLREDUCE_FN(self._allreduce)
+        self.shard = BAShard(self.rank, self.world, self.buf.data_ptr(), cap, self._cb, None)
+        self.calls = 0
+
+    def _allreduce(self, user, op, off, cnt):
+        try:
+            t = self.buf[off:off + cnt]
+            rop = self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX
+            self.dist.all_reduce(t, op=rop, group=self.group)
+            self.torch.cuda.synchronize(self.buf.device)
+            self.calls += 1
+            return 0
+        except Exception:   # never raise through the C stack
+            return 1
+
+
+def _solver_global_ba(self, pr, pose_only=False, stop_flag=None, exchange=None, trace=0):
+    """cOptimizer::BundleAdjustment (src/cOptimizer.cpp:73-261) on this rank's problem."""
+    from . import _check
+    s = as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    tr = np.zeros(max(trace, 1), np.float64)
+    rep = BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(tr) if trace else None, trace)
+    sf = None if stop_flag is None else ctypes.c_int32(int(stop_flag))
+    sh = ctypes.byref(exchange.shard) if exchange is not None else None
+    _check(self._lib.mcs_global_ba(self._h, ctypes.byref(s), 1 if pose_only else 0, _p(poses),
+                                   _p(points), ctypes.byref(sf) if sf is not None else None,
+                                   ctypes.byref(rep), sh))
+    return dict(poses=poses, points=points, report=rep,
+                stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
+
+
+def _solver_optimize_sharded(self, pr, exchange, options=None, edge_level=None, stop_flag=None,
+                             trace=0):
+    from . import _check
+    s = as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    lvl = np.zeros(len(pr["edge_pose"]), np.uint8) if edge_level is None else \
+        np.ascontiguousarray(edge_level, np.uint8)
+    chi = np.zeros(len(pr["edge_pose"]), np.float64)
+    o = options or BAOptions()
+    tr = np.zeros(max(trace, 1), np.float64)
+    rep = BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(tr) if trace else None, trace)
+    sf = None if stop_flag is None else ctypes.c_int32(int(stop_flag))
+    _check(self._lib.mcs_ba_optimize_sharded(self._h, ctypes.byref(s), ctypes.byref(o), _p(poses),
+                                             _p(points), _p(lvl), _p(chi),
+                                             ctypes.byref(sf) if sf is not None else None,
+                                             ctypes.byref(rep), ctypes.byref(exchange.shard)))
+    return dict(poses=poses, points=points, edge_chi2=chi, report=rep,
+                stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
+
+
+Solver.global_ba = _solver_global_ba
+Solver.optimize_sharded = _solver_optimize_sharded
+
+
+def dense_ldlt_solve(S, b, device=0):
+    """Device LDL^T solve of the reduced camera system (test hook) -> (x, zero_pivot)."""
+    from . import lib, _check
+    S = np.ascontiguousarray(S, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    n = S.shape[0]
+    x = np.zeros(n)
+    zp = ctypes.c_int32()
+    _check(lib().mcs_dense_ldlt_solve(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp)))
+    return x, zp.value

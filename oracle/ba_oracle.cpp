@@ -238,6 +238,8 @@ struct Graph {
   const mcs_ba_problem* P;
   std::vector<double> poses, points;   // current estimate
   std::vector<uint8_t> level;          // per edge, 0 active
+  bool points_fixed = false;           // BundleAdjustment(poseOnly): setFixed(poseOnly) (:178)
+  const double* pose_cnt = nullptr;    // optional: active-edge count per pose over ALL shards
   Huber hk;
   // active structure
   std::vector<int> aedges;             // active edges in id order
@@ -270,11 +272,14 @@ struct Graph {
   void initialize() {  // initializeOptimization(0) + buildIndexMapping
     const mcs_ba_problem& p = *P;
     aedges.clear();
+    // initializeOptimization (sparse_optimizer.cpp:206-267): level-0 edges that are not
+    // allVerticesFixed (Mc / IO are always fixed, so: pose fixed and point fixed)
     for (int e = 0; e < p.n_edges; e++)
-      if (level[e] == 0 && !p.pose_fixed[p.edge_pose[e]]) aedges.push_back(e);
-      else if (level[e] == 0) aedges.push_back(e);  // point vertices are never fixed
+      if (level[e] == 0 && !(p.pose_fixed[p.edge_pose[e]] && points_fixed)) aedges.push_back(e);
     std::vector<int> pose_has(p.n_poses, 0), pt_has(p.n_points, 0);
-    for (int e : aedges) { pose_has[p.edge_pose[e]] = 1; pt_has[p.edge_point[e]] = 1; }
+    for (int e : aedges) { pose_has[p.edge_pose[e]] = 1; pt_has[p.edge_point[e]] = !points_fixed; }
+    if (pose_cnt)
+      for (int i = 0; i < p.n_poses; i++) pose_has[i] = pose_cnt[i] > 0;
     pose_h.assign(p.n_poses, -1);
     point_h.assign(p.n_points, -1);
     np = nl = 0;
@@ -291,6 +296,7 @@ struct Graph {
     Hpl.assign(18 * p.n_edges, 0);
     for (int e : aedges) {
       const int pi = pose_h[p.edge_pose[e]], li = point_h[p.edge_point[e]];
+      if (pi < 0 && li < 0) continue;   // every vertex fixed: no contribution
       double jp[12], jl[6];
       edge_jac(&poses[6 * p.edge_pose[e]], &points[3 * p.edge_point[e]], p.mc + 6 * p.edge_cam[e],
                p.cam + 17 * p.edge_cam[e], jp, jl);
@@ -304,11 +310,12 @@ struct Graph {
           bp[6 * pi + a] += jp[a] * we[0] + jp[6 + a] * we[1];
         }
       }
-      for (int a = 0; a < 3; a++) {
-        for (int b = 0; b < 3; b++) Hll[9 * li + 3 * a + b] += w * (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
-        bl[3 * li + a] += jl[a] * we[0] + jl[3 + a] * we[1];
-      }
-      if (pi >= 0)
+      if (li >= 0)
+        for (int a = 0; a < 3; a++) {
+          for (int b = 0; b < 3; b++) Hll[9 * li + 3 * a + b] += w * (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
+          bl[3 * li + a] += jl[a] * we[0] + jl[3 + a] * we[1];
+        }
+      if (pi >= 0 && li >= 0)
         for (int a = 0; a < 6; a++)
           for (int b = 0; b < 3; b++) Hpl[18 * e + 3 * a + b] = w * (jp[a] * jl[b] + jp[6 + a] * jl[3 + b]);
     }
@@ -325,19 +332,32 @@ struct Graph {
 
   // BlockSolver::solve with lambda on the diagonal; returns false on an exact zero pivot
   bool solve(double lam) {
+    std::vector<double> S, bs;
+    schur(lam, lam, S, bs);
+    return factor_solve(S, bs);
+  }
+
+  // reduced camera system S = Hpp + lam_diag I - sum Hpl Hll(lam)^-1 Hpl^T, bs; also Dinv_
+  std::vector<double> Dinv_;
+  std::vector<std::vector<int>> pe_;
+  void schur(double lam, double lam_diag, std::vector<double>& S, std::vector<double>& bs) {
     const mcs_ba_problem& p = *P;
     const int n = 6 * np;
-    std::vector<double> S(n * n, 0.0), bs(n, 0.0);
+    S.assign((size_t)n * n, 0.0);
+    bs.assign(n, 0.0);
     for (int i = 0; i < np; i++)
       for (int a = 0; a < 6; a++) {
         for (int b = 0; b < 6; b++) S[(6 * i + a) * n + 6 * i + b] = Hpp[36 * i + 6 * a + b];
-        S[(6 * i + a) * n + 6 * i + a] += lam;
+        S[(6 * i + a) * n + 6 * i + a] += lam_diag;
         bs[6 * i + a] = bp[6 * i + a];
       }
-    std::vector<double> Dinv(9 * nl);
+    std::vector<double>& Dinv = Dinv_;
+    Dinv.assign(9 * nl, 0.0);
     // edges grouped per point in edge order
-    std::vector<std::vector<int>> pe(nl);
-    for (int e : aedges) pe[point_h[p.edge_point[e]]].push_back(e);
+    std::vector<std::vector<int>>& pe = pe_;
+    pe.assign(nl, {});
+    for (int e : aedges)
+      if (point_h[p.edge_point[e]] >= 0) pe[point_h[p.edge_point[e]]].push_back(e);
     for (int l = 0; l < nl; l++) {
       double D[9];
       for (int k = 0; k < 9; k++) D[k] = Hll[9 * l + k];
@@ -377,8 +397,15 @@ struct Graph {
         }
       }
     }
+  }
+
+  bool factor_solve(const std::vector<double>& S, const std::vector<double>& bs) {
+    const mcs_ba_problem& p = *P;
+    const int n = 6 * np;
+    const std::vector<double>& Dinv = Dinv_;
+    const std::vector<std::vector<int>>& pe = pe_;
     // LDL^T without pivoting (lower), solve
-    std::vector<double> L(n * n, 0.0), Dg(n, 0.0);
+    std::vector<double> L((size_t)n * n, 0.0), Dg(n, 0.0);
     for (int j = 0; j < n; j++) {
       double d = S[j * n + j];
       for (int k = 0; k < j; k++) d -= L[j * n + k] * L[j * n + k] * Dg[k];
@@ -565,6 +592,55 @@ int oracle_ba_optimize(const mcs_ba_problem* p, const mcs_ba_options* o, double*
     }
   }
   return 0;
+}
+
+// cOptimizer::BundleAdjustment (src/cOptimizer.cpp:73-261) after graph construction:
+// optimize(15) with the terminate action; poseOnly fixes every point (:178)
+int oracle_global_ba(const mcs_ba_problem* p, int32_t pose_only, double* poses, double* points,
+                     int32_t* stop_flag, mcs_ba_report* rep) {
+  mcs_ba_options o;
+  o.max_iterations = 15; o.gain_threshold = 1e-6; o.terminate_max_iter = 15; o.max_trials = 10;
+  o.tau = 1e-5;
+  Graph g;
+  g.P = p;
+  g.poses.assign(poses, poses + 6 * p->n_poses);
+  g.points.assign(points, points + 3 * p->n_points);
+  g.level.assign(p->n_edges, 0);
+  g.points_fixed = pose_only != 0;
+  g.hk.delta = p->huber_delta;
+  g.hk.dsqr = p->huber_delta * p->huber_delta;
+  optimize(g, o, stop_flag, rep);
+  std::memcpy(poses, g.poses.data(), sizeof(double) * 6 * p->n_poses);
+  std::memcpy(points, g.points.data(), sizeof(double) * 3 * p->n_points);
+  return 0;
+}
+
+// One rank's share of the reduced camera system at the given estimate:
+// S_r = Hpp_r + lam_diag I - sum_{own points} Hpl Hll(lam)^-1 Hpl^T (n x n row-major, full)
+// and bs_r; pose_cnt = active-edge count per pose over all shards (nullable = this problem).
+// Summing S_r / bs_r over the shards (lam_diag = lam on one rank, 0 elsewhere) gives the
+// unsharded system.  Returns n = 6 * (active poses).
+int oracle_ba_partial_schur(const mcs_ba_problem* p, const double* pose_cnt, double lam,
+                            double lam_diag, double* S_out, int32_t s_cap, double* bs_out) {
+  Graph g;
+  g.P = p;
+  g.poses.assign(p->poses, p->poses + 6 * p->n_poses);
+  g.points.assign(p->points, p->points + 3 * p->n_points);
+  g.level.assign(p->n_edges, 0);
+  g.pose_cnt = pose_cnt;
+  g.hk.delta = p->huber_delta;
+  g.hk.dsqr = p->huber_delta * p->huber_delta;
+  g.initialize();
+  g.err.assign(2 * p->n_edges, 0.0);
+  g.compute_errors();
+  g.build_system();
+  std::vector<double> S, bs;
+  g.schur(lam, lam_diag, S, bs);
+  const int n = 6 * g.np;
+  if (n > s_cap) return -1;
+  std::memcpy(S_out, S.data(), sizeof(double) * (size_t)n * n);
+  std::memcpy(bs_out, bs.data(), sizeof(double) * n);
+  return n;
 }
 
 // cOptimizer::LocalBundleAdjustment (src/cOptimizer.cpp:771-903) after graph construction

@@ -1,0 +1,265 @@
+"""Global BA (cOptimizer::BundleAdjustment, src/cOptimizer.cpp:73-261), the dense reduced-camera
+LDL^T (LinearSolverEigen::solve, ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126) and
+point-sharded BA.
+
+Tolerances: dense solve relative residual <= 1e-10 (well-conditioned SPD); GPU vs oracle robust
+chi2 per iteration rel 1e-6, poses abs 1e-6, well-constrained points abs 1e-5, identical
+iteration counts (same as tests/test_ba.py).  Sharded vs unsharded: the Schur sum is
+re-associated across ranks, so the same tolerances apply; every rank must hold bit-identical
+poses (lock-step).
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from tests import oracle_bind as ob
+
+
+@pytest.fixture(scope="module")
+def gproblem():
+    from mcs_amd import ba
+    return ba.make_global_problem(n_kf=24, n_points=3000, target_edges=24000, ncams=8, seed=1)
+
+
+def _oracle_global(pr, pose_only=False, trace=20):
+    from mcs_amd import ba
+    L = ob.lib()
+    f = L.oracle_global_ba
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
+    s = ba.as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    tr = np.zeros(trace)
+    rep = ba.BAReport(0, 0, 0, 0, 0, 0, 0, 0, ob._p(tr), trace)
+    sf = ctypes.c_int32(0)
+    f(ctypes.byref(s), 1 if pose_only else 0, ob._p(poses), ob._p(points), ctypes.byref(sf),
+      ctypes.byref(rep))
+    return dict(poses=poses, points=points, report=rep, trace=tr[:min(trace, rep.iterations)],
+                stop_flag=sf.value)
+
+
+def _partial_schur(pr, pose_cnt, lam, lam_diag):
+    from mcs_amd import ba
+    L = ob.lib()
+    f = L.oracle_ba_partial_schur
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double, ctypes.c_double,
+                  ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    s = ba.as_struct(pr)
+    cap = 6 * len(pr["poses"])
+    S = np.zeros(cap * cap)
+    bs = np.zeros(cap)
+    pc = None if pose_cnt is None else np.ascontiguousarray(pose_cnt, np.float64)
+    n = f(ctypes.byref(s), None if pc is None else ob._p(pc), lam, lam_diag, ob._p(S), cap,
+          ob._p(bs))
+    assert n >= 0
+    return S[:n * n].reshape(n, n), bs[:n]
+
+
+def test_global_problem_shape(gproblem):
+    pr = gproblem
+    assert pr["pose_fixed"][0] == 1 and pr["pose_fixed"][1:].sum() == 0
+    assert np.all(pr["edge_info"] == 1.0)
+    assert abs(pr["huber_delta"] - np.sqrt(5.991)) < 1e-15
+    cnt = np.bincount(pr["edge_point"], minlength=len(pr["points"]))
+    assert cnt.min() >= 2
+
+
+def test_shard_points_partition(gproblem):
+    from mcs_amd import ba
+    for world in (1, 2, 3, 8):
+        rng = ba.shard_points(gproblem, world)
+        assert rng[0][0] == 0 and rng[-1][1] == len(gproblem["points"])
+        assert all(rng[i][1] == rng[i + 1][0] for i in range(world - 1))
+        eids = np.concatenate([ba.shard_problem(gproblem, r, world)[2] for r in range(world)])
+        assert np.array_equal(np.sort(eids), np.arange(len(gproblem["edge_pose"])))
+
+
+def test_oracle_global_ba_converges(gproblem):
+    o = _oracle_global(gproblem)
+    assert o["report"].chi2_final < o["report"].chi2_initial and o["report"].iterations >= 2
+    assert o["report"].n_active_poses == len(gproblem["poses"]) - 1
+    po = _oracle_global(gproblem, pose_only=True)
+    assert po["report"].n_active_points == 0
+    assert np.array_equal(po["points"], gproblem["points"])
+    # edges whose every vertex is fixed (keyframe 0 + fixed points) are not active
+    n0 = int((gproblem["edge_pose"] == 0).sum())
+    assert po["report"].n_active_edges == len(gproblem["edge_pose"]) - n0
+
+
+def _gloo_partial_schur(rank, world, port, pr, ret):
+    import torch
+    import torch.distributed as dist
+    from mcs_amd import ba
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    try:
+        sub, _, _ = ba.shard_problem(pr, rank, world)
+        cnt = torch.tensor(np.bincount(sub["edge_pose"], minlength=len(pr["poses"])).astype(np.float64))
+        dist.all_reduce(cnt)   # global pose activity (as the library's structure exchange)
+        S, bs = _partial_schur(sub, cnt.numpy(), 1e-3, 1e-3 if rank == 0 else 0.0)
+        t = torch.tensor(np.concatenate([S.ravel(), bs]))
+        dist.all_reduce(t)
+        ret[rank] = t.numpy()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_schur_sum_equals_full_gloo(gproblem):
+    """world_size 2 over gloo: the sum of the per-rank partial Schur complements (points
+    sharded with all their edges, lambda on rank 0 only) equals the unsharded system."""
+    import torch.multiprocessing as mp
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    world = 2
+    mgr = mp.get_context("spawn").Manager()
+    ret = mgr.dict()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_gloo_partial_schur, args=(r, world, port, gproblem, ret))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    S, bs = _partial_schur(gproblem, None, 1e-3, 1e-3)
+    full = np.concatenate([S.ravel(), bs])
+    for r in range(world):
+        got = ret[r]
+        assert np.allclose(got, full, rtol=1e-10, atol=1e-9 * np.abs(full).max())
+    assert np.array_equal(ret[0], ret[1])
+
+
+# ------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 6, 60, 64, 65, 130, 600, 1194])
+def test_gpu_dense_ldlt_solve(gpu, n):
+    from mcs_amd import ba
+    rng = np.random.default_rng(n)
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    x, zp = ba.dense_ldlt_solve(S, b)
+    assert zp == 0
+    ref = np.linalg.solve(S, b)
+    assert np.linalg.norm(S @ x - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(S, 2))
+    assert np.allclose(x, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.gpu
+def test_gpu_dense_ldlt_zero_pivot(gpu):
+    from mcs_amd import ba
+    S = np.eye(70)
+    S[3, 3] = 0.0
+    _, zp = ba.dense_ldlt_solve(S, np.ones(70))
+    assert zp == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pose_only", [False, True])
+def test_gpu_global_ba_matches_oracle(gpu, gproblem, pose_only):
+    from mcs_amd import ba
+    S = ba.Solver()
+    g = S.global_ba(gproblem, pose_only=pose_only, trace=20)
+    o = _oracle_global(gproblem, pose_only=pose_only, trace=20)
+    assert g["report"].iterations == o["report"].iterations
+    assert g["report"].n_active_edges == o["report"].n_active_edges
+    assert g["report"].n_active_poses == o["report"].n_active_poses
+    assert g["report"].n_active_points == o["report"].n_active_points
+    assert np.allclose(g["trace"], o["trace"], rtol=1e-6)
+    assert np.abs(g["poses"] - o["poses"]).max() < 1e-6
+    cnt = np.bincount(gproblem["edge_point"], minlength=len(gproblem["points"]))
+    wc = cnt >= 3
+    assert np.abs(g["points"][wc] - o["points"][wc]).max() < 1e-5
+    if pose_only:
+        assert np.array_equal(g["points"], gproblem["points"])
+
+
+class ThreadExchange:
+    """In-process stand-in for the collective: `world` ranks run on threads of one process,
+    each with its own solver context / stream and exchange buffer on the same GPU."""
+
+    def __init__(self, world, n_poses):
+        import torch
+        from mcs_amd import ba, lib
+        self.world = world
+        cap = int(lib().mcs_ba_xchg_doubles(int(n_poses)))
+        self.bufs = [torch.zeros(cap, dtype=torch.float64, device="cuda") for _ in range(world)]
+        self.bar = threading.Barrier(world)
+        self.calls = [[] for _ in range(world)]
+        self.fns, self.shards = [], []
+        for r in range(world):
+            fn = ba.ALLREDUCE_FN(lambda u, op, off, cnt, r=r: self._cb(r, op, off, cnt))
+            self.fns.append(fn)
+            self.shards.append(ba.BAShard(r, world, self.bufs[r].data_ptr(), cap, fn, None))
+
+    def _cb(self, r, op, off, cnt):
+        import torch
+        try:
+            self.calls[r].append((op, off, cnt))
+            self.bar.wait(60)
+            if r == 0:
+                sl = [b[off:off + cnt] for b in self.bufs]
+                acc = sl[0].clone()
+                for t in sl[1:]:
+                    acc = acc + t if op == 0 else torch.maximum(acc, t)
+                for t in sl:
+                    t.copy_(acc)
+                torch.cuda.synchronize()
+            self.bar.wait(60)
+            return 0
+        except Exception:
+            return 1
+
+    class _One:
+        def __init__(self, shard):
+            self.shard = shard
+
+    def member(self, r):
+        return ThreadExchange._One(self.shards[r])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_global_ba_lockstep(gpu, gproblem, world):
+    from mcs_amd import ba
+    X = ThreadExchange(world, len(gproblem["poses"]))
+    out = [None] * world
+    err = [None] * world
+
+    def run(r):
+        try:
+            sub, rng, _ = ba.shard_problem(gproblem, r, world)
+            out[r] = (ba.Solver().global_ba(sub, exchange=X.member(r), trace=20), rng)
+        except Exception as e:   # surfaced below
+            err[r] = e
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert all(e is None for e in err), err
+    # every rank took the same collectives and ended with bit-identical poses
+    assert all(X.calls[r] == X.calls[0] for r in range(world))
+    for r in range(1, world):
+        assert np.array_equal(out[r][0]["poses"], out[0][0]["poses"])
+        assert out[r][0]["report"].iterations == out[0][0]["report"].iterations
+    pts = np.zeros_like(gproblem["points"])
+    for g, (lo, hi) in out:
+        pts[lo:hi] = g["points"]
+    full = ba.Solver().global_ba(gproblem, trace=20)
+    g0 = out[0][0]
+    assert g0["report"].iterations == full["report"].iterations
+    assert g0["report"].n_active_edges == full["report"].n_active_edges
+    assert g0["report"].n_active_points == full["report"].n_active_points
+    assert np.allclose(g0["trace"], full["trace"], rtol=1e-6)
+    assert np.abs(g0["poses"] - full["poses"]).max() < 1e-6
+    cnt = np.bincount(gproblem["edge_point"], minlength=len(gproblem["points"]))
+    wc = cnt >= 3
+    assert np.abs(pts[wc] - full["points"][wc]).max() < 1e-5
