@@ -32,6 +32,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "kfeatures/sec + LocalBA iters/sec, 3×754×480 fisheye, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# FP64 dense matrix peak of MI355X (AMD spec, 78.6 TFLOP/s; v_mfma_f64_16x16x4_f64).  Not
+# listed in the local guide: tools/mfma_f64_peak.hip measures the per-CU issue rate.
+FP64_MFMA_PEAK_TFLOPS = 78.6
 # algorithmic bytes of pyramid + FAST per 754x480 camera-frame
 PYR_FAST_BYTES_754x480 = 2_970_708
 
@@ -86,6 +89,72 @@ def _oracle_top2(ob, q, t):
     return bi, bd, sd
 
 
+def run_global_ba(args, rank, world, local_rank, dev):
+    """Config E: GlobalBA (cOptimizer::BundleAdjustment) over 200 MultiKeyFrames / ~50k points /
+    ~400k edges of an 8-camera 1024^2 ring rig.  N GPUs: points sharded with all their edges,
+    poses replicated, one RCCL all-reduce of the reduced camera system per LM trial
+    (strong scaling: the same problem on every N).  Returns (result dict, cpu baseline)."""
+    if args.gba_calls <= 0:
+        return None, None
+    import torch
+    import torch.distributed as dist
+    from mcs_amd import ba as mba
+    pr = mba.make_global_problem(n_kf=args.gba_kf, n_points=args.gba_points,
+                                 target_edges=args.gba_edges, seed=7)
+    xch = None
+    sub = pr
+    if world > 1:
+        sub, _, _ = mba.shard_problem(pr, rank, world)
+        xch = mba.TorchExchange(len(pr["poses"]), dev)
+    solver = mba.Solver(device=local_rank)
+    solver.global_ba(sub, exchange=xch)       # warm-up (allocations, code objects)
+    solver.enable_timing(True)
+    solver.read_timing(reset=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.gba_calls):
+        r = solver.global_ba(sub, exchange=xch)
+        iters += r["report"].iterations
+    tg = time.perf_counter() - t0
+    st, n_it, n_tr, n = solver.read_timing(reset=True)
+    tt = torch.tensor([tg], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    tg = float(tt.item())
+    # dense LDL^T of the n x n reduced camera system per trial: n^3/3 multiply-adds for the
+    # factorisation (2 flop each) + 2 n^2 for the two triangular solves
+    flops = 2.0 * n ** 3 / 3.0 + 4.0 * n * n
+    t_solve = st["solve"] / max(1, n_tr) / 1e3
+    achieved = flops / t_solve / 1e12 if t_solve > 0 else None
+    out = {"iters_per_s": round(iters / tg, 2), "ms_per_call": round(tg / args.gba_calls * 1e3, 2),
+           "iterations_per_call": r["report"].iterations,
+           "chi2": [r["report"].chi2_initial, r["report"].chi2_final],
+           "scaling": "strong", "parallelism": "points sharded over %d rank(s)" % world,
+           "problem": "config E: %d MKF (1 fixed), %d points, %d edges, 8 cams 1024^2" % (
+               len(pr["poses"]), len(pr["points"]), len(pr["edge_pose"])),
+           "stage_ms_per_trial": {k: round(v / max(1, n_tr), 4) for k, v in st.items()},
+           "trials": n_tr,
+           "roofline_solve": {"kernel": "ldlt k_panel x T + k_backward (n=%d)" % n, "bound": "mfma",
+                              "achieved": None if achieved is None else round(achieved, 4),
+                              "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": None if achieved is None else round(achieved / FP64_MFMA_PEAK_TFLOPS, 5),
+                              "flops_per_trial": flops}}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from tests import oracle_bind as ob
+        o = mba.BAOptions(max_iterations=1, terminate_max_iter=15)
+        t0 = time.perf_counter()
+        rr = ob.ba_optimize(pr, options=o)
+        tc = time.perf_counter() - t0
+        cpu = {"value": round(rr["report"].iterations / tc, 4), "unit": "GlobalBA iters/s",
+               "cores": 1, "kind": "port",
+               "sample": "1 LM iteration of config E (oracle restatement, dense LDL^T, single thread)"}
+    return out, cpu
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +167,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stage-timing", type=int, default=1)
     ap.add_argument("--ba-calls", type=int, default=5, help="timed LocalBA calls (config C)")
+    ap.add_argument("--gba-calls", type=int, default=2, help="timed GlobalBA calls (config E)")
+    ap.add_argument("--gba-kf", type=int, default=200)
+    ap.add_argument("--gba-points", type=int, default=50000)
+    ap.add_argument("--gba-edges", type=int, default=400000)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -239,6 +312,8 @@ def main():
                       "unit": "LocalBA iters/s", "cores": 1, "kind": "port",
                       "sample": "1 LocalBA call (config C), oracle restatement, single thread"}
 
+    gba, cpu_gba = run_global_ba(args, rank, world, local_rank, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         S = min(args.cpu_sample, U)
@@ -270,6 +345,8 @@ def main():
             "cpu_baseline": cpu,
             "localba": localba,
             "cpu_baseline_localba": cpu_ba,
+            "globalba": gba,
+            "cpu_baseline_globalba": cpu_gba,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),
         }

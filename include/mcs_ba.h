@@ -139,6 +139,16 @@ int mcs_global_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, int32_t pose_only, dou
                   double* points, volatile int32_t* stop_flag, mcs_ba_report* rep,
                   const mcs_ba_shard* shard);
 
+/* Stage timing (device time from HIP events on the context's stream; the exchange stage is
+ * host wall time around the allreduce callback).  Stages: 0 linearize (errors, Jacobians,
+ * Hpp / Hll / b), 1 Schur (Hll^-1, Y = Hpl Hll^-1, reduced camera system), 2 exchange
+ * (all-reduce of the reduced system, sharded runs only), 3 dense LDL^T solve, 4 update
+ * (back-substitution, oplus, chi2).  ms[] accumulates over calls until read with reset. */
+#define MCS_BA_NSTAGES 5
+int mcs_ba_enable_timing(mcs_ba_ctx* c, int32_t on);
+int mcs_ba_read_timing(mcs_ba_ctx* c, double* ms, int32_t* n_iterations, int32_t* n_trials,
+                       int32_t* last_n, int32_t reset);
+
 /* Test hook for the dense reduced-camera solve (LinearSolverEigen::solve,
  * ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126): S is n x n row-major (lower
  * triangle read), b and x length n.  *zero_pivot = 1 when the LDL^T meets an exact zero. */

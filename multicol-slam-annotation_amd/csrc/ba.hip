@@ -19,6 +19,7 @@
 #include "../../include/mcs_ba.h"
 #include "ldlt.hpp"
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -503,6 +504,12 @@ struct mcs_ba_ctx {
   size_t next = 0;
   double* pinned = nullptr;   // host-pinned readback scalars
   int32_t* pinned_i = nullptr;
+  // optional stage timing (mcs_ba_enable_timing): HIP events on st around each stage,
+  // accumulated after the per-trial synchronisation the LM control needs anyway
+  bool timing = false;
+  hipEvent_t ev[8] = {};
+  double acc_ms[MCS_BA_NSTAGES] = {};
+  int32_t n_iter = 0, n_trial = 0, last_n = 0;
   void* alloc(size_t bytes) {
     bytes += 64;
     if (next < bufs.size() && caps[next] >= bytes) return bufs[next++];
@@ -682,6 +689,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   }
   const bool sharded = sh.world > 1;
   hipStream_t st = c->st;
+  auto rec = [&](int k) { if (c->timing) (void)hipEventRecord(c->ev[k], st); };
+  auto ms = [&](int a, int b) { float f = 0.f; (void)hipEventElapsedTime(&f, c->ev[a], c->ev[b]); return (double)f; };
   c->free_all();
   hipError_t he = hipSuccess;
   if (!sharded) {
@@ -692,10 +701,13 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   auto allreduce = [&](int op, size_t off, size_t cnt) -> int {
     if (!sharded || cnt == 0) return MCS_OK;
     MCS_HIP_CHECK(hipStreamSynchronize(st));
+    const auto t0 = std::chrono::steady_clock::now();
     if (sh.fn(sh.user, op, (int64_t)off, (int64_t)cnt) != 0) {
       set_error("BA: allreduce callback failed");
       return MCS_ERR_HIP;
     }
+    if (c->timing)
+      c->acc_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MCS_OK;
   };
   // all-reduce host scalars through the tail of the exchange buffer
@@ -825,9 +837,13 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       // The robust chi2 of the linearisation point equals the chi2 the previous iteration
       // ended with (same kernel, same state: accepted trial or restored backup), so only
       // the first iteration reads anything back (the max diagonal for lambda's init).
+      rec(0);
       hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
       hipLaunchKernelGGL(k_points_build, dim3(gb(s.nl)), dim3(256), 0, st, d);
       if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
+      rec(1);
+      c->n_iter++;
+      bool lin_pending = c->timing;
       if ((rc = allreduce(MCS_REDUCE_SUM, X.hdiag, 12 * (size_t)s.np))) return rc;   // hdiag | bpf
       if (i == 0) {
         hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
@@ -843,15 +859,21 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       int qmax = 0;
       do {
         if ((rc = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc;  // push
+        rec(2);
         hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d, lambda);
         MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
         if (s.np) {
           hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(kRedNT), 0, st, d,
                              sh.rank == 0 ? lambda : 0.0);
           MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
+          rec(3);
           if ((rc = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc;   // S tiles | bs
+          rec(4);
           MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
+        } else {
+          rec(3); rec(4);
         }
+        rec(5);
         hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d, lambda);
         hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
         hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)(d.red + s.nl), s.np, d_scalar + 2);
@@ -859,7 +881,16 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
         MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
         MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
+        rec(6);
         MCS_HIP_CHECK(hipStreamSynchronize(st));
+        if (c->timing) {
+          if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
+          c->acc_ms[1] += ms(2, 3);
+          c->acc_ms[3] += ms(4, 5);
+          c->acc_ms[4] += ms(5, 6);
+          c->n_trial++;
+          c->last_n = n;
+        }
         double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
         const double scale_pose = c->pinned[2];
         const int fl = c->pinned_i[0];   // identical on every rank (same reduced system)
@@ -973,7 +1004,31 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_i) (void)hipHostFree(c->pinned_i);
   if (c->st) (void)hipStreamDestroy(c->st);
+  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   delete c;
+}
+
+int mcs_ba_enable_timing(mcs_ba_ctx* c, int32_t on) {
+  if (!c) return MCS_ERR_ARG;
+  MCS_HIP_CHECK(hipSetDevice(c->device));
+  if (on && !c->ev[0])
+    for (auto& e : c->ev) MCS_HIP_CHECK(hipEventCreate(&e));
+  c->timing = on != 0;
+  return MCS_OK;
+}
+
+int mcs_ba_read_timing(mcs_ba_ctx* c, double* ms, int32_t* n_iterations, int32_t* n_trials,
+                       int32_t* last_n, int32_t reset) {
+  if (!c) return MCS_ERR_ARG;
+  for (int k = 0; k < MCS_BA_NSTAGES; k++) if (ms) ms[k] = c->acc_ms[k];
+  if (n_iterations) *n_iterations = c->n_iter;
+  if (n_trials) *n_trials = c->n_trial;
+  if (last_n) *last_n = c->last_n;
+  if (reset) {
+    for (double& v : c->acc_ms) v = 0.0;
+    c->n_iter = c->n_trial = 0;
+  }
+  return MCS_OK;
 }
 
 int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o,

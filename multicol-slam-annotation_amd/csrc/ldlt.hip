@@ -28,47 +28,102 @@ __device__ __forceinline__ void load_tile(double* s, const double* __restrict__ 
   for (int e = threadIdx.x; e < TB * TB; e += 256) s[(e >> 6) * LS + (e & 63)] = g[e];
 }
 
-// In-LDS LDL^T of a 64x64 tile (lower triangle read).  On return the strict lower triangle
-// holds L, the diagonal holds D.  One barrier per column: column j is scaled by 1/d_j during
-// step j+1 (nothing reads it after step j's update).
-__device__ void factor_tile(double* sA, int* fail) {
-  const int t = threadIdx.x, i = t & 63, g = t >> 6;
-  double inv_prev = 0.0;
-  for (int j = 0; j < TB; j++) {
-    const double dj = sA[j * LS + j];
-    if (dj == 0.0 && t == 0) *fail = 1;
-    const double inv = 1.0 / dj;
-    if (j > 0 && g == 0 && i > j - 1) sA[i * LS + j - 1] *= inv_prev;
-    if (i > j) {
-      const double aij = sA[i * LS + j] * inv;
-      for (int m = j + 1 + g; m <= i; m += 4) sA[i * LS + m] -= aij * sA[m * LS + j];
-    }
-    inv_prev = inv;
-    __syncthreads();
+// diagonal tile: only the lower triangle is defined (the strict upper part of the storage is
+// never written by the producers and may hold stale bits), so it is loaded as 0
+__device__ __forceinline__ void load_tile_lower(double* s, const double* __restrict__ g) {
+  for (int e = threadIdx.x; e < TB * TB; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    s[r * LS + c] = (c <= r) ? g[e] : 0.0;
   }
 }
 
-// Linv = L^-1 (unit lower) into sI: lane c of wave 0 computes column c row by row,
-// Linv[r][c] = [r == c] - sum_{m<r} L[r][m] Linv[m][c]; L reads are broadcasts, the column
-// reads / writes are lane-consecutive (conflict-free).  Entries above the diagonal come out 0.
-__device__ void invert_unit_lower(const double* sA, double* sI) {
-  const int t = threadIdx.x;
-  if (t < TB) {
-    const int c = t;
-    for (int r = 0; r < TB; r++) {
-      const double* Lr = sA + r * LS;
-      double s0 = (r == c) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-      int m = 0;
-      for (; m + 3 < r; m += 4) {
-        s0 -= Lr[m] * sI[m * LS + c];
-        s1 -= Lr[m + 1] * sI[(m + 1) * LS + c];
-        s2 -= Lr[m + 2] * sI[(m + 2) * LS + c];
-        s3 -= Lr[m + 3] * sI[(m + 3) * LS + c];
-      }
-      for (; m < r; m++) s0 -= Lr[m] * sI[m * LS + c];
-      sI[r * LS + c] = (s0 + s1) + (s2 + s3);
-    }
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, register resident:
+// lane = row i, wave g owns the columns m = g + 4q.  A runtime loop runs over groups of 4
+// columns (j = 4 jj + gj, gj unrolled): the trailing-matrix registers a[] are shifted by one
+// after every group, so the column the owning wave gj works on is always a[0] and the code
+// stays small (a fully unrolled sweep is ~55 KB and runs instruction-fetch bound).
+// e[q] holds row i of E = L^-1 (column g + 4q), built by applying every elimination row
+// operation to the identity.
+// Per column j, before the barrier: the owning wave forms l_i = A[i][j] / d_j, publishes l_i
+// and c_i = A[i][j] and writes L / D of column j into sA; lane j of every wave publishes its
+// (final) row j of E is read from lane j of the same wave.  After the barrier every wave
+// updates its registers:
+// A[i][m] -= l_i c_m (m > j), E[i][m] -= l_i E[j][m] (m <= j).  Updates are branch-free
+// (masked operands are 0 and l_i = 0 for rows i <= j, so the FMA leaves the value exact).
+// Exchange buffers are double-buffered by column parity: one barrier per column.
+// On return sA holds L (strict lower) and D (diagonal), sI holds L^-1 (0 above the diagonal).
+__device__ __forceinline__ void factor_tile(double* sA, double* sI, double* scol, int* fail) {
+  const int t = threadIdx.x, i = t & 63, g = t >> 6;
+  double a[16], e[16];
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    a[q] = sA[i * LS + g + 4 * q];
+    e[q] = (i == g + 4 * q) ? 1.0 : 0.0;
   }
+  // scol layout (doubles): colL [2][64] | colC [2][4][16]
+  double* colL = scol;
+  double* colC = scol + 128;
+  __syncthreads();   // sA is rewritten column by column below
+  for (int jj = 0; jj < TB / 4; jj++) {
+#pragma unroll
+    for (int gj = 0; gj < 4; gj++) {
+      const int j = 4 * jj + gj, bf = gj & 1;
+      // every wave forms the candidate (only the owner's is published): no branch around
+      // register updates
+      const double dj = readlane_d(a[0], j);
+      const double c = a[0];
+      const double l = c / dj;
+      if (g == gj) {
+        if (dj == 0.0 && i == 0) *fail = 1;
+        colL[bf * 64 + i] = l;
+        const int slot = (i >> 2) - jj;   // register slot of row i's column after the shifts
+        if (slot >= 0) colC[bf * 64 + (i & 3) * 16 + slot] = c;
+        sA[i * LS + j] = (i > j) ? l : c;
+      }
+      __syncthreads();
+      // unconditional loads, masks applied as multipliers (all operands finite), so the
+      // compiler emits no branches between the LDS reads
+      const double lv = colL[bf * 64 + i];
+      const double li = (i > j) ? lv : 0.0;   // select, not a multiply: rows <= j may hold inf
+      // c of column g + 4 (q + jj); slots past the tile hold stale values, which only reach
+      // registers that stand for columns past the tile (never read back)
+      const double2* cg = reinterpret_cast<const double2*>(colC + bf * 64 + g * 16);
+      double cv[16];
+#pragma unroll
+      for (int q2 = 0; q2 < 8; q2++) {
+        const double2 v = cg[q2];
+        cv[2 * q2] = v.x;
+        cv[2 * q2 + 1] = v.y;
+      }
+      // a[q] is column g + 4 (q + jj) > j  <=>  g + 4 q > gj: only q = 0 can be <= j
+      cv[0] = (g > gj) ? cv[0] : 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) a[q] = __builtin_fma(-li, cv[q], a[q]);
+      // E row j of this wave's columns lives in lane j of the same wave: readlane, no LDS
+      // (a single-lane LDS publish of the row measured ~2000 cycles per column)
+      // E[j][m] == 0 for m > j: skip those readlanes (wave-uniform branch; each readlane
+      // pair costs ~25 cycles)
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        if (g + 4 * q <= j) {
+          const double ej = readlane_d(e[q], j);
+          e[q] = __builtin_fma(-li, ej, e[q]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 15; q++) a[q] = a[q + 1];
+    a[15] = 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) sI[i * LS + g + 4 * q] = e[q];
+  __syncthreads();
 }
 
 // acc = X Y^T (64x64x64), wave w owns output columns [16w, 16w+16), acc[q] rows [16q, 16q+16)
@@ -112,6 +167,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   double* sY = sX + TB * LS;     // A_jk -> W_j
   double* sv = sY + TB * LS;     // b_k
   double* su = sv + TB;          // u_k = Linv b_k
+  double* scol = su + TB;        // factor_tile column exchange (512 doubles)
   __shared__ int fail;
   const int t = threadIdx.x;
   const int wg = blockIdx.x;
@@ -126,16 +182,14 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   }
   const bool rhs = (wg == 0) || (i == j);
   if (t == 0) fail = 0;
-  load_tile(sK, A + toff(k, k));
+  load_tile_lower(sK, A + toff(k, k));
   if (wg > 0) {
     load_tile(sX, A + toff(i, k));
     if (j != i) load_tile(sY, A + toff(j, k));
   }
   if (rhs && t < TB) sv[t] = b[k * TB + t];
   __syncthreads();
-  factor_tile(sK, &fail);
-  invert_unit_lower(sK, sI);
-  __syncthreads();
+  factor_tile(sK, sI, scol, &fail);
   if (rhs) {
     const double u = gemv_row(sI, sv);
     if ((t & 3) == 0) su[t >> 2] = u;
@@ -187,41 +241,50 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   }
 }
 
-// L^T x = z, one workgroup; z is staged in LDS and updated right-looking.
-__global__ __launch_bounds__(256) void k_backward(const double* __restrict__ L,
-                                                  const double* __restrict__ Linv,
-                                                  const double* __restrict__ z,
-                                                  double* __restrict__ x, int T) {
-  extern __shared__ double sz[];   // 64 T
-  __shared__ double part[4][TB];
-  __shared__ double xk[TB];
+// L^T x = z, one workgroup of 1024 threads, left-looking:
+//   x_k = Linv_kk^T (z_k - sum_{i>k} L_ik^T x_i)
+// thread (c = t & 63, g = t >> 6) sums rows r = g (mod 16) of every tile below the diagonal
+// (all loads independent, coalesced over c); the 16 partials are combined in a fixed order.
+constexpr int kBwdNT = 1024;
+__global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ L,
+                                                     const double* __restrict__ Linv,
+                                                     const double* __restrict__ z,
+                                                     double* __restrict__ x, int T) {
+  extern __shared__ double sx[];   // 64 T: solved blocks of x
+  __shared__ double part[16][TB];
+  __shared__ double rk[TB];
   const int t = threadIdx.x, c = t & 63, g = t >> 6;
-  const int Np = T * TB;
-  for (int e = t; e < Np; e += 256) sz[e] = z[e];
-  __syncthreads();
   for (int k = T - 1; k >= 0; k--) {
-    // x_k = Linv_kk^T z_k : x[c] = sum_m Linv[m][c] z[m]
-    const double* I = Linv + (size_t)k * TB * TB;
-    double s = 0.0;
-    for (int m = g; m < TB; m += 4) s += I[m * TB + c] * sz[k * TB + m];
-    part[g][c] = s;
+    double s0 = 0.0, s1 = 0.0;
+    for (int ib = k + 1; ib < T; ib++) {
+      const double* Lik = L + toff(ib, k);
+      const double* xi = sx + ib * TB;
+      s0 += Lik[g * TB + c] * xi[g];
+      s1 += Lik[(g + 16) * TB + c] * xi[g + 16];
+      s0 += Lik[(g + 32) * TB + c] * xi[g + 32];
+      s1 += Lik[(g + 48) * TB + c] * xi[g + 48];
+    }
+    part[g][c] = s0 + s1;
     __syncthreads();
     if (t < TB) {
-      const double v = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-      xk[t] = v;
-      x[k * TB + t] = v;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) acc += part[q][t];
+      rk[t] = z[k * TB + t] - acc;
     }
     __syncthreads();
-    // z_j[c] -= sum_r L_kj[r][c] x_k[r], j < k
-    for (int o = t; o < k * TB; o += 256) {
-      const int jb = o >> 6, cc = o & 63;
-      const double* Lkj = L + toff(k, jb);
-      double a0 = 0.0, a1 = 0.0;
-      for (int r = 0; r < TB; r += 2) {
-        a0 += Lkj[r * TB + cc] * xk[r];
-        a1 += Lkj[(r + 1) * TB + cc] * xk[r + 1];
-      }
-      sz[jb * TB + cc] -= a0 + a1;
+    // x_k[c] = sum_m Linv[m][c] r[m], rows m = g (mod 16)
+    const double* I = Linv + (size_t)k * TB * TB;
+    double u = I[g * TB + c] * rk[g] + I[(g + 16) * TB + c] * rk[g + 16];
+    u += I[(g + 32) * TB + c] * rk[g + 32] + I[(g + 48) * TB + c] * rk[g + 48];
+    part[g][c] = u;
+    __syncthreads();
+    if (t < TB) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q++) acc += part[q][t];
+      sx[k * TB + t] = acc;
+      x[k * TB + t] = acc;
     }
     __syncthreads();
   }
@@ -239,7 +302,7 @@ __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int
 
 }  // namespace
 
-constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
+constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB + 512) * sizeof(double);
 
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st) {
   static bool attr_set = false;
@@ -258,7 +321,7 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
     const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);
     hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, flag);
   }
-  hipLaunchKernelGGL(k_backward, dim3(1), dim3(256), (size_t)T * TB * sizeof(double), st,
+  hipLaunchKernelGGL(k_backward, dim3(1), dim3(kBwdNT), (size_t)T * TB * sizeof(double), st,
                      (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T);
   return hipGetLastError();
 }

@@ -118,6 +118,8 @@ SIGNATURES = {
     "mcs_ba_optimize_sharded": (ctypes.c_int, [_P] * 10),
     "mcs_global_ba": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_dense_ldlt_solve": (ctypes.c_int, [_I32, _P, _I32, _P, _P, _P]),
+    "mcs_ba_enable_timing": (ctypes.c_int, [_P, _I32]),
+    "mcs_ba_read_timing": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32]),
     "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
 }
 

@@ -519,3 +519,25 @@ def dense_ldlt_solve(S, b, device=0):
     zp = ctypes.c_int32()
     _check(lib().mcs_dense_ldlt_solve(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp)))
     return x, zp.value
+
+
+BA_STAGES = ("linearize", "schur", "exchange", "solve", "update")
+
+
+def _solver_enable_timing(self, on=True):
+    from . import _check
+    _check(self._lib.mcs_ba_enable_timing(self._h, 1 if on else 0))
+
+
+def _solver_read_timing(self, reset=True):
+    """-> (dict stage -> accumulated ms, iterations, trials, last reduced-system size n)."""
+    from . import _check
+    ms = np.zeros(len(BA_STAGES))
+    it, tr, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    _check(self._lib.mcs_ba_read_timing(self._h, _p(ms), ctypes.byref(it), ctypes.byref(tr),
+                                        ctypes.byref(n), 1 if reset else 0))
+    return dict(zip(BA_STAGES, ms.tolist())), it.value, tr.value, n.value
+
+
+Solver.enable_timing = _solver_enable_timing
+Solver.read_timing = _solver_read_timing
