@@ -64,6 +64,81 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
                                      int32_t th_low, double epi_thresh, int32_t* matches12,
                                      int32_t* n_matches);
 
+/* ---- Projection-guided (windowed) matching -------------------------------------------
+ * cMultiFrame feature grid (src/cMultiFrame.cpp:154-184, PosInGrid :342-353; 64 x 48 cells
+ * per camera, include/cMultiFrame.h FRAME_GRID_COLS / FRAME_GRID_ROWS) and
+ * GetFeaturesInArea (:272-340), feeding the best / second-best Hamming scans of
+ *   SearchByProjection(F, vpMapPoints, th)          src/cORBmatcher.cpp:67-166   (rule 0)
+ *   SearchByProjection(CurrentFrame, LastFrame, th) src/cORBmatcher.cpp:1991-2123 (rule 1)
+ *   SearchForInitialization(F1, F2, ...)            src/cORBmatcher.cpp:579-726  (rule 2)
+ *   WindowSearch(F1, F2, windowSize, ...)           src/cORBmatcher.cpp:326-473  (rule 3)
+ * with checkOrientation = false (include/cORBmatcher.h:40).
+ * Split: the grid is built on the host (it is part of the cMultiFrame constructor); the
+ * device enumerates every query's window candidates in the reference's order (cells ix-major,
+ * then iy, then insertion order) and computes their Hamming distances; the host applies the
+ * reference's sequential selection rule (it depends on earlier queries' assignments). */
+#define MCS_GRID_COLS 64
+#define MCS_GRID_ROWS 48
+
+/* grid_params[cam] = {min_x, min_y, grid_w_inv, grid_h_inv} (mnMinX, mnMinY,
+ * mfGridElementWidthInv, mfGridElementHeightInv).  kp_xy [n_kp][2] float (cv::KeyPoint.pt),
+ * kp_cam [n_kp].  Out: cell_ptr [n_cams*64*48 + 1] (cell = (cam*64 + ix)*48 + iy), cell_kp
+ * [n_kp] (keypoints outside the grid are dropped; *n_in_grid entries used).  Host memory. */
+int mcs_frame_grid_build(const float* kp_xy, const int32_t* kp_cam, int32_t n_kp, int32_t n_cams,
+                         const double* grid_params, int32_t* cell_ptr, int32_t* cell_kp,
+                         int32_t* n_in_grid);
+
+/* Device window search.  Queries: q_xyr [nq][3] doubles (x, y, r), q_cam_lvl [nq][3]
+ * (cam, minLevel, maxLevel; -1/-1 = any level), q_desc [nq][bytes] (+ q_mask nullable).
+ * Keypoints: kp_xy [n][2] float, kp_octave [n], kp_desc [n][bytes] (+ kp_mask nullable; with
+ * masks the distance is DescriptorDistance64Masked).  Grid: device copies of the
+ * mcs_frame_grid_build outputs and grid_params.  Out: cand_ptr [nq+1], cand_kp / cand_dist
+ * [cap]; *total = number of candidates (MCS_ERR_CAPACITY if > cap; nothing else written).
+ * Synchronises `stream` once to read the total. */
+int mcs_window_search_device(const int32_t* d_cell_ptr, const int32_t* d_cell_kp,
+                             const double* d_grid_params, int32_t n_cams, const float* d_kp_xy,
+                             const int32_t* d_kp_octave, const uint8_t* d_kp_desc,
+                             const uint8_t* d_kp_mask, int32_t bytes, int32_t nq,
+                             const double* d_q_xyr, const int32_t* d_q_cam_lvl,
+                             const uint8_t* d_q_desc, const uint8_t* d_q_mask,
+                             int32_t* d_cand_ptr, int32_t* d_cand_kp, int32_t* d_cand_dist,
+                             int64_t cap, int64_t* total, void* stream);
+
+/* Host selection over the candidate lists (queries in the reference's loop order).
+ * rule 0: SearchByProjection(F, MPs): skip assigned keypoints, best / second with octaves,
+ *         accept best <= th unless (same octave and best > nnratio * second), assign.
+ * rule 1: SearchByProjection(Current, Last): skip assigned keypoints, best only,
+ *         accept best <= th, assign.
+ * rule 2: SearchForInitialization: skip candidates whose vMatchedDistance <= dist, accept
+ *         best <= th and best < second * nnratio, a re-matched train keypoint drops its
+ *         previous query.
+ * rule 3: WindowSearch: skip keypoints matched earlier in the call, accept
+ *         best <= second * nnratio and best <= th, assign.
+ * th = TH_HIGH (rules 0, 1, 3) or TH_LOW (rule 2) of cORBmatcher (src/cORBmatcher.cpp:46-65).
+ * kp_assigned [n_kp] in/out (rules 0, 1, 3: keypoint already holds a map point).  match [nq]
+ * out (keypoint index or -1; rule 2: vnMatches12).  *n_matches = match count. */
+int mcs_window_select(int32_t rule, int32_t nq, const int32_t* cand_ptr, const int32_t* cand_kp,
+                      const int32_t* cand_dist, const int32_t* kp_octave, int32_t n_kp,
+                      int32_t th, double nnratio, uint8_t* kp_assigned, int32_t* match,
+                      int32_t* n_matches);
+
+/* Host-buffer entry point for the reference's call sites (cv::Mat / std::vector data): builds
+ * the grid, uploads the frame and the queries, runs mcs_window_search_device and
+ * mcs_window_select on `device` (no CPU fallback).  kp_assigned may be NULL (= none). */
+typedef struct mcs_window_frame {
+  int32_t n_cams, n_kp, bytes;
+  const double* grid_params;     /* [n_cams][4], as above */
+  const float* kp_xy;            /* [n_kp][2] mvKeys pt */
+  const int32_t* kp_cam;         /* [n_kp] keypoint_to_cam */
+  const int32_t* kp_octave;      /* [n_kp] */
+  const uint8_t* desc;           /* [n_kp][bytes] mDescriptors in camera order */
+  const uint8_t* desc_mask;      /* nullable [n_kp][bytes] mDescriptorMasks (mdBRIEF) */
+} mcs_window_frame;
+int mcs_window_match(int32_t device, int32_t rule, const mcs_window_frame* frame, int32_t nq,
+                     const double* q_xyr, const int32_t* q_cam_lvl, const uint8_t* q_desc,
+                     const uint8_t* q_mask, int32_t th, double nnratio, uint8_t* kp_assigned,
+                     int32_t* match, int32_t* n_matches);
+
 #ifdef __cplusplus
 }
 #endif
