@@ -82,12 +82,28 @@ int mcs_ba_optimize(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options
 
 /* cOptimizer::LocalBundleAdjustment after graph construction (src/cOptimizer.cpp:771-903):
  * round 1 optimize(10); if the stop flag is set afterwards -> return (no write-back);
- * else disable edges with chi2 > delta^2, round 2 optimize(15), cull again.
+ * else disable edges with chi2 > delta^2, round 2 optimize(15), cull again.  stop_flag NULL
+ * (pbStopFlag == NULL): the terminate action's auxiliary flag persists from round 1 into
+ * round 2, as in g2o.  An empty active graph (optimize() == -1) returns without write-back.
  * Outputs: poses/points (in/out; only meaningful when *write_back == 1), edge_inlier[n_edges]
  * (0 = observation erased), write_back (bDoMore of the reference), reports of both rounds. */
 int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* points,
                  uint8_t* edge_inlier, int32_t* write_back, volatile int32_t* stop_flag,
                  mcs_ba_report* rep_round1, mcs_ba_report* rep_round2);
+
+/* cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) after graph construction:
+ * p->n_poses == 1 (the frame's M_t, optimised; pose_fixed is ignored), every map point fixed
+ * (:382), Mc / IO fixed, Huber delta = p->huber_delta (1.345 * huberMultiplier, :344),
+ * edge_info = invSigma2(octave) (:405-406).  optimize(10), edges with chi2 > delta^2 become
+ * outliers and are disabled, optimize(10) again, the remaining edges are classified
+ * (:432-474).  No force-stop flag is set, so the terminate action's auxiliary flag carries
+ * over from round 1 to round 2 (a converged round 1 leaves round 2 without iterations).
+ * pose: in/out [6]; outlier: out [n_edges] (mvbOutlier of the observations);
+ * *n_good = nInitialCorrespondences - nBad (the reference's return value);
+ * *bad_ratio = nBad / nInitialCorrespondences (its `inliers` output, nullable). */
+int mcs_pose_optimization(mcs_ba_ctx* c, const mcs_ba_problem* p, double* pose, uint8_t* outlier,
+                          int32_t* n_good, double* bad_ratio, mcs_ba_report* rep_round1,
+                          mcs_ba_report* rep_round2);
 
 /* Per-edge error and Jacobians (vertex order Mt, point) at the given estimate, for tests:
  * err [n][2], jac_pose [n][2][6], jac_point [n][2][3] (g2o sign: d(meas - proj)/d(param)). */

@@ -1064,21 +1064,73 @@ int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* 
   const double huberK2 = p->huber_delta * p->huber_delta;
   std::vector<uint8_t> level(p->n_edges, 0);
   std::vector<double> chi(p->n_edges);
+  // pbStopFlag == NULL: the terminate action raises its own auxiliary flag and g2o keeps it
+  // installed as the force-stop flag, so a round 1 that converged leaves round 2 with zero
+  // iterations (sparse_optimizer_terminate_action.cpp:64-72, sparse_optimizer.cpp:376)
+  volatile int32_t aux = 0;
+  volatile int32_t* sf = stop_flag ? stop_flag : &aux;
+  mcs_ba_report t1{}, t2{};
+  if (!r1) r1 = &t1;
+  if (!r2) r2 = &t2;
   *write_back = 0;
   for (int e = 0; e < p->n_edges; e++) edge_inlier[e] = 1;
   if (stop_flag && *stop_flag) return MCS_OK;               // :771-773
   o.max_iterations = 10;
-  int rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), stop_flag, r1);
+  int rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r1);
   if (rc) return rc;
+  // optimize() returns -1 == OptimizationAlgorithm::Fail only for an empty active graph
+  if (r1->n_active_poses + r1->n_active_points == 0) return MCS_OK;   // :784-788
   if (stop_flag && *stop_flag) return MCS_OK;               // bDoMore = false (:790-794)
   for (int e = 0; e < p->n_edges; e++)                      // :798-817
     if (chi[e] > huberK2) { level[e] = 1; edge_inlier[e] = 0; }
   o.max_iterations = 15;                                    // :819-820
-  rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), stop_flag, r2);
+  rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r2);
   if (rc) return rc;
+  if (r2->n_active_poses + r2->n_active_points == 0) return MCS_OK;   // :822-826
   for (int e = 0; e < p->n_edges; e++)                      // :830-849
     if (edge_inlier[e] && chi[e] > huberK2) edge_inlier[e] = 0;
   *write_back = 1;
+  return MCS_OK;
+}
+
+int mcs_pose_optimization(mcs_ba_ctx* c, const mcs_ba_problem* p, double* pose, uint8_t* outlier,
+                          int32_t* n_good, double* bad_ratio, mcs_ba_report* r1, mcs_ba_report* r2) {
+  if (!c || !p || !pose || !n_good || (p->n_edges > 0 && !outlier)) return MCS_ERR_ARG;
+  if (p->n_poses != 1) {
+    set_error("PoseOptimization: the problem must hold exactly one pose vertex");
+    return MCS_ERR_ARG;
+  }
+  mcs_ba_problem q = *p;
+  const uint8_t not_fixed = 0;
+  q.pose_fixed = &not_fixed;                                // vSE3->setFixed(false) (:299)
+  mcs_ba_options o;
+  mcs_ba_default_options(&o);                               // gain 1e-6, max 15 (:290-291)
+  o.max_iterations = 10;                                    // optimize(10) (:434, :457)
+  const double th2 = p->huber_delta * p->huber_delta;      // thHuber = 1.345 * mult (:344)
+  const int N = p->n_edges;
+  std::vector<uint8_t> level(N, 0);
+  std::vector<double> chi(N), pts(p->points, p->points + 3 * (size_t)p->n_points);
+  // no setForceStopFlag: the terminate action's own flag is shared by both optimize() calls
+  volatile int32_t aux = 0;
+  mcs_ba_report t1{}, t2{};
+  int rc = optimize_impl(c, &q, &o, pose, pts.data(), level.data(), chi.data(), &aux,
+                         r1 ? r1 : &t1, nullptr, true);    // map points fixed (:382)
+  if (rc) return rc;
+  int nBad = 0;
+  for (int e = 0; e < N; e++) {                             // :439-454
+    if (chi[e] > th2) { outlier[e] = 1; level[e] = 1; nBad++; }
+    else outlier[e] = 0;
+  }
+  rc = optimize_impl(c, &q, &o, pose, pts.data(), level.data(), chi.data(), &aux,
+                     r2 ? r2 : &t2, nullptr, true);
+  if (rc) return rc;
+  for (int e = 0; e < N; e++) {                             // :460-474
+    if (level[e]) continue;
+    if (chi[e] > th2) { outlier[e] = 1; nBad++; }
+    else outlier[e] = 0;
+  }
+  *n_good = N - nBad;                                       // return value (:485)
+  if (bad_ratio) *bad_ratio = N > 0 ? (double)nBad / N : 0.0;   // `inliers` (:481-483)
   return MCS_OK;
 }
 

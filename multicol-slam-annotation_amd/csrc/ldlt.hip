@@ -43,87 +43,106 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-// LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, register resident:
-// lane = row i, wave g owns the columns m = g + 4q.  A runtime loop runs over groups of 4
-// columns (j = 4 jj + gj, gj unrolled): the trailing-matrix registers a[] are shifted by one
-// after every group, so the column the owning wave gj works on is always a[0] and the code
-// stays small (a fully unrolled sweep is ~55 KB and runs instruction-fetch bound).
-// e[q] holds row i of E = L^-1 (column g + 4q), built by applying every elimination row
-// operation to the identity.
-// Per column j, before the barrier: the owning wave forms l_i = A[i][j] / d_j, publishes l_i
-// and c_i = A[i][j] and writes L / D of column j into sA; lane j of every wave publishes its
-// (final) row j of E is read from lane j of the same wave.  After the barrier every wave
-// updates its registers:
-// A[i][m] -= l_i c_m (m > j), E[i][m] -= l_i E[j][m] (m <= j).  Updates are branch-free
-// (masked operands are 0 and l_i = 0 for rows i <= j, so the FMA leaves the value exact).
-// Exchange buffers are double-buffered by column parity: one barrier per column.
+// LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, blocked by 16-column panels.
+//   panel p (wave p, lane = row): columns 16p..16p+15 are eliminated in registers; the value of
+//     column j at another row comes from v_readlane (one wave: no barrier, no LDS).  The wave
+//     writes L (strict lower) and D (diagonal) of its columns into sA, and the unscaled columns
+//     C = L D of the rows below the panel, transposed, into the strict upper triangle (scratch:
+//     only the lower triangle and the diagonal of sA are results).
+//   trailing update: A[bi][bj] -= C_bi L_bj^T for the 16x16 blocks p < bj <= bi, on
+//     v_mfma_f64_16x16x4_f64, blocks spread over the 4 waves.
+//   L^-1: diagonal 16x16 blocks by forward substitution with lane = column (no cross-lane
+//     traffic; the L entries are LDS broadcasts), then block rows i = 1..3:
+//     X_ij = -X_ii (sum_{k=j}^{i-1} L_ik X_kj) on MFMA; the inner sum stays in accumulator
+//     layout, which is already the B-operand layout of the outer product.
+// The column-at-a-time version this replaces needed one barrier and a 64-row exchange per
+// column (~138k cycles per tile); here 8 barriers remain.
 // On return sA holds L (strict lower) and D (diagonal), sI holds L^-1 (0 above the diagonal).
-__device__ __forceinline__ void factor_tile(double* sA, double* sI, double* scol, int* fail) {
-  const int t = threadIdx.x, i = t & 63, g = t >> 6;
-  double a[16], e[16];
+__device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int r16 = l & 15, k4 = l >> 4;
+  for (int p = 0; p < 4; p++) {
+    const int P = 16 * p;
+    if (w == p) {
+      double a[16];
 #pragma unroll
-  for (int q = 0; q < 16; q++) {
-    a[q] = sA[i * LS + g + 4 * q];
-    e[q] = (i == g + 4 * q) ? 1.0 : 0.0;
-  }
-  // scol layout (doubles): colL [2][64] | colC [2][4][16]
-  double* colL = scol;
-  double* colC = scol + 128;
-  __syncthreads();   // sA is rewritten column by column below
-  for (int jj = 0; jj < TB / 4; jj++) {
+      for (int c = 0; c < 16; c++) a[c] = sA[l * LS + P + c];
 #pragma unroll
-    for (int gj = 0; gj < 4; gj++) {
-      const int j = 4 * jj + gj, bf = gj & 1;
-      // every wave forms the candidate (only the owner's is published): no branch around
-      // register updates
-      const double dj = readlane_d(a[0], j);
-      const double c = a[0];
-      const double l = c / dj;
-      if (g == gj) {
-        if (dj == 0.0 && i == 0) *fail = 1;
-        colL[bf * 64 + i] = l;
-        const int slot = (i >> 2) - jj;   // register slot of row i's column after the shifts
-        if (slot >= 0) colC[bf * 64 + (i & 3) * 16 + slot] = c;
-        sA[i * LS + j] = (i > j) ? l : c;
-      }
-      __syncthreads();
-      // unconditional loads, masks applied as multipliers (all operands finite), so the
-      // compiler emits no branches between the LDS reads
-      const double lv = colL[bf * 64 + i];
-      const double li = (i > j) ? lv : 0.0;   // select, not a multiply: rows <= j may hold inf
-      // c of column g + 4 (q + jj); slots past the tile hold stale values, which only reach
-      // registers that stand for columns past the tile (never read back)
-      const double2* cg = reinterpret_cast<const double2*>(colC + bf * 64 + g * 16);
-      double cv[16];
+      for (int j = 0; j < 16; j++) {
+        const int J = P + j;
+        const double cj = a[j];
+        const double dj = readlane_d(cj, J);
+        const double lj = cj / dj;
 #pragma unroll
-      for (int q2 = 0; q2 < 8; q2++) {
-        const double2 v = cg[q2];
-        cv[2 * q2] = v.x;
-        cv[2 * q2 + 1] = v.y;
-      }
-      // a[q] is column g + 4 (q + jj) > j  <=>  g + 4 q > gj: only q = 0 can be <= j
-      cv[0] = (g > gj) ? cv[0] : 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; q++) a[q] = __builtin_fma(-li, cv[q], a[q]);
-      // E row j of this wave's columns lives in lane j of the same wave: readlane, no LDS
-      // (a single-lane LDS publish of the row measured ~2000 cycles per column)
-      // E[j][m] == 0 for m > j: skip those readlanes (wave-uniform branch; each readlane
-      // pair costs ~25 cycles)
-#pragma unroll
-      for (int q = 0; q < 16; q++) {
-        if (g + 4 * q <= j) {
-          const double ej = readlane_d(e[q], j);
-          e[q] = __builtin_fma(-li, ej, e[q]);
-        }
+        for (int m = j + 1; m < 16; m++) a[m] = __builtin_fma(-lj, readlane_d(cj, P + m), a[m]);
+        if (dj == 0.0 && l == 0) *fail = 1;
+        if (l >= J) sA[l * LS + J] = (l > J) ? lj : cj;
+        if (l >= P + 16) sA[J * LS + l] = cj;
       }
     }
+    __syncthreads();
+    const int nb = 3 - p;
+    for (int b = w; b < nb * (nb + 1) / 2; b += 4) {
+      int q = 0, s = b;
+      while (s > q) { s -= q + 1; q++; }
+      const int bi = p + 1 + q, bj = p + 1 + s;
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int q = 0; q < 15; q++) a[q] = a[q + 1];
-    a[15] = 0.0;
+      for (int k0 = 0; k0 < 16; k0 += 4) {
+        const double av = sA[(P + k0 + k4) * LS + 16 * bi + r16];   // C[16 bi + m][P + k]
+        const double bv = sA[(16 * bj + r16) * LS + P + k0 + k4];   // L[16 bj + n][P + k]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) sA[(16 * bi + k4 + 4 * r) * LS + 16 * bj + r16] -= acc[r];
+    }
+    __syncthreads();
   }
+  // L^-1, diagonal blocks: wave w solves L_ww x = e_c for column c = lane & 15
+  {
+    const int B = 16 * w;
+    double x[16];
 #pragma unroll
-  for (int q = 0; q < 16; q++) sI[i * LS + g + 4 * q] = e[q];
+    for (int r = 0; r < 16; r++) {
+      double s = (r == r16) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < r; k++) s = __builtin_fma(-sA[(B + r) * LS + B + k], x[k], s);
+      x[r] = s;
+    }
+    if (l < 16) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) sI[(B + r) * LS + B + r16] = x[r];
+    }
+    for (int e = t; e < TB * TB; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      if ((cc >> 4) > (rr >> 4)) sI[rr * LS + cc] = 0.0;
+    }
+  }
   __syncthreads();
+  // off-diagonal blocks, one block row at a time (row i needs the rows above it)
+  for (int i = 1; i < 4; i++) {
+    if (w < i) {
+      const int j = w;
+      d4 s = {0.0, 0.0, 0.0, 0.0};
+      for (int k = j; k < i; k++) {
+#pragma unroll
+        for (int k0 = 0; k0 < 16; k0 += 4) {
+          const double av = sA[(16 * i + r16) * LS + 16 * k + k0 + k4];   // L_ik[m][kk]
+          const double bv = sI[(16 * k + k0 + k4) * LS + 16 * j + r16];   // X_kj[kk][n]
+          s = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, s, 0, 0, 0);
+        }
+      }
+      d4 xo = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const double av = sI[(16 * i + r16) * LS + 16 * i + 4 * r + k4];  // X_ii[m][4r + kk]
+        xo = __builtin_amdgcn_mfma_f64_16x16x4f64(av, s[r], xo, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) sI[(16 * i + k4 + 4 * r) * LS + 16 * j + r16] = -xo[r];
+    }
+    __syncthreads();
+  }
 }
 
 // acc = X Y^T (64x64x64), wave w owns output columns [16w, 16w+16), acc[q] rows [16q, 16q+16)
@@ -167,7 +186,6 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   double* sY = sX + TB * LS;     // A_jk -> W_j
   double* sv = sY + TB * LS;     // b_k
   double* su = sv + TB;          // u_k = Linv b_k
-  double* scol = su + TB;        // factor_tile column exchange (512 doubles)
   __shared__ int fail;
   const int t = threadIdx.x;
   const int wg = blockIdx.x;
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   }
   if (rhs && t < TB) sv[t] = b[k * TB + t];
   __syncthreads();
-  factor_tile(sK, sI, scol, &fail);
+  factor_tile(sK, sI, &fail);
   if (rhs) {
     const double u = gemv_row(sI, sv);
     if ((t & 3) == 0) su[t >> 2] = u;
@@ -302,7 +320,7 @@ __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int
 
 }  // namespace
 
-constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB + 512) * sizeof(double);
+constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
 
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st) {
   static bool attr_set = false;

@@ -206,6 +206,27 @@ def make_problem(n_local=10, n_fixed=3, n_points=3000, target_edges=20000, seed=
                 gt_poses=gt_poses, gt_points=gt_pts)
 
 
+def make_pose_problem(seed=0, n_points=1500, target_edges=5000, outlier_frac=0.05,
+                      noise_scale=0.5, pose_noise=(0.01, 0.05), huber_multiplier=2.0):
+    """PoseOptimization problem (src/cOptimizer.cpp:264-486): the current MultiFrame's pose
+    (perturbed) and its 2D-3D correspondences to fixed map points (true positions), with
+    information invSigma2(octave) and Huber delta 1.345 * huberMultiplier (:344)."""
+    pr = make_problem(n_local=2, n_fixed=0, n_points=n_points, target_edges=target_edges,
+                      seed=seed, outlier_frac=outlier_frac, noise_scale=noise_scale,
+                      pose_noise=pose_noise, point_noise=0.0)
+    sel = pr["edge_pose"] == 0
+    used = np.unique(pr["edge_point"][sel])
+    remap = -np.ones(len(pr["points"]), np.int64)
+    remap[used] = np.arange(len(used))
+    return dict(poses=pr["poses"][:1].copy(), pose_fixed=np.zeros(1, np.uint8),
+                points=pr["gt_points"][used].copy(), mc=pr["mc"], cam=pr["cam"],
+                edge_pose=np.zeros(int(sel.sum()), np.int32),
+                edge_point=remap[pr["edge_point"][sel]].astype(np.int32),
+                edge_cam=pr["edge_cam"][sel].copy(), edge_meas=pr["edge_meas"][sel].copy(),
+                edge_info=pr["edge_info"][sel].copy(), huber_delta=1.345 * huber_multiplier,
+                gt_pose=pr["gt_poses"][0].copy())
+
+
 # ---------------------------------------------------------------------------
 # GPU solver binding
 # ---------------------------------------------------------------------------
@@ -250,20 +271,42 @@ class Solver:
                     stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
 
     def local_ba(self, pr, stop_flag=0):
+        """mcs_local_ba; stop_flag None = pbStopFlag NULL (g2o's auxiliary terminate flag)."""
         from . import _check
         s = as_struct(pr)
         poses = pr["poses"].copy()
         points = pr["points"].copy()
         inl = np.zeros(len(pr["edge_pose"]), np.uint8)
         wb = ctypes.c_int32()
-        sf = ctypes.c_int32(int(stop_flag))
+        sf = None if stop_flag is None else ctypes.c_int32(int(stop_flag))
         r1 = BAReport()
         r2 = BAReport()
         _check(self._lib.mcs_local_ba(self._h, ctypes.byref(s), _p(poses), _p(points), _p(inl),
-                                      ctypes.byref(wb), ctypes.byref(sf), ctypes.byref(r1),
-                                      ctypes.byref(r2)))
+                                      ctypes.byref(wb), None if sf is None else ctypes.byref(sf),
+                                      ctypes.byref(r1), ctypes.byref(r2)))
         return dict(poses=poses, points=points, edge_inlier=inl, write_back=wb.value,
-                    stop_flag=sf.value, report1=r1, report2=r2)
+                    stop_flag=None if sf is None else sf.value, report1=r1, report2=r2)
+
+    def pose_optimization(self, pr, trace=0):
+        """cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) via mcs_pose_optimization;
+        pr holds one pose and fixed map points (make_pose_problem)."""
+        from . import _check
+        s = as_struct(pr)
+        pose = np.ascontiguousarray(pr["poses"][0], np.float64).copy()
+        n = len(pr["edge_pose"])
+        out = np.zeros(max(n, 1), np.uint8)
+        ngood = ctypes.c_int32()
+        bad = ctypes.c_double()
+        t1 = np.zeros(max(trace, 1))
+        t2 = np.zeros(max(trace, 1))
+        r1 = BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(t1) if trace else None, trace)
+        r2 = BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(t2) if trace else None, trace)
+        _check(self._lib.mcs_pose_optimization(self._h, ctypes.byref(s), _p(pose), _p(out),
+                                               ctypes.byref(ngood), ctypes.byref(bad),
+                                               ctypes.byref(r1), ctypes.byref(r2)))
+        return dict(pose=pose, outlier=out[:n].copy(), n_good=ngood.value, bad_ratio=bad.value,
+                    report1=r1, report2=r2, trace1=t1[:min(trace, r1.iterations)],
+                    trace2=t2[:min(trace, r2.iterations)])
 
     def linearize(self, pr):
         from . import _check

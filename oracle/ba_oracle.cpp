@@ -14,12 +14,13 @@
 //     (sparse_optimizer.cpp:166-267, 354-435), SparseOptimizerTerminateAction (:21-72)
 //   * the reduced camera system is solved by LDLT without pivoting: Eigen's SimplicialLDLT
 //     (linear_solver_eigen.h:94-126) also only fails on an exact zero pivot
-//   * cOptimizer::LocalBundleAdjustment rounds + culling (src/cOptimizer.cpp:771-903)
+//   * cOptimizer::LocalBundleAdjustment rounds + culling (src/cOptimizer.cpp:771-903),
+//     BundleAdjustment (:73-261) and PoseOptimization (:264-486)
 //
 // PARITY STATUS: unpinned against the reference binary.  The MultiCol edge needs OpenCV
 // (absent); the vendored g2o core needs the cmake-generated ThirdParty/g2o/config.h
 // (core/openmp_mutex.h:30 includes "../../config.h"), so it is unbuildable here without a
-// stand-in header.  The restatement is checked by the properties in tests/test_ba_oracle.py.
+// stand-in header.  The restatement is checked by the properties in tests/test_ba.py.
 // ============================================================================
 #include <algorithm>
 #include <cfloat>
@@ -652,19 +653,85 @@ int oracle_local_ba(const mcs_ba_problem* p, double* poses, double* points, uint
   const double huberK2 = p->huber_delta * p->huber_delta;
   std::vector<uint8_t> level(p->n_edges, 0);
   std::vector<double> chi(p->n_edges);
+  // pbStopFlag == NULL: g2o installs the terminate action's auxiliary flag as the force-stop
+  // flag the first time the action stops (sparse_optimizer_terminate_action.cpp:64-72) and
+  // nothing resets it, so it is shared by both rounds
+  int32_t aux = 0;
+  int32_t* sf = stop_flag ? stop_flag : &aux;
+  mcs_ba_report t1{}, t2{};
+  if (!r1) r1 = &t1;
+  if (!r2) r2 = &t2;
   *write_back = 0;
   for (int e = 0; e < p->n_edges; e++) edge_inlier[e] = 1;
   if (stop_flag && *stop_flag) return 0;
-  oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), stop_flag, r1);
+  oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), sf, r1);
+  // optimize() == -1 == OptimizationAlgorithm::Fail: empty active graph (:784-788)
+  if (r1->n_active_poses + r1->n_active_points == 0) return 0;
   if (stop_flag && *stop_flag) return 0;   // bDoMore = false: no culling, no write-back
   for (int e = 0; e < p->n_edges; e++)
     if (chi[e] > huberK2) { level[e] = 1; edge_inlier[e] = 0; }
   o.max_iterations = 15;
-  oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), stop_flag, r2);
+  oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), sf, r2);
+  if (r2->n_active_poses + r2->n_active_points == 0) return 0;   // :822-826
   for (int e = 0; e < p->n_edges; e++)
     if (edge_inlier[e] && chi[e] > huberK2) edge_inlier[e] = 0;
   *write_back = 1;
   return 0;
+}
+
+// cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) after graph construction: one pose
+// vertex (p->n_poses == 1, optimised), every map point fixed (:382), Huber delta =
+// p->huber_delta (1.345 * huberMultiplier, :344), information invSigma2(octave) (:405-406).
+// optimize(10); chi2 > delta^2 -> outlier, edge level 1; optimize(10); classify the remaining
+// edges (:432-474).  No force-stop flag is set, so the terminate action's auxiliary flag
+// carries over from round 1 to round 2.  Returns nInitialCorrespondences - nBad;
+// *bad_ratio = nBad / nInitialCorrespondences (the reference's `inliers` output).
+int oracle_pose_optimization(const mcs_ba_problem* p, double* pose, uint8_t* outlier,
+                             double* bad_ratio, mcs_ba_report* r1, mcs_ba_report* r2) {
+  mcs_ba_options o;
+  o.max_iterations = 10; o.gain_threshold = 1e-6; o.terminate_max_iter = 15; o.max_trials = 10;
+  o.tau = 1e-5;
+  const double th2 = p->huber_delta * p->huber_delta;
+  const int N = p->n_edges;
+  std::vector<uint8_t> level(N, 0);
+  const uint8_t not_fixed = 0;
+  mcs_ba_problem q = *p;
+  q.pose_fixed = &not_fixed;
+  int32_t aux = 0;
+  auto round = [&](mcs_ba_report* rep) {
+    Graph g;
+    g.P = &q;
+    g.poses.assign(pose, pose + 6);
+    g.points.assign(p->points, p->points + 3 * p->n_points);
+    g.level = level;
+    g.points_fixed = true;
+    g.hk.delta = p->huber_delta;
+    g.hk.dsqr = th2;
+    optimize(g, o, &aux, rep);
+    std::memcpy(pose, g.poses.data(), sizeof(double) * 6);
+    std::vector<double> chi(N);
+    double err[2];
+    for (int e = 0; e < N; e++) {
+      edge_error(pose, &g.points[3 * p->edge_point[e]], p->mc + 6 * p->edge_cam[e],
+                 p->cam + 17 * p->edge_cam[e], p->edge_meas + 2 * e, err);
+      chi[e] = p->edge_info[e] * (err[0] * err[0] + err[1] * err[1]);
+    }
+    return chi;
+  };
+  int nBad = 0;
+  std::vector<double> chi = round(r1);
+  for (int e = 0; e < N; e++) {
+    if (chi[e] > th2) { outlier[e] = 1; level[e] = 1; nBad++; }
+    else outlier[e] = 0;
+  }
+  chi = round(r2);
+  for (int e = 0; e < N; e++) {
+    if (level[e]) continue;
+    if (chi[e] > th2) { outlier[e] = 1; nBad++; }
+    else outlier[e] = 0;
+  }
+  if (bad_ratio) *bad_ratio = N > 0 ? (double)nBad / N : 0.0;
+  return N - nBad;
 }
 
 }  // extern "C"

@@ -246,6 +246,7 @@ def ba_optimize(pr, options=None, edge_level=None, stop_flag=None, trace=0):
 
 
 def local_ba(pr, stop_flag=0):
+    """stop_flag None = pbStopFlag NULL."""
     import ctypes as C
     from mcs_amd import ba
     L = _ba_sigs()
@@ -254,9 +255,32 @@ def local_ba(pr, stop_flag=0):
     points = pr["points"].copy()
     inl = np.zeros(len(pr["edge_pose"]), np.uint8)
     wb = C.c_int32()
-    sf = C.c_int32(int(stop_flag))
+    sf = None if stop_flag is None else C.c_int32(int(stop_flag))
     r1, r2 = ba.BAReport(), ba.BAReport()
-    L.oracle_local_ba(C.byref(s), _p(poses), _p(points), _p(inl), C.byref(wb), C.byref(sf),
-                      C.byref(r1), C.byref(r2))
+    L.oracle_local_ba(C.byref(s), _p(poses), _p(points), _p(inl), C.byref(wb),
+                      None if sf is None else C.byref(sf), C.byref(r1), C.byref(r2))
     return dict(poses=poses, points=points, edge_inlier=inl, write_back=wb.value,
-                stop_flag=sf.value, report1=r1, report2=r2)
+                stop_flag=None if sf is None else sf.value, report1=r1, report2=r2)
+
+
+def pose_optimization(pr, trace=0):
+    """oracle_pose_optimization (cOptimizer::PoseOptimization restatement)."""
+    import ctypes as C
+    from mcs_amd import ba
+    L = lib()
+    f = L.oracle_pose_optimization
+    f.restype = _I
+    f.argtypes = [_P] * 6
+    s = ba.as_struct(pr)
+    pose = np.ascontiguousarray(pr["poses"][0], np.float64).copy()
+    n = len(pr["edge_pose"])
+    out = np.zeros(max(n, 1), np.uint8)
+    bad = C.c_double()
+    t1 = np.zeros(max(trace, 1))
+    t2 = np.zeros(max(trace, 1))
+    r1 = ba.BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(t1) if trace else None, trace)
+    r2 = ba.BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(t2) if trace else None, trace)
+    ngood = f(C.byref(s), _p(pose), _p(out), C.byref(bad), C.byref(r1), C.byref(r2))
+    return dict(pose=pose, outlier=out[:n].copy(), n_good=ngood, bad_ratio=bad.value,
+                report1=r1, report2=r2, trace1=t1[:min(trace, r1.iterations)],
+                trace2=t2[:min(trace, r2.iterations)])
