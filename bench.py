@@ -13,6 +13,9 @@ SearchForTriangulationRaw, src/cORBmatcher.cpp:968-1156).
 Multi-GPU (torchrun, one process per GPU): every rank runs the same step on its own
 segment of multi-frames (independent units -> weak scaling, no data-path collective);
 the timed region is bracketed by barrier + synchronize and the max over ranks is taken.
+Side legs in the same JSON line: LocalBA (config C, replicas), GlobalBA (config E, points
+sharded, RCCL all-reduce per LM trial) and config D (8 cams 1024^2, camera per GPU, RCCL
+all-gather of the per-camera blocks).
 
 Prints ONE JSON line (rank 0).
 """
@@ -155,6 +158,91 @@ def run_global_ba(args, rank, world, local_rank, dev):
     return out, cpu
 
 
+def run_config_d(args, rank, world, local_rank, dev, stream):
+    """Config D: 8 synthetic fisheye cameras 1024^2, 4000 features/camera, camera c extracted
+    on rank c % N (cMultiFrame's per-camera OpenMP loop, src/cMultiFrame.cpp:128, becomes one
+    camera per GPU); per step every rank extracts its cameras for `d_multiframes` multi-frames
+    and one all-gather per per-camera buffer (RCCL over xGMI) hands every rank the whole
+    MultiFrame (the host concatenation :166-184).  Strong scaling: the same 8 x MD
+    camera-frames on every N."""
+    if args.d_multiframes <= 0:
+        return None
+    import torch
+    import torch.distributed as dist
+    import mcs_amd
+    from mcs_amd import synth, rig
+    NC, W, H, MD = 8, 1024, 1024, args.d_multiframes
+    S = rig.slots_per_rank(NC, world)
+    owned = rig.owned_cameras(NC, world, rank)
+    slot_cam = [owned[min(s, len(owned) - 1)] if owned else 0 for s in range(S)]
+    U = max(1, min(args.d_unique, MD))
+    imgs = np.zeros((S, U, H, W), np.uint8)
+    masks = np.zeros((S, H, W), np.uint8)
+    for s, c in enumerate(slot_cam):
+        for t in range(U):
+            img, m = synth.fisheye_frame(W, H, seed=500 + c, cam_index=c, yaw=0.015 * t,
+                                         noise_seed=900000 + 16 * t + c)
+            imgs[s, t] = img
+            masks[s] = m
+    # slot-major frame order f = s * MD + t, so each slot's block is contiguous for the gather
+    frames = imgs[:, np.arange(MD) % U].reshape(S * MD, H, W)
+    F = S * MD
+    params = mcs_amd.ExtractorParams(nfeatures=4000, fast_threshold=20)
+    ex = mcs_amd.Extractor(params, W, H, max_frames=F, device=local_rank)
+    cap = ex.capacity
+    d_img = torch.from_numpy(frames).to(dev)
+    d_mask = torch.from_numpy(masks).to(dev)
+    ex.set_masks_device(d_mask.data_ptr(), S, stream.cuda_stream)
+    d_midx = torch.from_numpy(np.repeat(np.arange(S, dtype=np.int32), MD)).to(dev)
+    d_kps = torch.zeros((F, cap * 7), dtype=torch.int32, device=dev)
+    d_cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gathered = {}
+
+    def step(timed):
+        ex.extract_batch_device(d_img.data_ptr(), F, d_midx.data_ptr(), d_kps.data_ptr(),
+                                d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
+        if timed:
+            ev0.record(stream)
+        gathered["cnt"] = rig.gather_camera_blocks(d_cnt.view(S, MD), NC)
+        gathered["kps"] = rig.gather_camera_blocks(d_kps.view(S, MD * cap * 7), NC)
+        gathered["desc"] = rig.gather_camera_blocks(d_desc.view(S, MD * cap * 32), NC)
+        if timed:
+            ev1.record(stream)
+
+    for _ in range(max(1, args.warmup)):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    cnt = gathered["cnt"]                       # [8, MD] in camera order, on every rank
+    kp_per_step = int(cnt.sum().item())
+    # the gathered MultiFrame must hold every camera's own extraction (rank-local check)
+    mine = d_cnt.view(S, MD)
+    for s, c in enumerate(owned):
+        if not torch.equal(cnt[c], mine[s]):
+            raise RuntimeError("config D all-gather mismatch for camera %d" % c)
+    gb = (d_kps.numel() * 4 + d_desc.numel() + d_cnt.numel() * 4) * world / 1e9
+    return {"kfeatures_per_s": round(kp_per_step * args.steps / dt / 1e3, 2),
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "allgather_ms_last_step": round(ev0.elapsed_time(ev1), 4),
+            "allgather_gb_per_step": round(gb, 4),
+            "keypoints_per_step": kp_per_step,
+            "scaling": "strong", "parallelism": "camera-per-GPU (%d camera slot(s) per rank)" % S,
+            "problem": "config D: 8 cams 1024x1024, 4000 feat/cam, %d multi-frames per step" % MD}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +259,9 @@ def main():
     ap.add_argument("--gba-kf", type=int, default=200)
     ap.add_argument("--gba-points", type=int, default=50000)
     ap.add_argument("--gba-edges", type=int, default=400000)
+    ap.add_argument("--d-multiframes", type=int, default=16,
+                    help="config D multi-frames per step (8 cams 1024^2, camera per GPU); 0 = off")
+    ap.add_argument("--d-unique", type=int, default=2, help="distinct rendered config D multi-frames")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -313,6 +404,7 @@ def main():
                       "sample": "1 LocalBA call (config C), oracle restatement, single thread"}
 
     gba, cpu_gba = run_global_ba(args, rank, world, local_rank, dev)
+    cfg_d = run_config_d(args, rank, world, local_rank, dev, stream)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -347,6 +439,7 @@ def main():
             "cpu_baseline_localba": cpu_ba,
             "globalba": gba,
             "cpu_baseline_globalba": cpu_gba,
+            "config_d": cfg_d,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),
         }
