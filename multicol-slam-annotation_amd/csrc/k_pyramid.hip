@@ -19,19 +19,26 @@ __device__ __forceinline__ int refl101(int p, int n) {
   return p >= n ? 2 * n - 2 - p : p;
 }
 
+// Vertical pass of cv::resize INTER_LINEAR.  Operand ranges: s = p0*a0 + p1*a1
+// with p <= 255 and a0 + a1 = 2048 (each in [0, 2048]) so 0 <= s <= 522240 < 2^23, and
+// b0, b1 in [0, 2048]: every product fits v_mul_i32_i24 exactly (< 2^31).
+//   SSE2 form (VResizeLinearVec_32s8u): x0 = s0 >> 4 <= 32640, (x0*b0 >> 16) + (y0*b1 >> 16)
+//   <= 1020, so the int16 saturations of the reference are no-ops and only the final u8
+//   clamp remains; the caller passes x0 = s0 >> 4, y0 = s1 >> 4 (computed once per row).
+//   scalar tail (FixedPtCast<int,uchar,22>): (s0*b0 + s1*b1 + 2^21) >> 22.
+// The bit-field extracts below are exact for these ranges; they only tell the compiler the
+// operand widths so that it emits v_mul_u32_u24 instead of the quarter-rate v_mul_lo_u32.
+__device__ __forceinline__ uint32_t sse_x(int s) { return __builtin_amdgcn_ubfe((uint32_t)s, 4, 15); }
+__device__ __forceinline__ int vres_sse(uint32_t x0, uint32_t y0, int b0, int b1) {
+  const uint32_t t = ((x0 * ((uint32_t)b0 & 0xFFFu)) >> 16) + ((y0 * ((uint32_t)b1 & 0xFFFu)) >> 16);
+  return (int)min(255u, (t + 2u) >> 2);
+}
+__device__ __forceinline__ int vres_fixed(int s0, int s1, int b0, int b1) {
+  const uint32_t u0 = __builtin_amdgcn_ubfe((uint32_t)s0, 0, 20), u1 = __builtin_amdgcn_ubfe((uint32_t)s1, 0, 20);
+  return (int)min(255u, (u0 * ((uint32_t)b0 & 0xFFFu) + u1 * ((uint32_t)b1 & 0xFFFu) + (1u << 21)) >> 22);
+}
 __device__ __forceinline__ int vres(int s0, int s1, int b0, int b1, bool simd) {
-  int v;
-  if (simd) {  // OpenCV 3.1 SSE2 VResizeLinearVec_32s8u
-    const int x0 = max(-32768, min(32767, s0 >> 4));
-    const int y0 = max(-32768, min(32767, s1 >> 4));
-    int t = ((x0 * b0) >> 16) + ((y0 * b1) >> 16);
-    t = max(-32768, min(32767, t));
-    t = max(-32768, min(32767, t + 2));
-    v = t >> 2;
-  } else {
-    v = (s0 * b0 + s1 * b1 + (1 << 21)) >> 22;  // FixedPtCast<int,uchar,22>
-  }
-  return max(0, min(255, v));
+  return simd ? vres_sse(sse_x(s0), sse_x(s1), b0, b1) : vres_fixed(s0, s1, b0, b1);
 }
 
 // (2s + 25) / 50 for 2s + 25 <= 12775 (s = 5x5 sum of u8) by multiply-shift;
@@ -181,7 +188,10 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
   auto push_row = [&](int r, uint32_t v) {
     if (RESIZE && core_lane && r >= seg0 && r < seg1)
       *reinterpret_cast<uint32_t*>(dstf + (int64_t)r * a.dpitch + xb) = v;
-    const uint32_t L = __shfl_up(v, 1), R = __shfl_down(v, 1);
+    // lane neighbours by DPP wave shifts (VALU, no LDS round trip); lane 0 / 63 get 0, and
+    // those lanes are halo lanes whose blurred output is never stored
+    const uint32_t L = __builtin_amdgcn_update_dpp(0u, v, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
+    const uint32_t R = __builtin_amdgcn_update_dpp(0u, v, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
     const uint32_t sc = __builtin_amdgcn_sad_u8(v, 0u, 0u);
     const uint32_t l2 = (L >> 16) & 0xFF, l3 = L >> 24, c0 = v & 0xFF, c3 = v >> 24;
     const uint32_t r0 = R & 0xFF, r1 = (R >> 8) & 0xFF;
@@ -225,6 +235,10 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
                     : (uint32_t)__builtin_amdgcn_readlane((int)betB, i - 64);
     };
     const int sr0 = (int)(row_tab(r_begin) & 0xFFFF), sr1 = (int)(row_tab(r_end - 1) >> 16);
+    // wave-uniform: every pixel of the strip (mirrors included) is in the SSE2 range (all
+    // strips but the one holding the scalar tail), so the per-pixel select disappears
+    const bool lane_sse = simd[0] && simd[1] && simd[2] && simd[3];
+    const bool wave_sse = __ballot(!lane_sse) == 0;
     int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
     int r = r_begin;
     uint32_t t = row_tab(r);
@@ -237,8 +251,14 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
         const uint32_t bb = row_beta(r);
         const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
         int o[4];
+        if (wave_sse) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, simd[k]);
+          for (int k = 0; k < 4; k++)
+            o[k] = vres_sse(sse_x(same ? hcur[k] : hprev[k]), sse_x(hcur[k]), b0, b1);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, simd[k]);
+        }
         push_row(r, pack4(o));
         r++;
         if (r < r_end) t = row_tab(r);
