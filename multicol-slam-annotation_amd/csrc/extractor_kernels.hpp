@@ -79,10 +79,10 @@ struct FastArgs {
 // LDS layout of k_fast_cells for windows up to max_ww x max_wh
 inline void fast_lds_layout(int max_ww, int max_wh, FastArgs& a) {
   auto al16 = [](int v) { return (v + 15) & ~15; };
-  a.tile_pitch = (max_ww + 6 + 3 + 3) & ~3;
+  a.tile_pitch = 4 * ((max_ww + 3) / 4) + 8;   // window - 4 .. quads + 7 (k_fast_cells staging)
   a.smap_off = al16(a.tile_pitch * (max_wh + 6));
-  a.surv_off = a.smap_off + al16(max_ww * max_wh);
-  a.wave_lds = a.surv_off + 3 * 256 * 2;
+  a.surv_off = a.smap_off + al16((max_ww + 2) * (max_wh + 2));
+  a.wave_lds = a.surv_off + al16(2 * max_ww * max_wh);
 }
 void launch_fast_cells(const FastArgs& a, hipStream_t st);
 
