@@ -3,6 +3,7 @@
 // (ping-pong), candidates + their current node in global memory (L2-resident).
 #include "common.hpp"
 #include "extractor_kernels.hpp"
+#include <algorithm>
 
 namespace mcs {
 
@@ -28,13 +29,16 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   if (!xcd_frame_map(blockIdx.x, a.nframes, a.nlevels, &f, &l)) return;
   const int tid = threadIdx.x;
   const LevelPlan& L = a.lv[l];
-  __shared__ int s_pref[kMaxCellsPerLevel];  // cell prefix; reused as sort keys
+  // LDS is what limits residency (workgroups per CU) of this latency-bound kernel, so the
+  // tables are sized to their value ranges: positions < MAXL fit int16, flags are 0/1/2;
+  // counts stay int (a node may hold tens of thousands of candidates on noise images).
+  __shared__ __attribute__((aligned(8))) int s_pref[2 * MAXL];  // cell prefix (<= 2*MAXL cells, launch_octree); then u64 sort keys
   __shared__ int s_scan[kOctThreads / 64 + 1];
   __shared__ int16_t nx0[2][MAXL], ny0[2][MAXL], nx1[2][MAXL], ny1[2][MAXL];
   __shared__ int ncnt[2][MAXL], nseq[2][MAXL];
-  __shared__ int ccnt[MAXL * 4];  // child counts; reused for best keys
-  __shared__ int npos[MAXL * 4];  // new position per (node, child); kept uses slot 0
-  __shared__ int nflag[MAXL];     // expanding / in-E / processed flags
+  __shared__ int ccnt[MAXL * 4];      // child counts; reused for best keys
+  __shared__ int16_t npos[MAXL * 4];  // new position per (node, child); kept uses slot 0
+  __shared__ uint8_t nflag[MAXL];     // expanding / in-E / processed flags
   __shared__ int s_var[8];
 
   uint32_t* cand = a.cand + (int64_t)f * a.cand_fstride + L.cand_off;
@@ -91,7 +95,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       if (ncnt[0][i] > 0) {
         nx0[1][m] = nx0[0][i]; ny0[1][m] = ny0[0][i]; nx1[1][m] = nx1[0][i]; ny1[1][m] = ny1[0][i];
         ncnt[1][m] = ncnt[0][i]; nseq[1][m] = nseq[0][i];
-        npos[i] = m++;
+        npos[i] = (int16_t)m++;
       }
     }
     s_var[0] = m;
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
             const int cq = ccnt[4 * i + q];
             if (cq == 0) continue;
             const int pos = P - 1 - s;
-            npos[4 * i + q] = pos;
+            npos[4 * i + q] = (int16_t)pos;
             nx0[nxt][pos] = (int16_t)((q & 1) ? mx : x0);
             nx1[nxt][pos] = (int16_t)((q & 1) ? x1 : mx);
             ny0[nxt][pos] = (int16_t)((q & 2) ? my : y0);
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
           }
         } else {
           const int pos = P + kp;
-          npos[4 * i] = pos;
+          npos[4 * i] = (int16_t)pos;
           nx0[nxt][pos] = nx0[cur][i]; nx1[nxt][pos] = nx1[cur][i];
           ny0[nxt][pos] = ny0[cur][i]; ny1[nxt][pos] = ny1[cur][i];
           ncnt[nxt][pos] = ncnt[cur][i];
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
     while (true) {
       const int prevSize = Lsz;
       const int nxt = cur ^ 1;
-      unsigned long long* keys = reinterpret_cast<unsigned long long*>(s_pref);  // 2048 x u64
+      unsigned long long* keys = reinterpret_cast<unsigned long long*>(s_pref);  // MAXL x u64
       // E = nodes created in the previous round with > 1 key
       int inE = 0;
       const int i0 = tid * kOctPer;
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
             const int cq = ccnt[4 * nd + q];
             if (cq == 0) continue;
             const int pos = Pn - 1 - s;
-            npos[4 * nd + q] = pos;
+            npos[4 * nd + q] = (int16_t)pos;
             nx0[nxt][pos] = (int16_t)((q & 1) ? mx : x0);
             nx1[nxt][pos] = (int16_t)((q & 1) ? x1 : mx);
             ny0[nxt][pos] = (int16_t)((q & 2) ? my : y0);
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
         const int i = i0 + j;
         if (i < Lsz && nflag[i] != 2) {
           const int pos = Pn + kb++;
-          npos[4 * i] = pos;
+          npos[4 * i] = (int16_t)pos;
           nx0[nxt][pos] = nx0[cur][i]; nx1[nxt][pos] = nx1[cur][i];
           ny0[nxt][pos] = ny0[cur][i]; ny1[nxt][pos] = ny1[cur][i];
           ncnt[nxt][pos] = ncnt[cur][i];
@@ -375,7 +379,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
 
 void launch_octree(const OctArgs& a, int max_list, hipStream_t st) {
   const unsigned g = xcd_grid(a.nframes, a.nlevels);
-  if (max_list <= 512)
+  int max_cells = 0;
+  for (int l = 0; l < a.nlevels; l++) max_cells = std::max(max_cells, a.lv[l].cell_end - a.lv[l].cell_begin);
+  // s_pref holds 2*MAXL cell prefixes (the plan rejects > kMaxCellsPerLevel = 2048)
+  if (max_list <= 512 && max_cells <= 1024)
     hipLaunchKernelGGL(k_octree<512>, dim3(g), dim3(kOctThreads), 0, st, a);
   else
     hipLaunchKernelGGL(k_octree<1024>, dim3(g), dim3(kOctThreads), 0, st, a);
