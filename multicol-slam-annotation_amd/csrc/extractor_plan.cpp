@@ -169,7 +169,9 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
       return MCS_ERR_UNSUPPORTED;
     }
     L.hx = (double)L.width_rel / L.nini;
-    const int cap = std::max(L.nfeat + 3, 4 * L.nini);
+    // even, so every level starts at an even selection index (k_orient_desc pairs keypoints
+    // 2j, 2j+1 in one wave and needs them on one level)
+    const int cap = (std::max(L.nfeat + 3, 4 * L.nini) + 1) & ~1;
     if (cap > kOctMaxL) {
       set_error("per-level feature budget exceeds the octree kernel's node bound (1024)");
       return MCS_ERR_UNSUPPORTED;

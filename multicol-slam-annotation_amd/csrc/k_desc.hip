@@ -103,48 +103,59 @@ __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
 // 4 aligned chunks of 16 bytes cover the 43 bytes of a row.
 constexpr int kBlrRow = 64;
 
-// IC moments of the raw patch staged in LDS (see c_icw)
-__device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int lane) {
+// IC moments of the raw patch staged in LDS (see c_icw); one half-wave (32 lanes) per
+// keypoint, sums reduced within the half (xor offsets < 32 never cross halves)
+__device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
   uint32_t a10 = 0, aS = 0, a01 = 0;
-  int r = lane / kRawW, c = lane - kRawW * (lane / kRawW);
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const int q = lane + 64 * k;
+  for (int k = 0; k < 10; k++) {
+    const int q = hl + 32 * k;
     if (q < kRawH * kRawW) {
       const uint32_t px = rawp[q];
       const uint32_t d1 = __builtin_amdgcn_udot4(c_icw[0][q], px, 0u, false);
       const uint32_t d0 = __builtin_amdgcn_udot4(c_icw[1][q], px, 0u, false);
       a10 += d1;
       aS += d0;
-      a01 += (uint32_t)r * d0;
+      a01 += (uint32_t)(q / kRawW) * d0;
     }
-    r += 7; c += 1;                       // q += 64 = 7 rows + 1 dword
-    if (c >= kRawW) { c -= kRawW; r++; }
   }
-  const int S = dev::wave_sum((int)aS);
-  const int m10 = dev::wave_sum((int)a10) - kHalfPatch * S;
-  const int m01 = dev::wave_sum((int)a01) - kHalfPatch * S;
+  int S = (int)aS, m10 = (int)a10, m01 = (int)a01;
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    S += __shfl_xor(S, o, 64);
+    m10 += __shfl_xor(m10, o, 64);
+    m01 += __shfl_xor(m01, o, 64);
+  }
+  m10 -= kHalfPatch * S;
+  m01 -= kHalfPatch * S;
   return fast_atan2_dev((float)m01, (float)m10);
 }
 
+// Two keypoints per wave, one per 32-lane half: the per-keypoint scalar work (level lookup,
+// fastAtan2, double sincos, keypoint record) runs once for both, the 8-32 test words of a
+// descriptor come from one 64-bit ballot per 32 tests (low half / high half).
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
-  __shared__ uint32_t s_raw[4][kRawH * kRawW];
-  __shared__ __attribute__((aligned(16))) uint8_t s_blr[4][kBlrH * kBlrRow];
+  __shared__ uint32_t s_raw[8][kRawH * kRawW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blr[8][kBlrH * kBlrRow];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
   int f, item;
-  const int chunks = (a.sel_per_frame + 3) / 4;
-  if (!xcd_frame_map(blockIdx.x, a.nframes, chunks, &f, &item)) return;
-  const int j = item * 4 + wv;
-  if (j >= a.sel_per_frame) return;
+  const int pairs = (a.sel_per_frame + 1) / 2;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, (pairs + 3) / 4, &f, &item)) return;
+  // even j0: both keypoints on one level (every level's sel_off is even, build_plan)
+  const int j0 = 2 * (item * 4 + wv);
+  if (j0 >= a.sel_per_frame) return;
   int l = 0;
-  while (l + 1 < a.nlevels && j >= a.lv[l + 1].sel_off) l++;
+  while (l + 1 < a.nlevels && j0 >= a.lv[l + 1].sel_off) l++;
   const LevelPlan& L = a.lv[l];
-  const int i = j - L.sel_off;
   const int32_t* scount = a.sel_count + (int64_t)f * a.nlevels;
-  if (i >= scount[l]) return;
-  int outIdx = i;
+  const int cnt = scount[l];
+  const int i0 = j0 - L.sel_off;
+  if (i0 >= cnt) return;                      // both halves past the level's selection
+  const bool valid = i0 + half < cnt;          // else: recompute keypoint i0, write nothing
+  int outIdx = i0 + (valid ? half : 0);
   for (int t = 0; t < l; t++) outIdx += scount[t];
-  const uint32_t pk = a.sel[(int64_t)f * a.sel_fstride + j];
+  const uint32_t pk = a.sel[(int64_t)f * a.sel_fstride + j0 + (valid ? half : 0)];
   const int cx = (int)(pk & 0xFFF) + kMinBorder, cy = (int)((pk >> 12) & 0xFFF) + kMinBorder;
   const int score = (int)(pk >> 24);
   const int pitch = L.pitch, bp = L.bpitch;
@@ -155,55 +166,56 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   const int mis = (cx - 21) & 15;
   {
     const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
-    int r = lane / kRawW, c = lane - kRawW * (lane / kRawW);
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const int q = lane + 64 * k;
-      if (q < kRawH * kRawW) s_raw[wv][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
-      r += 7; c += 1;
-      if (c >= kRawW) { c -= kRawW; r++; }
+    for (int k = 0; k < 10; k++) {
+      const int q = hl + 32 * k;
+      if (q < kRawH * kRawW) {
+        const int r = q / kRawW, c = q - kRawW * r;
+        s_raw[slot][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+      }
     }
     const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21 - mis);
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int q = lane + 64 * k;        // chunk q: row q >> 2, 16-byte chunk q & 3
+    for (int k = 0; k < 6; k++) {
+      const int q = hl + 32 * k;        // chunk q: row q >> 2, 16-byte chunk q & 3
       if (q < kBlrH * 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(b0 + (int64_t)(q >> 2) * bp + 16 * (q & 3));
-        *reinterpret_cast<uint4*>(&s_blr[wv][(q >> 2) * kBlrRow + 16 * (q & 3)]) = v;
+        *reinterpret_cast<uint4*>(&s_blr[slot][(q >> 2) * kBlrRow + 16 * (q & 3)]) = v;
       }
     }
   }
   dev::wave_sync();
   // ---- IC_Angle: integer moments over the circular r=16 patch
-  const float angle = ic_angle_lds(s_raw[wv], lane);
+  const float angle = ic_angle_lds(s_raw[slot], hl);
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
   double ca, sa;
   sincos(theta, &sa, &ca);
-  const int nwords = a.desc_size / 8;
-  uint8_t* dptr = a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size;
-  const uint8_t* bc = &s_blr[wv][21 * kBlrRow + 21 + mis];
-  uint64_t words[8];
+  const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
+  const uint8_t* bc = &s_blr[slot][21 * kBlrRow + 21 + mis];
+  uint32_t words[16];
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
-    if (r < nwords) {
-      const int t = r * 64 + lane;  // test t: byte t/8, bit t%8
+  for (int r = 0; r < 16; r++) {
+    words[r] = 0u;
+    if (r < nw) {
+      const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
       const double px0 = c_pattern_d[4 * t], py0 = c_pattern_d[4 * t + 1];
       const double px1 = c_pattern_d[4 * t + 2], py1 = c_pattern_d[4 * t + 3];
       const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
       const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
-      words[r] = __ballot(bc[o0] < bc[o1]);
+      const uint64_t b = __ballot(bc[o0] < bc[o1]);
+      words[r] = half ? (uint32_t)(b >> 32) : (uint32_t)b;
     }
   }
-  if (lane < nwords) {
-    uint64_t w = words[0];
+  if (valid && hl < nw) {
+    uint32_t w = words[0];
 #pragma unroll
-    for (int r = 1; r < 8; r++)
-      if (lane == r) w = words[r];
-    reinterpret_cast<uint64_t*>(dptr)[lane] = w;
+    for (int r = 1; r < 16; r++)
+      if (hl == r) w = words[r];
+    reinterpret_cast<uint32_t*>(a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size)[hl] = w;
   }
-  if (lane == 0) {
+  if (valid && hl == 0) {
     mcs_keypoint kp;
     kp.x = (float)cx; kp.y = (float)cy;
     if (l != 0) { kp.x = __fmul_rn((float)cx, L.scale); kp.y = __fmul_rn((float)cy, L.scale); }
@@ -316,7 +328,7 @@ __global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
     }
   }
   dev::wave_sync();
-  const float angle = ic_angle_lds(reinterpret_cast<const uint32_t*>(xs), lane);
+  const float angle = ic_angle_lds(reinterpret_cast<const uint32_t*>(xs), lane & 31);
   dev::wave_sync();
   // ---- undistorted keypoint (zero unless do_dBrief, :1304-1316)
   const mcs_cam_model& m = a.cams[a.cam_index ? a.cam_index[f] : 0];
@@ -414,7 +426,7 @@ __global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
 
 void launch_orient_desc(const DescArgs& a, hipStream_t st) {
   if (a.mode == 0) {
-    const unsigned g = xcd_grid(a.nframes, (a.sel_per_frame + 3) / 4);
+    const unsigned g = xcd_grid(a.nframes, ((a.sel_per_frame + 1) / 2 + 3) / 4);
     hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(256), 0, st, a);
     return;
   }
