@@ -243,6 +243,53 @@ def run_config_d(args, rank, world, local_rank, dev, stream):
             "problem": "config D: 8 cams 1024x1024, 4000 feat/cam, %d multi-frames per step" % MD}
 
 
+def run_bow(args, rank, world, dev, stream, d_desc, n_valid):
+    """DBoW2 transform: every descriptor slot of one step's extraction
+    output through the reference's own vocabulary (small_orb_omni_voc_9_6, k=9, L=6),
+    levelsup = 4 as cMultiFrame::ComputeBoW.  Reported beside the headline, not in `value`."""
+    if args.bow_reps <= 0:
+        return None, None
+    import torch
+    from mcs_amd import vocab
+    v = vocab.load_npz(os.path.join(ROOT, "tests", "golden", "small_orb_omni_voc_9_6.npz"))
+    V = vocab.Vocabulary(v, device=dev.index)
+    flat = d_desc.view(-1, 32)
+    n = flat.shape[0]
+    word = torch.empty(n, dtype=torch.int32, device=dev)
+    weight = torch.empty(n, dtype=torch.float64, device=dev)
+    node = torch.empty(n, dtype=torch.int32, device=dev)
+    ptrs = (flat.data_ptr(), n, 4, word.data_ptr(), weight.data_ptr(), node.data_ptr(),
+            stream.cuda_stream)
+    V.transform_words_device(*ptrs)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.bow_reps):
+        V.transform_words_device(*ptrs)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.bow_reps
+    V.close()
+    bpd = 48   # 32 B descriptor in, word (4) + weight (8) + node (4) out
+    gbs = n * bpd / (ms / 1e3) / 1e9
+    out = {"descriptors_per_s": round(n / (ms / 1e3), 1), "ms_per_call": round(ms, 4),
+           "descriptor_slots": n, "valid_descriptors": n_valid,
+           "vocabulary": "small_orb_omni_voc_9_6 (k=9, L=6, 8822 nodes, 6999 words), levelsup=4",
+           "roofline": {"kernel": "k_descend", "bound": "hbm", "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_descriptor": bpd}}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from tests import oracle_bind as ob
+        sample = flat[: min(n, 200000)].cpu().numpy()
+        t0 = time.perf_counter()
+        ob.vocab_words(v, sample, 4)
+        tc = time.perf_counter() - t0
+        cpu = {"value": round(len(sample) / tc, 1), "unit": "descriptors/s", "cores": 1,
+               "kind": "port", "sample": "%d descriptor slots of the step, oracle restatement "
+                                         "(vocabulary build included)" % len(sample)}
+    return out, cpu
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,6 +308,7 @@ def main():
     ap.add_argument("--gba-edges", type=int, default=400000)
     ap.add_argument("--d-multiframes", type=int, default=16,
                     help="config D multi-frames per step (8 cams 1024^2, camera per GPU); 0 = off")
+    ap.add_argument("--bow-reps", type=int, default=10, help="timed DBoW2 transform launches; 0 = off")
     ap.add_argument("--d-unique", type=int, default=2, help="distinct rendered config D multi-frames")
     args = ap.parse_args()
 
@@ -403,6 +451,7 @@ def main():
                       "unit": "LocalBA iters/s", "cores": 1, "kind": "port",
                       "sample": "1 LocalBA call (config C), oracle restatement, single thread"}
 
+    bow, cpu_bow = run_bow(args, rank, world, dev, stream, d_desc, kp_per_step)
     gba, cpu_gba = run_global_ba(args, rank, world, local_rank, dev)
     cfg_d = run_config_d(args, rank, world, local_rank, dev, stream)
 
@@ -440,6 +489,8 @@ def main():
             "globalba": gba,
             "cpu_baseline_globalba": cpu_gba,
             "config_d": cfg_d,
+            "bow": bow,
+            "cpu_baseline_bow": cpu_bow,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),
         }

@@ -126,6 +126,12 @@ SIGNATURES = {
     "mcs_window_search_device": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
     "mcs_window_select": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P, _I32, _I32, ctypes.c_double, _P, _P, _P]),
     "mcs_window_match": (ctypes.c_int, [_I32, _I32, _P, _I32, _P, _P, _P, _P, _I32, ctypes.c_double, _P, _P, _P]),
+    # DBoW2 vocabulary (include/mcs_vocab.h)
+    "mcs_vocab_create": (_I32, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _I32, _P]),
+    "mcs_vocab_destroy": (_I32, [_P]),
+    "mcs_vocab_info": (_I32, [_P, _P]),
+    "mcs_vocab_transform_words_device": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P]),
+    "mcs_vocab_transform": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

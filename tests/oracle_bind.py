@@ -41,6 +41,10 @@ _SIGS = {
     "oracle_search_for_triangulation_raw": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
     "oracle_frame_grid": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "oracle_window_candidates": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I]),
+    # DBoW2 vocabulary oracle
+    "oracle_vocab_words": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P]),
+    "oracle_vocab_transform": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I,
+                                    _P, _P, _P, _P, _P, _P, _P]),
     "oracle_window_match": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _D, _P, _P]),
 }
 
@@ -284,3 +288,35 @@ def pose_optimization(pr, trace=0):
     return dict(pose=pose, outlier=out[:n].copy(), n_good=ngood, bad_ratio=bad.value,
                 report1=r1, report2=r2, trace1=t1[:min(trace, r1.iterations)],
                 trace2=t2[:min(trace, r2.iterations)])
+
+
+def _voc_args(voc):
+    a = [np.ascontiguousarray(voc[k]) for k in ("node_id", "parent_id", "weight", "desc", "word_node")]
+    return a, [voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(a[0]), _p(a[0]), _p(a[1]),
+               _p(a[2]), _p(a[3]), len(a[4]), _p(a[4])]
+
+
+def vocab_words(voc, feats, levelsup=4):
+    """DBoW2 transform(feature, ...) per descriptor (TemplatedVocabulary.h:1217-1261)."""
+    feats = np.ascontiguousarray(feats, np.uint8).reshape(-1, 32)
+    n = feats.shape[0]
+    keep, args = _voc_args(voc)
+    word, w, node = np.zeros(n, np.uint32), np.zeros(n, np.float64), np.zeros(n, np.uint32)
+    lib().oracle_vocab_words(*args, _p(feats), n, levelsup, _p(word), _p(w), _p(node))
+    return word, w, node
+
+
+def vocab_transform(voc, feats, levelsup=4):
+    """DBoW2 transform(features, BowVector, FeatureVector, levelsup) (:1126-1196)."""
+    feats = np.ascontiguousarray(feats, np.uint8).reshape(-1, 32)
+    n = feats.shape[0]
+    m = max(n, 1)
+    keep, args = _voc_args(voc)
+    bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+    fn, fp, ff = np.zeros(m, np.uint32), np.zeros(m + 1, np.int32), np.zeros(m, np.uint32)
+    bn, fvn = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    lib().oracle_vocab_transform(*args, _p(feats), n, levelsup, _p(bw), _p(bv), _p(bn), _p(fn),
+                                 _p(fp), _p(ff), _p(fvn))
+    bow = {int(bw[i]): float(bv[i]) for i in range(int(bn[0]))}
+    fv = {int(fn[j]): ff[fp[j]:fp[j + 1]].tolist() for j in range(int(fvn[0]))}
+    return bow, fv
