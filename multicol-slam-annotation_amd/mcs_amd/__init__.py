@@ -132,6 +132,10 @@ SIGNATURES = {
     "mcs_vocab_info": (_I32, [_P, _P]),
     "mcs_vocab_transform_words_device": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P]),
     "mcs_vocab_transform": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    # omni camera mirror masks (include/mcs_cammodel.h)
+    "mcs_mirror_mask_layout": (_I32, [_I32, _I32, _I32, _P, _P, _P, _P]),
+    "mcs_create_mirror_mask_device": (_I32, [ctypes.c_double, ctypes.c_double, _I32, _I32, _I32, _P, _P]),
+    "mcs_is_point_in_mirror_mask": (_I32, [_P, _I32, _I32, ctypes.c_double, ctypes.c_double]),
 }
 
 _lib = None

@@ -145,3 +145,51 @@ def tracking_frames(settings):
 
 def load_settings(path):
     return read_filestorage(path)
+
+
+def mirror_mask_layout(width, height, levels=4):
+    """Level sizes/offsets of the packed mirror-mask pyramid (include/mcs_cammodel.h)."""
+    from . import _check, lib
+    w = np.zeros(levels, np.int32)
+    h = np.zeros(levels, np.int32)
+    off = np.zeros(levels, np.int64)
+    tot = np.zeros(1, np.int64)
+    _check(lib().mcs_mirror_mask_layout(int(width), int(height), int(levels),
+                                        w.ctypes.data, h.ctypes.data, off.ctypes.data,
+                                        tot.ctypes.data))
+    return w, h, off, int(tot[0])
+
+
+def create_mirror_masks(cam, width, height, levels=4, device=0):
+    """CreateMirrorMask (src/cam_model_omni.cpp:183-222) on the GPU: list of torch uint8 masks
+    (255 inside the mirror circle), one per level, views into one packed device buffer."""
+    import torch
+    from . import _check, lib
+    w, h, off, total = mirror_mask_layout(width, height, levels)
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda:%d" % device)
+    stream = torch.cuda.current_stream(buf.device).cuda_stream
+    _check(lib().mcs_create_mirror_mask_device(float(cam["u0"]), float(cam["v0"]), int(width),
+                                               int(height), int(levels), buf.data_ptr(), stream))
+    return [buf[int(off[l]):int(off[l]) + int(w[l]) * int(h[l])].view(int(h[l]), int(w[l]))
+            for l in range(levels)]
+
+
+def rig_mirror_masks(rig, device=0):
+    """cSystem::LoadMCS mask choice (src/cSystem.cpp:164-172): 4-level mirror masks when
+    Camera.mirrorMask == 1, else one all-ones Iw x Ih mask."""
+    import torch
+    out = []
+    for cam, (iw, ih), flag in zip(rig["cams"], rig["sizes"], rig["mirror_mask"]):
+        if flag:
+            out.append(create_mirror_masks(cam, iw, ih, 4, device))
+        else:
+            out.append([torch.ones((ih, iw), dtype=torch.uint8, device="cuda:%d" % device)])
+    return out
+
+
+def is_point_in_mirror_mask(mask, u, v):
+    """isPointInMirrorMask (src/cam_model_omni.cpp:165-180) on one level's host mask."""
+    from . import lib
+    m = np.ascontiguousarray(mask, dtype=np.uint8)
+    return bool(lib().mcs_is_point_in_mirror_mask(m.ctypes.data, m.shape[1], m.shape[0],
+                                                  float(u), float(v)))

@@ -45,6 +45,9 @@ _SIGS = {
     "oracle_vocab_words": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P]),
     "oracle_vocab_transform": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _I, _I,
                                     _P, _P, _P, _P, _P, _P, _P]),
+    # omni camera mirror masks
+    "oracle_create_mirror_mask": (_I, [_D, _D, _I, _I, _I, _P]),
+    "oracle_is_point_in_mirror_mask": (_I, [_P, _I, _I, _D, _D]),
     "oracle_window_match": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _D, _P, _P]),
 }
 
