@@ -290,6 +290,63 @@ def run_bow(args, rank, world, dev, stream, d_desc, n_valid):
     return out, cpu
 
 
+def launch_ranks(n):
+    """One process per GPU via torch.distributed.run (rendezvous on 127.0.0.1); the children
+    re-enter main() with RANK/LOCAL_RANK/WORLD_SIZE set.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def reduce_over_ranks(dt, kp_total, dev, world):
+    """Timed-region reduction of every leg: MAX of the wall time, SUM of the work."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    k = torch.tensor([kp_total], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(k, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(k.item())
+
+
+def selftest_dist(rank, world):
+    """`--selftest-dist`: the N-rank launch and the collective code of the legs on CPU (gloo):
+    the timed-region reduction, the config-D camera all-gather (mcs_amd/rig.py) and the
+    GlobalBA exchange callback (mcs_amd/ba.py TorchExchange).  No GPU is touched."""
+    import torch
+    import torch.distributed as dist
+    from mcs_amd import rig
+    from mcs_amd import ba as mba
+    dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    dt, kp = reduce_over_ranks(0.01 * (rank + 1), 1000.0 * (rank + 1), dev, world)
+    assert dt == 0.01 * world and kp == 1000.0 * world * (world + 1) / 2
+    NC, MD = 8, 3
+    S = rig.slots_per_rank(NC, world)
+    own = rig.owned_cameras(NC, world, rank)
+    local = torch.full((S, MD), -1, dtype=torch.int32)
+    for s, c in enumerate(own):
+        local[s] = torch.arange(MD, dtype=torch.int32) + 100 * c
+    g = rig.gather_camera_blocks(local, NC)
+    want = torch.stack([torch.arange(MD, dtype=torch.int32) + 100 * c for c in range(NC)])
+    assert torch.equal(g, want), g
+    xch = mba.TorchExchange(10, dev)
+    xch.buf.fill_(float(rank + 1))
+    assert xch._allreduce(None, 0, 0, 60) == 0
+    assert float(xch.buf[0]) == world * (world + 1) / 2
+    if rank == 0:
+        print(json.dumps({"selftest": "ok", "n_gpus": world, "ms_per_step": dt * 1e3,
+                          "value": kp, "allgather_cameras": NC}))
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -310,11 +367,21 @@ def main():
                     help="config D multi-frames per step (8 cams 1024^2, camera per GPU); 0 = off")
     ap.add_argument("--bow-reps", type=int, default=10, help="timed DBoW2 transform launches; 0 = off")
     ap.add_argument("--d-unique", type=int, default=2, help="distinct rendered config D multi-frames")
+    ap.add_argument("--selftest-dist", action="store_true",
+                    help="CPU (gloo) rehearsal of the multi-rank launch and collectives only")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside torchrun: start N fresh ranks as child processes (nothing
+        # has touched the GPU in this process yet) and exit with their status
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.selftest_dist:
+        return selftest_dist(rank, world)
 
     import torch
     import torch.distributed as dist
@@ -390,13 +457,8 @@ def main():
     stages, ncalls = ex.read_timing() if args.stage_timing else ({}, 0)
 
     kp_per_step = int(d_cnt.sum().item())
-    t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
-    kp_tot = torch.tensor([kp_per_step * args.steps], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kp_tot, op=dist.ReduceOp.SUM)
-    dt_max = float(t_max.item())
-    value = float(kp_tot.item()) / dt_max / 1e3
+    dt_max, kp_tot = reduce_over_ranks(dt, kp_per_step * args.steps, dev, world)
+    value = kp_tot / dt_max / 1e3
 
     wh, _ = ex.levels()
     bpf = alg_bytes_pyr_fast(wh)

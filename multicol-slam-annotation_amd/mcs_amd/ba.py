@@ -503,7 +503,8 @@ class TorchExchange:
             t = self.buf[off:off + cnt]
             rop = self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX
             self.dist.all_reduce(t, op=rop, group=self.group)
-            self.torch.cuda.synchronize(self.buf.device)
+            if self.buf.is_cuda:
+                self.torch.cuda.synchronize(self.buf.device)
             self.calls += 1
             return 0
         except Exception:   # never raise through the C stack
