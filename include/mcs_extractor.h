@@ -40,8 +40,9 @@ typedef struct mcs_extractor_params {
   int32_t fast_threshold;  /* 20 (5 for the initialisation extractor) */
   int32_t use_agast;       /* must be 0 (AGAST: MCS_ERR_UNSUPPORTED) */
   int32_t fast_agast_type; /* must be 2 == TYPE_9_16 */
-  int32_t do_dbrief;       /* must be 0 this round (dBRIEF: MCS_ERR_UNSUPPORTED) */
-  int32_t learn_masks;     /* must be 0 this round (mdBRIEF: MCS_ERR_UNSUPPORTED) */
+  int32_t do_dbrief;       /* 1 = dBRIEF (needs mcs_extractor_set_cam_models) */
+  int32_t learn_masks;     /* 1 = mdBRIEF: 3 rotated patterns -> descriptor + stability mask
+                              (src/mdBRIEFextractorOct.cpp:410-554; needs camera models) */
   int32_t desc_size;       /* bytes: 16, 32 or 64 */
 } mcs_extractor_params;
 

@@ -5,8 +5,8 @@
 //   reference                                        here
 //   mdBRIEFextractorOct(nfeatures, scaleFactor, ...)  mcs::mdBRIEFextractorOct(same args, w, h)
 //     include/mdBRIEFextractorOct.h:339-351
-//   operator()(image, mask, kps, camModel, desc,      operator()(image, stride, mask, kps, desc,
-//              descMasks)  :355-361                               descMasks)
+//   operator()(image, mask, kps, camModel, desc,      operator()(image, stride, mask, mstride,
+//              descMasks)  :355-361                      kps, camModel, desc, descMasks)
 //   DescriptorDistance64 (include/cORBmatcher.h:43)   mcs::DescriptorDistance64
 //   cOptimizer::LocalBundleAdjustment (cOptimizer.h:61) mcs::LocalBA::run(problem, ...)
 //
@@ -14,6 +14,7 @@
 // std::vector<mcs_keypoint> can be copied into std::vector<cv::KeyPoint> member-wise.
 #pragma once
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -43,6 +44,8 @@ class mdBRIEFextractorOct {
     p.desc_size = descSize;
     check(mcs_extractor_create(&p, width, height, 1, device, &h_), "mcs_extractor_create");
     desc_size_ = descSize;
+    do_dbrief_ = do_dBrief;
+    learn_masks_ = learnMasks;
     nlevels_ = nlevels;
     scale_factor_ = scaleFactor;
   }
@@ -50,11 +53,18 @@ class mdBRIEFextractorOct {
   mdBRIEFextractorOct(const mdBRIEFextractorOct&) = delete;
   mdBRIEFextractorOct& operator=(const mdBRIEFextractorOct&) = delete;
 
-  // operator()(image, mask, kps, camModel, desc, descMasks): the camera model is only read by
-  // the dBRIEF/mdBRIEF branches, which this build rejects (MCS_ERR_UNSUPPORTED).
+  // operator()(image, mask, kps, camModel, desc, descMasks) (:355-361).  The camera model is
+  // read only by the dBRIEF / mdBRIEF branches (keypoint undistortion :1304-1316 and the
+  // re-distorted pattern :250-283); it is forwarded to the device when it changes.
   void operator()(const uint8_t* image, int stride, const uint8_t* mask, int mask_stride,
-                  std::vector<mcs_keypoint>& kps, std::vector<uint8_t>& desc,
-                  std::vector<uint8_t>& descMasks) {
+                  std::vector<mcs_keypoint>& kps, const mcs_cam_model& camModel,
+                  std::vector<uint8_t>& desc, std::vector<uint8_t>& descMasks) {
+    if ((do_dbrief_ || learn_masks_) &&
+        (!cam_set_ || std::memcmp(&cam_, &camModel, sizeof(cam_)) != 0)) {
+      check(mcs_extractor_set_cam_models(h_, &camModel, 1), "mcs_extractor_set_cam_models");
+      cam_ = camModel;
+      cam_set_ = true;
+    }
     const int cap = mcs_extractor_capacity(h_);
     kps.resize(cap);
     desc.resize((size_t)cap * desc_size_);
@@ -70,7 +80,7 @@ class mdBRIEFextractorOct {
 
   int GetLevels() const { return nlevels_; }
   double GetScaleFactor() const { return (double)scale_factor_; }
-  bool GetMasksLearned() const { return false; }
+  bool GetMasksLearned() const { return learn_masks_; }   // mdBRIEFextractorOct.h:367
   int GetDescriptorSize() const { return desc_size_; }
   mcs_extractor* handle() { return h_; }
 
@@ -78,6 +88,8 @@ class mdBRIEFextractorOct {
   mcs_extractor* h_ = nullptr;
   int desc_size_ = 32, nlevels_ = 8;
   float scale_factor_ = 1.2f;
+  bool do_dbrief_ = false, learn_masks_ = false, cam_set_ = false;
+  mcs_cam_model cam_{};
 };
 
 inline int DescriptorDistance64(const uint64_t* d1, const uint64_t* d2, const int& dim) {
