@@ -35,11 +35,33 @@ sys.path.insert(0, ROOT)
 
 METRIC = "kfeatures/sec + LocalBA iters/sec, 3×754×480 fisheye, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# FP64 dense matrix peak of MI355X (AMD spec, 78.6 TFLOP/s; v_mfma_f64_16x16x4_f64).  Not
-# listed in the local guide: tools/mfma_f64_peak.hip measures the per-CU issue rate.
-FP64_MFMA_PEAK_TFLOPS = 78.6
+# FP64 dense matrix peak of MI355X as MEASURED on the box by tools/bench/mfma_f64_peak.hip
+# (back-to-back v_mfma_f64_16x16x4_f64, every CU; profiles/r02_mfma_f64_peak.json).  The AMD
+# spec figure (78.6 TFLOP/s) is not reached by that instruction stream and is not used.
+FP64_MFMA_PEAK_TFLOPS = 45.14
+FP64_MFMA_PEAK_SRC = "profiles/r02_mfma_f64_peak.json (measured)"
 # algorithmic bytes of pyramid + FAST per 754x480 camera-frame
 PYR_FAST_BYTES_754x480 = 2_970_708
+
+
+def pmc_traffic(alg_bytes):
+    """HBM traffic of the pyramid+FAST launches from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py output named in profiles/pmc_traffic.json): FETCH_SIZE + WRITE_SIZE
+    per bench step, raw and with the guide's x2 correction of FETCH_SIZE for wide streaming
+    reads.  The kernels read dwords, for which the correction is uncalibrated, so both are
+    reported; `traffic` is the raw figure."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tf):
+        return {}
+    try:
+        d = json.load(open(tf))
+        raw = d["pyramid+fast_raw_bytes_per_call"]
+        return {"traffic": raw, "traffic_raw": raw,
+                "traffic_fetch_x2": d.get("pyramid+fast_bytes_per_call"),
+                "traffic_source": d.get("source", tf),
+                "traffic_over_alg": round(raw / alg_bytes, 3) if raw else None}
+    except (KeyError, ValueError):
+        return {}
 
 
 def alg_bytes_pyr_fast(level_wh):
@@ -142,7 +164,8 @@ def run_global_ba(args, rank, world, local_rank, dev):
            "trials": n_tr,
            "roofline_solve": {"kernel": "ldlt k_panel x T + k_backward (n=%d)" % n, "bound": "mfma",
                               "achieved": None if achieved is None else round(achieved, 4),
-                              "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "peak": FP64_MFMA_PEAK_TFLOPS, "peak_source": FP64_MFMA_PEAK_SRC,
+                              "unit": "TFLOP/s",
                               "frac": None if achieved is None else round(achieved / FP64_MFMA_PEAK_TFLOPS, 5),
                               "flops_per_trial": flops}}
     cpu = None
@@ -466,19 +489,16 @@ def main():
     stage_ms = {}
     if ncalls:
         stage_ms = {k: v / ncalls for k, v in stages.items()}
+        # pyramid + FAST = k_pyr_rows<true> x (L-1) (resize + fused blur) + k_fast_cells; the
+        # level-0 blur launch is not part of the algorithmic bytes and is not timed
         t_pf = (stage_ms["pyramid"] + stage_ms["fast"]) / 1e3
         achieved = bpf * F / t_pf / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):
-            try:
-                traffic = json.load(open(tf)).get("pyramid+fast_bytes_per_call")
-            except Exception:
-                traffic = None
-        roofline = {"kernel": "pyramid+fast (k_pyr_rows<true> x7: resize + fused blur, k_fast_cells)",
+        roofline = {"kernel": "pyramid+fast: k_pyr_rows<true> x %d (resize + 5x5 blur) + "
+                              "k_fast_cells (FAST-9/16 + cell-local NMS + mask)" % (len(wh) - 1),
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "alg_bytes_per_call": bpf * F}
+                    "traffic": None, "alg_bytes_per_call": bpf * F}
+        roofline.update(pmc_traffic(bpf * F))
 
     # ---- LocalBA (config C): 10 local MultiKeyFrames + 3 fixed observers, 3k points, ~20k edges
     localba = None

@@ -5,11 +5,11 @@
 //
 // Reference path (billamiable/MultiCol-SLAM-Annotation):
 //   mdBRIEFextractorOct::operator()        src/mdBRIEFextractorOct.cpp:1244-1337
-//   ComputePyramid                         :1158-1201   -> k_pyr_blur, k_mask_nearest
+//   ComputePyramid                         :1158-1201   -> k_pyr_rows, k_mask_nearest
 //   ComputeKeyPointsOctTree (FAST part)    :863-949     -> k_fast_cells
 //   DistributeOctTree / DivideNode         :569-861     -> k_octree
 //   computeOrientation / IC_Angle          :221-248     -> k_orient_desc (part 1)
-//   boxFilter 5x5                          :1301        -> k_pyr_blur (fused)
+//   boxFilter 5x5                          :1301        -> k_pyr_rows (fused)
 //   compute_ORB / rotatePattern            :285-354     -> k_orient_desc (part 2)
 #include "common.hpp"
 #include "extractor_plan.hpp"
@@ -414,7 +414,7 @@ int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const ui
   const uint8_t* mf = nullptr;
   if (mask) {
     // level 0 of the single-call mask pyramid doubles as the upload buffer
-    MCS_HIP_CHECK(hipMemcpy2D(h->d_mask_single, pl.W, mask, mask_stride, pl.W, pl.H,
+    MCS_HIP_CHECK(hipMemcpy2D(h->d_mask_single, pl.lv[0].bpitch, mask, mask_stride, pl.W, pl.H,
                               hipMemcpyHostToDevice));
     launch_mask_pyramids(pl, h->d_mask_single, 1, h->d_mask_single, st);
     launch_cell_maskflags(pl, h->d_cells, h->d_mask_single, 1, h->d_flags_single, st);

@@ -94,7 +94,7 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     L.img_off = img_off;
     img_off = align(img_off + (int64_t)L.bpitch * L.h, 256);
     L.mask_off = mask_off;
-    mask_off += (int64_t)L.w * L.h;
+    mask_off = align(mask_off + (int64_t)L.bpitch * L.h, 256);
     L.nfeat = nfl[l];
     L.scale = (float)sf[l];
     L.patch_size_scaled = (int)(kPatchSize * sf[l]);

@@ -35,7 +35,7 @@ struct LevelPlan {
   int32_t bpitch;
   int64_t pyr_off;            // offset of the level inside a frame's pyramid workspace (l >= 1)
   int64_t img_off;            // offset inside a frame's blurred-level workspace (pitch bpitch)
-  int64_t mask_off;           // offset inside a mask pyramid (pitch w, unpadded)
+  int64_t mask_off;           // offset inside a mask pyramid (pitch bpitch: aligned dword loads)
   int32_t cell_begin, cell_end;
   int32_t cand_off, cand_cap; // candidate gather area within a frame (sum of cell caps)
   int32_t sel_off, sel_cap;   // octree output area within a frame
@@ -56,7 +56,7 @@ struct Plan {
   std::vector<CellDesc> cells;
   int64_t pyr_frame_bytes = 0;   // levels 1..L-1
   int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred levels, padded pitch)
-  int64_t mask_frame_bytes = 0;  // levels 0..L-1 (mask pyramid, unpadded)
+  int64_t mask_frame_bytes = 0;  // levels 0..L-1 (mask pyramid, pitch bpitch)
   int32_t slots_per_frame = 0;   // sum of cell caps
   int32_t cand_per_frame = 0;    // == slots_per_frame
   int32_t sel_per_frame = 0;     // sum of level sel caps == mcs_extractor_capacity

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     }
     mask = a.mask_pyr + (int64_t)mi * a.mask_fstride + a.lp.mask_off[l];
   }
-  const int pitch = a.lp.pitch[l], mw = a.lp.w[l];
+  const int pitch = a.lp.pitch[l], mw = a.lp.bpitch[l];   // mask pyramid pitch = bpitch
   const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
                                 : a.pyr + (int64_t)f * a.pyr_fstride + a.lp.pyr_off[l];
   const int ww = max(0, c.wx1 - c.wx0), wh = max(0, c.wy1 - c.wy0);

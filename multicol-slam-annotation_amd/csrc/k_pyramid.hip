@@ -1,14 +1,10 @@
 // K1 + K5 fused: one pyramid level = cv::resize(INTER_LINEAR) of level l-1 and
-// the 5x5 normalised box blur of level l, computed from one LDS tile.
+// the 5x5 normalised box blur of level l, in one row stream per wave.
 //
 // Reference: ComputePyramid src/mdBRIEFextractorOct.cpp:1158-1201 (resize chain) and the
 // in-place boxFilter of operator() :1298-1301.  The reference pads every level by 25 px of
 // BORDER_REFLECT_101 (:1185-1197) only so that later stages may read outside it; nothing
 // downstream reads outside a level except the blur, which reflects explicitly here.
-//
-// Tile: 124 x 16 output pixels per 256-thread workgroup; the level-l tile is recomputed
-// with a 2-pixel halo (128 x 20) so raw and blurred tiles leave in one pass (stores are
-// aligned dwords: levels >= 1 and all blurred levels have a 64-byte-aligned row pitch).
 #include "common.hpp"
 #include "extractor_kernels.hpp"
 
@@ -52,21 +48,26 @@ __device__ __forceinline__ uint32_t div50(uint32_t n) { return (n * 20972u) >> 2
 // so the horizontal 5-sum needs no border cases.  Rows are produced top to bottom with a
 // 2-row halo above and below the segment:
 //   RESIZE: every source row the segment needs is streamed once per wave with aligned dword
-//           loads (two rows in flight), staged in wave-private LDS, and horizontally resized
-//           per lane (coefficients in registers); an output row combines the last two;
+//           loads (kPF rows in flight), staged in wave-private LDS, and horizontally resized
+//           per lane (coefficients in registers, v_dot2_u32_u16); an output row combines the
+//           last two;
 //   level 0: the input row is streamed the same way.
-// Each raw row is written out (RESIZE); its horizontal 5-sums (lane neighbours by shuffle)
+// Each raw row is written out (RESIZE); its horizontal 5-sums (lane neighbours by DPP)
 // enter a 5-row register window; once row r+2 exists the blurred row r is written.
-// No workgroup barriers: every wave works alone.
+// No workgroup barriers: every wave works alone.  Everything derived from the work unit is
+// wave-uniform and kept scalar (readfirstlane of the wave index and of table reads).
 constexpr int kStageDW = 192;    // staged source row (dwords), scale <= 2.2
 constexpr int kPF = 4;           // source rows in flight per wave
 
-// NDW = staged dwords per lane per source row: 1 (level 0, core <= 244), 2 (scale <= 1.5),
-// 3 (scale <= 2.2)
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// NDW = staged dwords per lane per source row: 1 (level 0), 2 (scale <= 1.5), 3 (scale <= 2.2)
 template <bool RESIZE, int NDW>
 __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
   __shared__ uint32_t lds_stage[4][kStageDW];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index as a scalar: everything derived from the work unit is wave-uniform, and the
+  // compiler must know it (SGPRs, scalar branches) or it keeps all of it in VGPRs
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   uint32_t* const stage = lds_stage[wv];
   const uint8_t* const stb = reinterpret_cast<const uint8_t*>(stage);
   int f, item;
@@ -83,27 +84,25 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
   const int xb = xs - 4 + 4 * lane;                // lane's first pixel
   const bool core_lane = xb >= xs && xb < xcore1;
   const uint8_t* S = a.src + (int64_t)f * a.src_fstride;
-  const int sh = RESIZE ? a.sh : dh, swid = RESIZE ? a.sw : dw;
+  const int sh = RESIZE ? a.sh : dh;
 
-  // staged source columns [c_lo, c_hi]; per pixel: the (mirrored) column(s) it reads
+  // staged source columns [c_lo, c_hi]: the mirrors of the strip's pixels stay inside
+  // [xs-4, xs+core+4) clamped to the level; per pixel: the (mirrored) column it reads
   int c_lo, c_hi;
-  int sx[4], sx1[4], a0[4], a1[4];
-  bool simd[4];
+  int sx[4];
+  uint32_t aa[4];     // alpha0 | alpha1 << 16 (v_dot2_u32_u16 operand)
+  int simd = 0;       // bit k: pixel k uses the SSE2 vertical form
   if (RESIZE) {
-    // mirrors of the strip's pixels stay inside [xs-4, xs+core+4) clamped to the level
-    c_lo = a.xofs[max(xs - 4, 0)];
-    c_hi = min(a.xofs[min(xs + core + 3, dw - 1)] + 1, a.sw - 1);
+    c_lo = __builtin_amdgcn_readfirstlane(a.xofs[max(xs - 4, 0)]);
+    c_hi = min(__builtin_amdgcn_readfirstlane(a.xofs[min(xs + core + 3, dw - 1)]) + 1, a.sw - 1);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int p = min(max(refl101(xb + k, dw), 0), dw - 1);
-      sx[k] = a.xofs[p] - c_lo;
-      sx1[k] = min(a.xofs[p] + 1, a.sw - 1) - c_lo;
-      a0[k] = a.alpha[2 * p];
-      a1[k] = a.alpha[2 * p + 1];
-      simd[k] = p < a.simd_end;
-      // lanes outside the strip's halo read garbage, but always inside the staged row
-      sx[k] = min(max(sx[k], 0), c_hi - c_lo);
-      sx1[k] = min(max(sx1[k], 0), c_hi - c_lo);
+      // the right neighbour is read at sx + 1 even where resize clamps it to sx (the last
+      // source column): alpha1 is 0 there, and sx + 1 stays inside the staged LDS row
+      sx[k] = min(max(a.xofs[p] - c_lo, 0), c_hi - c_lo);
+      aa[k] = (uint32_t)(uint16_t)a.alpha[2 * p] | ((uint32_t)(uint16_t)a.alpha[2 * p + 1] << 16);
+      simd |= (p < a.simd_end) << k;
     }
   } else {
     c_lo = max(xs - 4, 0);
@@ -111,38 +110,23 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       sx[k] = min(max(min(max(refl101(xb + k, dw), 0), dw - 1) - c_lo, 0), c_hi - c_lo);
-      sx1[k] = 0; a0[k] = a1[k] = 0; simd[k] = false;
+      aa[k] = 0;
     }
   }
   const int nbytes0 = c_hi - c_lo + 1;
 
   // ---- streamed source rows: aligned dwords covering [c_lo, c_hi]
   auto row_base = [&](int sr) -> const uint8_t* { return S + (int64_t)sr * a.spitch; };
+  // Every dword is loaded whole, also the last one of the last row of a frame buffer: an
+  // aligned dword that holds a valid byte lies in that byte's page, so it cannot fault, and
+  // its bytes past the row end are never consumed.  No conditional tail: a register written
+  // on two paths would have to be merged, and that merge waits for every load in flight.
   auto load_row = [&](int sr, uint32_t (&v)[NDW]) {
-    const uint8_t* rb = row_base(sr);
-    const uint8_t* st = rb + c_lo;
+    const uint8_t* st = row_base(sr) + c_lo;
     const uint32_t* ap = dev::align_down4(st);
     const int ndw = ((int)((uintptr_t)st & 3) + nbytes0 + 3) >> 2;
-    // the last row may end the buffer: only its fully valid dwords are loaded directly
-    // (indices clamped, so the loads are unconditional and stay in flight), the partial
-    // tail dword is assembled bytewise
-    const bool last = sr == sh - 1;
-    const int lim = last ? (int)((rb + swid) - reinterpret_cast<const uint8_t*>(ap)) : 4 * ndw;
-    const int jfull = max(0, min(ndw, lim >> 2) - 1);
 #pragma unroll
-    for (int m = 0; m < NDW; m++) v[m] = ap[min(lane + 64 * m, jfull)];
-    if (last && (lim & 3)) {
-#pragma unroll
-      for (int m = 0; m < NDW; m++) {
-        const int j = lane + 64 * m;
-        if (j == (lim >> 2) && j < ndw) {
-          const uint8_t* q = reinterpret_cast<const uint8_t*>(ap + j);
-          uint32_t x = 0;
-          for (int k = 0; k < (lim & 3); k++) x |= (uint32_t)q[k] << (8 * k);
-          v[m] = x;
-        }
-      }
-    }
+    for (int m = 0; m < NDW; m++) v[m] = ap[min(lane + 64 * m, ndw - 1)];
   };
   // stage a row and read this lane's 4 (mirrored) source bytes / resized values
   auto stage_and_gather = [&](int sr, const uint32_t (&v)[NDW], int (&h)[4]) {
@@ -152,8 +136,12 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
     dev::wave_sync();
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      if (RESIZE) h[k] = stb[shft + sx[k]] * a0[k] + stb[shft + sx1[k]] * a1[k];
-      else h[k] = stb[shft + sx[k]];
+      if (RESIZE) {
+        const uint32_t pp = (uint32_t)stb[shft + sx[k]] | ((uint32_t)stb[shft + sx[k] + 1] << 16);
+        h[k] = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(us2, pp), __builtin_bit_cast(us2, aa[k]), 0u, false);
+      } else {
+        h[k] = stb[shft + sx[k]];
+      }
     }
     dev::wave_sync();
   };
@@ -165,19 +153,23 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
 #pragma unroll
   for (int i = 0; i < 5; i++) win[i][0] = win[i][1] = 0;
   int next_emit = seg0;
+  // blurred row y from the window of raw rows r-4..r (r = y+2, or r = dh-1 for the last two
+  // rows); BORDER_REFLECT_101 at the top / bottom folds mirrored rows into window weights
+  // (row -1 = row 1, row -2 = row 2, row dh = row dh-2, row dh+1 = row dh-3)
   auto emit = [&](int y, int r) {
+    (void)r;
+    // window weights (wave-uniform, 4 bits each, row r-4 first)
+    const uint32_t wts = (y >= 2 && y + 2 <= dh - 1) ? 0x11111u     // interior
+                       : y == 0 ? 0x22100u                            // rows 2 1 0 1 2
+                       : y == 1 ? 0x11210u                            // rows 1 0 1 2 3
+                       : y == dh - 2 ? 0x12110u                       // rows dh-4..dh-1, dh-2
+                       : 0x12200u;                                    // dh-3 dh-2 dh-1 dh-2 dh-3
     uint32_t s01 = 0, s23 = 0;
-    if (y - 2 >= 0 && y + 2 <= dh - 1) {   // interior: window rows r-4..r == y-2..y+2
 #pragma unroll
-      for (int i = 0; i < 5; i++) { s01 += win[i][0]; s23 += win[i][1]; }
-    } else {
-#pragma unroll
-      for (int d = -2; d <= 2; d++) {
-        const int idx = refl101(y + d, dh) - (r - 4);
-#pragma unroll
-        for (int i = 0; i < 5; i++)
-          if (i == idx) { s01 += win[i][0]; s23 += win[i][1]; }
-      }
+    for (int i = 0; i < 5; i++) {
+      const uint32_t wi = (wts >> (4 * i)) & 15u;
+      s01 += wi * win[i][0];
+      s23 += wi * win[i][1];
     }
     if (core_lane) {
       const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |
@@ -237,17 +229,16 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
     const int sr0 = (int)(row_tab(r_begin) & 0xFFFF), sr1 = (int)(row_tab(r_end - 1) >> 16);
     // wave-uniform: every pixel of the strip (mirrors included) is in the SSE2 range (all
     // strips but the one holding the scalar tail), so the per-pixel select disappears
-    const bool lane_sse = simd[0] && simd[1] && simd[2] && simd[3];
-    const bool wave_sse = __ballot(!lane_sse) == 0;
+    const bool wave_sse = __ballot(simd != 15) == 0;
     int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
     int r = r_begin;
-    uint32_t t = row_tab(r);
+    uint32_t tr = row_tab(r);
     auto consume = [&](int sr, const uint32_t (&v)[NDW]) {
 #pragma unroll
       for (int k = 0; k < 4; k++) hprev[k] = hcur[k];
       stage_and_gather(sr, v, hcur);
-      while (r < r_end && (int)(t >> 16) == sr) {
-        const bool same = (int)(t & 0xFFFF) == sr;
+      while (r < r_end && (int)(tr >> 16) == sr) {
+        const bool same = (int)(tr & 0xFFFF) == sr;
         const uint32_t bb = row_beta(r);
         const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
         int o[4];
@@ -257,11 +248,11 @@ __global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
             o[k] = vres_sse(sse_x(same ? hcur[k] : hprev[k]), sse_x(hcur[k]), b0, b1);
         } else {
 #pragma unroll
-          for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, simd[k]);
+          for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, (simd >> k) & 1);
         }
         push_row(r, pack4(o));
         r++;
-        if (r < r_end) t = row_tab(r);
+        if (r < r_end) tr = row_tab(r);
       }
     };
 #pragma unroll
@@ -311,8 +302,8 @@ void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st) {
 // mask pyramid: cv::resize(INTER_NEAREST) chain, unpadded levels
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_mask_nearest(const uint8_t* __restrict__ src, int sw,
-                                                      int sh, uint8_t* __restrict__ dst, int dw,
-                                                      int dh, int64_t fstride) {
+                                                      int sh, int spitch, uint8_t* __restrict__ dst,
+                                                      int dw, int dh, int dpitch, int64_t fstride) {
   const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
   const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (dx >= dw || dy >= dh) return;
@@ -320,29 +311,32 @@ __global__ __launch_bounds__(256) void k_mask_nearest(const uint8_t* __restrict_
   const int sx = min((int)floor(dx * ifx), sw - 1);
   const int sy = min((int)floor(dy * ify), sh - 1);
   const int64_t f = (int64_t)blockIdx.z * fstride;
-  dst[f + (int64_t)dy * dw + dx] = src[f + (int64_t)sy * sw + sx];
+  dst[f + (int64_t)dy * dpitch + dx] = src[f + (int64_t)sy * spitch + sx];
 }
 
-__global__ void k_copy_bytes(const uint8_t* __restrict__ src, int64_t sstride,
-                             uint8_t* __restrict__ dst, int64_t dstride, int w, int h) {
+__global__ void k_copy_bytes(const uint8_t* __restrict__ src, int64_t sstride, int spitch,
+                             uint8_t* __restrict__ dst, int64_t dstride, int dpitch, int w, int h) {
   const int x = blockIdx.x * 64 + (threadIdx.x & 63);
   const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (x >= w || y >= h) return;
-  dst[(int64_t)blockIdx.z * dstride + (int64_t)y * w + x] =
-      src[(int64_t)blockIdx.z * sstride + (int64_t)y * w + x];
+  dst[(int64_t)blockIdx.z * dstride + (int64_t)y * dpitch + x] =
+      src[(int64_t)blockIdx.z * sstride + (int64_t)y * spitch + x];
 }
 
+// mask pyramids of n masks; level 0 comes from d_masks (n x H x W, pitch W) unless
+// d_masks == dst (level 0 already in place at pitch bpitch)
 void launch_mask_pyramids(const Plan& pl, const uint8_t* d_masks, int n, uint8_t* dst,
                           hipStream_t st) {
   const LevelPlan& L0 = pl.lv[0];
   dim3 b(256);
-  hipLaunchKernelGGL(k_copy_bytes, dim3((L0.w + 63) / 64, (L0.h + 3) / 4, n), b, 0, st, d_masks,
-                     (int64_t)L0.w * L0.h, dst, pl.mask_frame_bytes, L0.w, L0.h);
+  if (d_masks != dst)
+    hipLaunchKernelGGL(k_copy_bytes, dim3((L0.w + 63) / 64, (L0.h + 3) / 4, n), b, 0, st, d_masks,
+                       (int64_t)L0.w * L0.h, L0.w, dst, pl.mask_frame_bytes, L0.bpitch, L0.w, L0.h);
   for (int l = 1; l < pl.nlevels; l++) {
     const LevelPlan& S = pl.lv[l - 1];
     const LevelPlan& D = pl.lv[l];
     hipLaunchKernelGGL(k_mask_nearest, dim3((D.w + 63) / 64, (D.h + 3) / 4, n), b, 0, st,
-                       dst + S.mask_off, S.w, S.h, dst + D.mask_off, D.w, D.h,
+                       dst + S.mask_off, S.w, S.h, S.bpitch, dst + D.mask_off, D.w, D.h, D.bpitch,
                        pl.mask_frame_bytes);
   }
 }
@@ -357,11 +351,11 @@ __global__ __launch_bounds__(64) void k_cell_maskflags(const CellDesc* __restric
   const CellDesc cd = cells[c];
   const int ww = max(0, cd.wx1 - cd.wx0), wh = max(0, cd.wy1 - cd.wy0);
   const uint8_t* mk = mp + (int64_t)m * mfs + lp.mask_off[cd.level];
-  const int w = lp.w[cd.level];
+  const int mpitch = lp.bpitch[cd.level];
   bool any = false;
   for (int i = threadIdx.x; i < ww * wh; i += 64) {
     const int y = i / ww, x = i - y * ww;
-    any |= mk[(int64_t)(cd.wy0 + y) * w + cd.wx0 + x] != 0;
+    any |= mk[(int64_t)(cd.wy0 + y) * mpitch + cd.wx0 + x] != 0;
   }
   const uint64_t b = __ballot(any);
   if (threadIdx.x == 0) flags[(int64_t)m * ncells + c] = b != 0;

@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmcs_amd.so")
+# MCS_AMD_LIB: an alternative build of the same library (tools/ ablation runs only)
+LIB_PATH = os.environ.get("MCS_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libmcs_amd.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
 
 MCS_OK = 0

@@ -47,19 +47,22 @@ def main(fetch_csv, write_csv, out_json):
             "write": (sum(w) / len(w) * 1024) if w else None,
         }
     k = out["kernels"]
-    # per extractor call (= one k_fast_cells launch): every k_pyr_blur<true> launch of the
-    # call (one per level 1..L-1: resize + fused blur) + the FAST launch
+    # per extractor call (= one k_fast_cells launch): every k_pyr_rows<true> launch of the call
+    # (one per level 1..L-1: resize + fused blur) + the FAST launch
     fa = k.get("k_fast_cells")
-    rs = next((v for n, v in k.items() if n.startswith(("k_pyr_blur<true", "k_pyr_rows<true"))), None)
+    rs = [v for n, v in k.items() if n.startswith("k_pyr_rows<true")]
     if rs and fa and fa["launches"]:
-        per_call = rs["launches"] / fa["launches"]
-        rd = rs["fetch_raw"] * per_call + fa["fetch_raw"]
-        rd2 = rs["fetch_x2"] * per_call + fa["fetch_x2"]
-        wt = rs["write"] * per_call + (fa["write"] or 0)
-        out["pyr_launches_per_call"] = per_call
-        out["pyramid+fast_bytes_per_call_rawread"] = rd + wt
-        # reported figure: gfx950 x2 read correction (MI355X_MICROARCH.md "HBM")
+        calls = fa["launches"]
+        rd = sum(v["fetch_raw"] * v["launches"] for v in rs) / calls + fa["fetch_raw"]
+        rd2 = sum(v["fetch_x2"] * v["launches"] for v in rs) / calls + fa["fetch_x2"]
+        wt = sum((v["write"] or 0) * v["launches"] for v in rs) / calls + (fa["write"] or 0)
+        out["pyr_launches_per_call"] = sum(v["launches"] for v in rs) / calls
+        out["pyramid+fast_raw_bytes_per_call"] = rd + wt
+        out["pyramid+fast_fetch_raw_per_call"] = rd
+        out["pyramid+fast_write_per_call"] = wt
+        # gfx950 x2 read correction (MI355X_MICROARCH.md "HBM"; exact for 16 B/lane only)
         out["pyramid+fast_bytes_per_call"] = rd2 + wt
+    out["source"] = {"fetch": fetch_csv, "write": write_csv}
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
