@@ -50,9 +50,9 @@ struct mcs_extractor {
   int32_t* d_cnode = nullptr;    // [F][cand_per_frame]
   uint32_t* d_sel = nullptr;     // [F][sel_per_frame]     octree selection per level
   int32_t* d_sel_count = nullptr;  // [F][nlevels]
-  // masks: registered set + single-call slot, each with per-cell "any mask pixel" flags
-  uint8_t* d_mask_pyr = nullptr; uint8_t* d_mask_flags = nullptr; int n_masks = 0;
-  uint8_t* d_mask_single = nullptr; uint8_t* d_flags_single = nullptr;
+  // masks: registered set + single-call slot, each with per-cell window bitmaps
+  uint8_t* d_mask_pyr = nullptr; uint64_t* d_mask_bits = nullptr; int n_masks = 0;
+  uint8_t* d_mask_single = nullptr; uint64_t* d_bits_single = nullptr;
   // single-frame staging
   uint8_t* d_in = nullptr;
   mcs_keypoint* d_kps = nullptr; uint8_t* d_desc = nullptr; int32_t* d_count = nullptr;
@@ -88,7 +88,7 @@ static inline void stage_mark(mcs_extractor* h, int stage, hipStream_t st) {
 
 // Core batched pipeline on device buffers.
 static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uint8_t* mask_pyr,
-                     const uint8_t* mask_flags, const int32_t* d_mask_index, mcs_keypoint* d_kps,
+                     const uint64_t* mask_bits, const int32_t* d_mask_index, mcs_keypoint* d_kps,
                      int32_t* d_counts, uint8_t* d_desc, uint8_t* d_desc_masks,
                      const int32_t* d_cam_index, hipStream_t st) {
   const Plan& pl = h->plan;
@@ -129,8 +129,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     FastArgs fa;
     fa.img0 = d_images; fa.img0_fstride = img0_fs;
     fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
-    fa.mask_pyr = mask_pyr; fa.mask_fstride = pl.mask_frame_bytes;
-    fa.cell_flags = mask_flags;
+    fa.mask_bits = mask_bits;
     fa.mask_index = d_mask_index;
     fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
     fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
@@ -254,7 +253,7 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
   ALLOC(h->d_sel, F * pl.sel_per_frame);
   ALLOC(h->d_sel_count, F * pl.nlevels);
   ALLOC(h->d_mask_single, pl.mask_frame_bytes);
-  ALLOC(h->d_flags_single, pl.cells.size());
+  ALLOC(h->d_bits_single, pl.cells.size() * kMaskBitRows);
   ALLOC(h->d_in, (size_t)width * height);
   ALLOC(h->d_kps, pl.sel_per_frame);
   ALLOC(h->d_desc, (size_t)pl.sel_per_frame * pl.p.desc_size);
@@ -281,7 +280,7 @@ void mcs_extractor_destroy(mcs_extractor* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_pyr, h->d_blur,
                   h->d_slots, h->d_cell_counts, h->d_cand, h->d_cnode, h->d_sel, h->d_sel_count,
-                  h->d_mask_pyr, h->d_mask_flags, h->d_mask_single, h->d_flags_single, h->d_in,
+                  h->d_mask_pyr, h->d_mask_bits, h->d_mask_single, h->d_bits_single, h->d_in,
                   h->d_kps, h->d_desc, h->d_count, h->d_dmask, h->d_cams};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -342,16 +341,16 @@ int mcs_extractor_set_masks_device(mcs_extractor* h, const uint8_t* d_masks, int
   if (!h || n_masks < 0 || (n_masks > 0 && !d_masks)) return MCS_ERR_ARG;
   MCS_HIP_CHECK(hipSetDevice(h->device));
   if (h->d_mask_pyr) { MCS_HIP_CHECK(hipFree(h->d_mask_pyr)); h->d_mask_pyr = nullptr; }
-  if (h->d_mask_flags) { MCS_HIP_CHECK(hipFree(h->d_mask_flags)); h->d_mask_flags = nullptr; }
+  if (h->d_mask_bits) { MCS_HIP_CHECK(hipFree(h->d_mask_bits)); h->d_mask_bits = nullptr; }
   h->n_masks = 0;
   if (n_masks == 0) return MCS_OK;
   int rc = dalloc(&h->d_mask_pyr, (size_t)n_masks * h->plan.mask_frame_bytes);
   if (rc) return rc;
-  rc = dalloc(&h->d_mask_flags, (size_t)n_masks * h->plan.cells.size());
+  rc = dalloc(&h->d_mask_bits, (size_t)n_masks * h->plan.cells.size() * kMaskBitRows);
   if (rc) return rc;
   launch_mask_pyramids(h->plan, d_masks, n_masks, h->d_mask_pyr, (hipStream_t)stream);
-  launch_cell_maskflags(h->plan, h->d_cells, h->d_mask_pyr, n_masks, h->d_mask_flags,
-                        (hipStream_t)stream);
+  launch_cell_maskbits(h->plan, h->d_cells, h->d_mask_pyr, n_masks, h->d_mask_bits,
+                       (hipStream_t)stream);
   MCS_HIP_CHECK(hipGetLastError());
   h->n_masks = n_masks;
   return MCS_OK;
@@ -386,7 +385,7 @@ int mcs_extract_batch_device_ex(mcs_extractor* h, const uint8_t* d_images, int32
   if (n_frames > h->max_frames) { set_error("n_frames > max_frames"); return MCS_ERR_CAPACITY; }
   MCS_HIP_CHECK(hipSetDevice(h->device));
   const uint8_t* mp = h->n_masks > 0 ? h->d_mask_pyr : nullptr;
-  const uint8_t* mf = h->n_masks > 0 ? h->d_mask_flags : nullptr;
+  const uint64_t* mf = h->n_masks > 0 ? h->d_mask_bits : nullptr;
   return run_batch(h, d_images, n_frames, mp, mf, mp ? d_cam_index : nullptr, d_kps, d_counts,
                    d_desc, d_desc_masks, h->n_cams > 1 ? d_cam_index : nullptr,
                    (hipStream_t)stream);
@@ -411,16 +410,16 @@ int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const ui
   hipStream_t st = nullptr;
   MCS_HIP_CHECK(hipMemcpy2D(h->d_in, pl.W, image, stride, pl.W, pl.H, hipMemcpyHostToDevice));
   const uint8_t* mp = nullptr;
-  const uint8_t* mf = nullptr;
+  const uint64_t* mf = nullptr;
   if (mask) {
     // level 0 of the single-call mask pyramid doubles as the upload buffer
     MCS_HIP_CHECK(hipMemcpy2D(h->d_mask_single, pl.lv[0].bpitch, mask, mask_stride, pl.W, pl.H,
                               hipMemcpyHostToDevice));
     launch_mask_pyramids(pl, h->d_mask_single, 1, h->d_mask_single, st);
-    launch_cell_maskflags(pl, h->d_cells, h->d_mask_single, 1, h->d_flags_single, st);
+    launch_cell_maskbits(pl, h->d_cells, h->d_mask_single, 1, h->d_bits_single, st);
     MCS_HIP_CHECK(hipGetLastError());
     mp = h->d_mask_single;
-    mf = h->d_flags_single;
+    mf = h->d_bits_single;
   }
   const bool learn = pl.p.learn_masks != 0;
   int rc = run_batch(h, h->d_in, 1, mp, mf, nullptr, h->d_kps, h->d_count, h->d_desc,
