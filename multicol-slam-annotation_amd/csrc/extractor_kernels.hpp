@@ -38,7 +38,7 @@ struct PyrArgs {
 };
 // strips of <= 244 columns (61 lanes x 4 px, so a level-0 strip + halo is <= 64 dwords);
 // segment height chosen so that a batch of F
-// frames gives ~16k waves (latency hiding), between 16 and 64 rows
+// frames gives ~16k waves (latency hiding), between 8 and 64 rows
 inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
   const int n = (dw + 243) / 244;
   a.core = ((dw + n - 1) / n + 3) & ~3;
@@ -47,7 +47,7 @@ inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
   const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
   const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
   int rows = (dh + segs - 1) / segs;
-  rows = std::min(64, std::max(16, rows));
+  rows = std::min(64, std::max(8, rows));
   a.seg_rows = rows;
   a.tiles_y = (dh + rows - 1) / rows;
 }

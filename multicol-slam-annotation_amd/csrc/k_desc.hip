@@ -137,7 +137,8 @@ __device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   __shared__ uint32_t s_raw[8][kRawH * kRawW];
   __shared__ __attribute__((aligned(16))) uint8_t s_blr[8][kBlrH * kBlrRow];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index as a scalar: the pair, its level and counts are wave-uniform
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
   int f, item;
   const int pairs = (a.sel_per_frame + 1) / 2;
@@ -194,27 +195,18 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   sincos(theta, &sa, &ca);
   const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
   const uint8_t* bc = &s_blr[slot][21 * kBlrRow + 21 + mis];
-  uint32_t words[16];
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    words[r] = 0u;
-    if (r < nw) {
-      const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
-      const double px0 = c_pattern_d[4 * t], py0 = c_pattern_d[4 * t + 1];
-      const double px1 = c_pattern_d[4 * t + 2], py1 = c_pattern_d[4 * t + 3];
-      const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
-      const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
-      const uint64_t b = __ballot(bc[o0] < bc[o1]);
-      words[r] = half ? (uint32_t)(b >> 32) : (uint32_t)b;
-    }
+  uint32_t w = 0u;   // lane hl keeps test word hl of its half's descriptor
+  for (int r = 0; r < nw; r++) {
+    const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
+    const double px0 = c_pattern_d[4 * t], py0 = c_pattern_d[4 * t + 1];
+    const double px1 = c_pattern_d[4 * t + 2], py1 = c_pattern_d[4 * t + 3];
+    const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
+    const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
+    const uint64_t b = __ballot(bc[o0] < bc[o1]);
+    if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
   }
-  if (valid && hl < nw) {
-    uint32_t w = words[0];
-#pragma unroll
-    for (int r = 1; r < 16; r++)
-      if (hl == r) w = words[r];
+  if (valid && hl < nw)
     reinterpret_cast<uint32_t*>(a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size)[hl] = w;
-  }
   if (valid && hl == 0) {
     mcs_keypoint kp;
     kp.x = (float)cx; kp.y = (float)cy;
