@@ -91,6 +91,67 @@ int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* 
                  uint8_t* edge_inlier, int32_t* write_back, volatile int32_t* stop_flag,
                  mcs_ba_report* rep_round1, mcs_ba_report* rep_round2);
 
+/* mcs_local_ba with the reference's point bookkeeping (src/cOptimizer.cpp:798-903,
+ * cMapPoint::EraseObservation src/cMapPoint.cpp:120-152, TotalNrObservations :166-178):
+ * both culling passes walk the edges in order and skip edges of a point that has turned bad;
+ * erasing an observation turns its point bad once fewer than 2 observations remain,
+ * counting point_extra_obs[i] observations of point i from bad keyframes (edges exist only for
+ * good keyframes; nullable = 0).  Edges of a point that turned bad stay active in round 2, as in
+ * the reference.  point_write[i] (out) = the point is written back: write_back, not bad, more
+ * than one remaining observation from good keyframes and >= 2 edges (:885-902). */
+int mcs_local_ba_ex(mcs_ba_ctx* c, const mcs_ba_problem* p, const int32_t* point_extra_obs,
+                    double* poses, double* points, uint8_t* edge_inlier, uint8_t* point_write,
+                    int32_t* write_back, volatile int32_t* stop_flag, mcs_ba_report* rep_round1,
+                    mcs_ba_report* rep_round2);
+
+/* ---- LocalBundleAdjustment graph assembly (src/cOptimizer.cpp:503-769) ---------------------
+ * The map as flat arrays (indices, not pointers).  Observation order per point is the
+ * reference's std::map<cMultiKeyFrame*, vector<size_t>> iteration order (keyframe, then the
+ * image points of that keyframe); map-point matches per keyframe are GetMapPointMatches(). */
+typedef struct mcs_lba_map {
+  int32_t n_kf;
+  const int64_t* kf_id;       /* [n_kf] mnId */
+  const uint8_t* kf_bad;      /* [n_kf] isBad() */
+  const int32_t* kf_mp_off;   /* [n_kf + 1] CSR offsets into kf_mp */
+  const int32_t* kf_mp;       /* map point matches (point index, -1 = NULL) */
+  int32_t n_points;
+  const uint8_t* pt_bad;      /* [n_points] isBad() */
+  const int32_t* pt_obs_off;  /* [n_points + 1] CSR offsets into obs_kf */
+  const int32_t* obs_kf;      /* observing keyframe of every observation */
+} mcs_lba_map;
+
+/* Outputs (caller-allocated arrays, counts written back).  Pose slots: the local keyframes
+ * first (pKF, then its covisibles in order), then the fixed keyframes. */
+typedef struct mcs_lba_graph {
+  int32_t* local_kf;          /* [n_kf] */
+  int32_t n_local;
+  int32_t* fixed_kf;          /* [n_kf] */
+  int32_t n_fixed;
+  uint8_t* pose_fixed;        /* [n_kf] per pose slot: setFixed of the vertex */
+  int32_t* points;            /* [n_points] local map points (vertex order) */
+  int32_t n_points;
+  int32_t* point_extra_obs;   /* [n_points] per local point: observations from bad keyframes */
+  int32_t* edge_obs;          /* [edge_cap] observation index of every edge (vpEdges order) */
+  int32_t* edge_pose;         /* [edge_cap] pose slot */
+  int32_t* edge_point;        /* [edge_cap] local point slot */
+  int32_t n_edges;
+  int32_t edge_cap;
+} mcs_lba_graph;
+
+/* Local keyframes = pKF + every non-bad covisible keyframe (GetVectorCovisibleKeyFrames order,
+ * :503-517); local points = first appearance over their map-point matches, non-bad (:521-537);
+ * fixed keyframes = observers of local points that are neither local (bad covisibles count as
+ * local) nor already fixed, non-bad (:540-558); vertex fixed flags follow the reference exactly:
+ * a local keyframe is fixed iff mnId == 0, and `oneFixed` keeps only the LAST local keyframe's
+ * test, so when that is false and there is no fixed keyframe pKF is fixed too (:585-612); one
+ * edge per observation of a local point from a non-bad keyframe (:688-766).  cur_kf = pKF.
+ * Returns MCS_OK, MCS_LBA_EMPTY when there is at most one local keyframe (the reference
+ * returns without optimising, :519-520), or MCS_ERR_CAPACITY (n_edges > edge_cap; counts are
+ * still written). */
+#define MCS_LBA_EMPTY 1
+int mcs_local_ba_select(const mcs_lba_map* m, int32_t cur_kf, const int32_t* covis,
+                        int32_t n_covis, mcs_lba_graph* g);
+
 /* cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) after graph construction:
  * p->n_poses == 1 (the frame's M_t, optimised; pose_fixed is ignored), every map point fixed
  * (:382), Mc / IO fixed, Huber delta = p->huber_delta (1.345 * huberMultiplier, :344),

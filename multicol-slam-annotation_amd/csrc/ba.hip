@@ -1055,15 +1055,24 @@ int mcs_global_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, int32_t pose_only, dou
   return optimize_impl(c, p, &o, poses, points, nullptr, nullptr, stop_flag, rep, shard, pose_only != 0);
 }
 
-int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* points,
-                 uint8_t* edge_inlier, int32_t* write_back, volatile int32_t* stop_flag,
-                 mcs_ba_report* r1, mcs_ba_report* r2) {
+int mcs_local_ba_ex(mcs_ba_ctx* c, const mcs_ba_problem* p, const int32_t* point_extra_obs,
+                    double* poses, double* points, uint8_t* edge_inlier, uint8_t* point_write,
+                    int32_t* write_back, volatile int32_t* stop_flag, mcs_ba_report* r1,
+                    mcs_ba_report* r2) {
   if (!c || !p || !poses || !points || !edge_inlier || !write_back) return MCS_ERR_ARG;
   mcs_ba_options o;
   mcs_ba_default_options(&o);
   const double huberK2 = p->huber_delta * p->huber_delta;
   std::vector<uint8_t> level(p->n_edges, 0);
   std::vector<double> chi(p->n_edges);
+  // cMapPoint bookkeeping: observations left (good-keyframe edges + observations from bad
+  // keyframes) and the bad flag EraseObservation raises below two (src/cMapPoint.cpp:120-152)
+  std::vector<int32_t> obs_left(p->n_points, 0), edges_left(p->n_points, 0);
+  std::vector<uint8_t> pt_bad(p->n_points, 0);
+  for (int e = 0; e < p->n_edges; e++) edges_left[p->edge_point[e]]++;
+  for (int i = 0; i < p->n_points; i++)
+    obs_left[i] = edges_left[i] + (point_extra_obs ? point_extra_obs[i] : 0);
+  if (point_write) std::memset(point_write, 0, (size_t)p->n_points);
   // pbStopFlag == NULL: the terminate action raises its own auxiliary flag and g2o keeps it
   // installed as the force-stop flag, so a round 1 that converged leaves round 2 with zero
   // iterations (sparse_optimizer_terminate_action.cpp:64-72, sparse_optimizer.cpp:376)
@@ -1075,22 +1084,44 @@ int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* 
   *write_back = 0;
   for (int e = 0; e < p->n_edges; e++) edge_inlier[e] = 1;
   if (stop_flag && *stop_flag) return MCS_OK;               // :771-773
+  // culling pass (:798-817, :830-849): edges in vpEdges order, a bad point's edges skipped
+  auto cull = [&](bool disable) {
+    for (int e = 0; e < p->n_edges; e++) {
+      const int pt = p->edge_point[e];
+      if (!edge_inlier[e] || pt_bad[pt] || !(chi[e] > huberK2)) continue;
+      edge_inlier[e] = 0;
+      if (disable) level[e] = 1;
+      edges_left[pt]--;
+      if (--obs_left[pt] < 2) pt_bad[pt] = 1;
+    }
+  };
   o.max_iterations = 10;
   int rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r1);
   if (rc) return rc;
   // optimize() returns -1 == OptimizationAlgorithm::Fail only for an empty active graph
   if (r1->n_active_poses + r1->n_active_points == 0) return MCS_OK;   // :784-788
   if (stop_flag && *stop_flag) return MCS_OK;               // bDoMore = false (:790-794)
-  for (int e = 0; e < p->n_edges; e++)                      // :798-817
-    if (chi[e] > huberK2) { level[e] = 1; edge_inlier[e] = 0; }
+  cull(true);
   o.max_iterations = 15;                                    // :819-820
   rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r2);
   if (rc) return rc;
   if (r2->n_active_poses + r2->n_active_points == 0) return MCS_OK;   // :822-826
-  for (int e = 0; e < p->n_edges; e++)                      // :830-849
-    if (edge_inlier[e] && chi[e] > huberK2) edge_inlier[e] = 0;
+  cull(false);
   *write_back = 1;
+  if (point_write) {   // :885-902: not bad, TotalNrObservations() > 1, >= 2 vertex edges
+    std::vector<int32_t> edges_all(p->n_points, 0);
+    for (int e = 0; e < p->n_edges; e++) edges_all[p->edge_point[e]]++;
+    for (int i = 0; i < p->n_points; i++)
+      point_write[i] = !pt_bad[i] && edges_left[i] > 1 && edges_all[i] >= 2;
+  }
   return MCS_OK;
+}
+
+int mcs_local_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, double* poses, double* points,
+                 uint8_t* edge_inlier, int32_t* write_back, volatile int32_t* stop_flag,
+                 mcs_ba_report* r1, mcs_ba_report* r2) {
+  return mcs_local_ba_ex(c, p, nullptr, poses, points, edge_inlier, nullptr, write_back, stop_flag,
+                         r1, r2);
 }
 
 int mcs_pose_optimization(mcs_ba_ctx* c, const mcs_ba_problem* p, double* pose, uint8_t* outlier,

@@ -228,6 +228,145 @@ def make_pose_problem(seed=0, n_points=1500, target_edges=5000, outlier_frac=0.0
 
 
 # ---------------------------------------------------------------------------
+# LocalBundleAdjustment graph assembly (mcs_local_ba_select, src/cOptimizer.cpp:503-769)
+# ---------------------------------------------------------------------------
+class LbaMap(ctypes.Structure):
+    _fields_ = [("n_kf", ctypes.c_int32), ("kf_id", ctypes.c_void_p), ("kf_bad", ctypes.c_void_p),
+                ("kf_mp_off", ctypes.c_void_p), ("kf_mp", ctypes.c_void_p),
+                ("n_points", ctypes.c_int32), ("pt_bad", ctypes.c_void_p),
+                ("pt_obs_off", ctypes.c_void_p), ("obs_kf", ctypes.c_void_p)]
+
+
+class LbaGraph(ctypes.Structure):
+    _fields_ = [("local_kf", ctypes.c_void_p), ("n_local", ctypes.c_int32),
+                ("fixed_kf", ctypes.c_void_p), ("n_fixed", ctypes.c_int32),
+                ("pose_fixed", ctypes.c_void_p), ("points", ctypes.c_void_p),
+                ("n_points", ctypes.c_int32), ("point_extra_obs", ctypes.c_void_p),
+                ("edge_obs", ctypes.c_void_p), ("edge_pose", ctypes.c_void_p),
+                ("edge_point", ctypes.c_void_p), ("n_edges", ctypes.c_int32),
+                ("edge_cap", ctypes.c_int32)]
+
+
+MCS_LBA_EMPTY = 1
+
+
+def lba_map_struct(m):
+    """numpy map dict (make_map) -> LbaMap (arrays kept alive in the dict)."""
+    for k, dt in (("kf_id", np.int64), ("kf_bad", np.uint8), ("kf_mp_off", np.int32),
+                  ("kf_mp", np.int32), ("pt_bad", np.uint8), ("pt_obs_off", np.int32),
+                  ("obs_kf", np.int32)):
+        m[k] = np.ascontiguousarray(m[k], dt)
+    return LbaMap(len(m["kf_id"]), _p(m["kf_id"]), _p(m["kf_bad"]), _p(m["kf_mp_off"]),
+                  _p(m["kf_mp"]), len(m["pt_bad"]), _p(m["pt_bad"]), _p(m["pt_obs_off"]),
+                  _p(m["obs_kf"]))
+
+
+def lba_graph_buffers(m):
+    nk, npt, nobs = len(m["kf_id"]), len(m["pt_bad"]), len(m["obs_kf"])
+    b = dict(local_kf=np.zeros(nk, np.int32), fixed_kf=np.zeros(nk, np.int32),
+             pose_fixed=np.zeros(nk, np.uint8), points=np.zeros(npt, np.int32),
+             point_extra_obs=np.zeros(npt, np.int32), edge_obs=np.zeros(max(1, nobs), np.int32),
+             edge_pose=np.zeros(max(1, nobs), np.int32), edge_point=np.zeros(max(1, nobs), np.int32))
+    g = LbaGraph(_p(b["local_kf"]), 0, _p(b["fixed_kf"]), 0, _p(b["pose_fixed"]), _p(b["points"]),
+                 0, _p(b["point_extra_obs"]), _p(b["edge_obs"]), _p(b["edge_pose"]),
+                 _p(b["edge_point"]), 0, nobs)
+    return g, b
+
+
+def lba_graph_result(rc, g, b):
+    nl, nf, npt, ne = g.n_local, g.n_fixed, g.n_points, g.n_edges
+    return dict(status=rc, local_kf=b["local_kf"][:nl].copy(), fixed_kf=b["fixed_kf"][:nf].copy(),
+                pose_fixed=b["pose_fixed"][:nl + nf].copy(), points=b["points"][:npt].copy(),
+                point_extra_obs=b["point_extra_obs"][:npt].copy(),
+                edge_obs=b["edge_obs"][:ne].copy(), edge_pose=b["edge_pose"][:ne].copy(),
+                edge_point=b["edge_point"][:ne].copy())
+
+
+def local_ba_select(m, cur, covis):
+    """mcs_local_ba_select: local / fixed keyframes, local points and edges of
+    LocalBundleAdjustment for keyframe `cur` with covisibles `covis` (ordered)."""
+    from . import lib
+    st = lba_map_struct(m)
+    cv = np.ascontiguousarray(covis, np.int32)
+    g, b = lba_graph_buffers(m)
+    rc = lib().mcs_local_ba_select(ctypes.byref(st), int(cur), _p(cv), len(cv), ctypes.byref(g))
+    if rc < 0:
+        from . import McsError, lib as _l
+        raise McsError(rc, _l().mcs_last_error().decode())
+    return lba_graph_result(rc, g, b)
+
+
+def problem_from_graph(m, g, huber_delta=1.345 * 2):
+    """mcs_ba_problem of one LocalBundleAdjustment call (vertices :585-711, edges :712-766):
+    pose slots = local then fixed keyframes, points = local points, one edge per selected
+    observation (measurement kp.pt, information invSigma2(octave))."""
+    slots = np.concatenate([g["local_kf"], g["fixed_kf"]]).astype(np.int64)
+    o = g["edge_obs"]
+    return dict(poses=m["kf_pose"][slots].copy(), pose_fixed=g["pose_fixed"].copy(),
+                points=m["pt_pos"][g["points"]].copy(), mc=m["mc"], cam=m["cam"],
+                edge_pose=g["edge_pose"].astype(np.int32), edge_point=g["edge_point"].astype(np.int32),
+                edge_cam=m["obs_cam"][o].astype(np.int32), edge_meas=m["obs_meas"][o].copy(),
+                edge_info=m["obs_info"][o].copy(), huber_delta=huber_delta)
+
+
+def make_map(n_kf=16, n_points=2500, target_edges=14000, seed=0, bad_kf=(), bad_points=0.01,
+             zero_id_kf=None, unmatched_frac=0.1, covis_th=15):
+    """Synthetic MultiKeyFrame map for LocalBundleAdjustment assembly: keyframes with mnId,
+    isBad, map-point matches (with NULL entries), points with isBad and observations in
+    keyframe order (the std::map iteration order of the reference with pointer order taken as
+    keyframe order).  Geometry and observations from make_problem.  Returns the map dict;
+    covisibles(m, k) gives GetVectorCovisibleKeyFrames (shared >= covis_th, weight order)."""
+    rng = np.random.default_rng(seed + 17)
+    pr = make_problem(n_local=n_kf, n_fixed=0, n_points=n_points, target_edges=target_edges,
+                      seed=seed)
+    nk, npt = len(pr["poses"]), len(pr["points"])
+    ids = np.sort(rng.choice(np.arange(1, 10 * nk), nk, replace=False)).astype(np.int64)
+    if zero_id_kf is not None:
+        ids[zero_id_kf] = 0
+    kf_bad = np.zeros(nk, np.uint8)
+    kf_bad[list(bad_kf)] = 1
+    pt_bad = (rng.random(npt) < bad_points).astype(np.uint8)
+    order = np.lexsort((np.arange(len(pr["edge_pose"])), pr["edge_pose"], pr["edge_point"]))
+    e_kf, e_pt = pr["edge_pose"][order], pr["edge_point"][order]
+    obs_kf = e_kf.astype(np.int32)
+    pt_obs_off = np.zeros(npt + 1, np.int32)
+    np.add.at(pt_obs_off, e_pt + 1, 1)
+    pt_obs_off = np.cumsum(pt_obs_off).astype(np.int32)
+    # keyframe map-point matches: each observation is a keypoint of its keyframe, plus NULLs
+    kf_lists = [[] for _ in range(nk)]
+    for k, p in zip(e_kf, e_pt):
+        kf_lists[k].append(int(p))
+    kf_mp, kf_mp_off = [], [0]
+    for k in range(nk):
+        lst = kf_lists[k] + [-1] * int(unmatched_frac * len(kf_lists[k]))
+        rng.shuffle(lst)
+        kf_mp += lst
+        kf_mp_off.append(len(kf_mp))
+    return dict(kf_id=ids, kf_bad=kf_bad, kf_mp_off=np.array(kf_mp_off, np.int32),
+                kf_mp=np.array(kf_mp, np.int32), pt_bad=pt_bad, pt_obs_off=pt_obs_off,
+                obs_kf=obs_kf, obs_cam=pr["edge_cam"][order], obs_meas=pr["edge_meas"][order],
+                obs_info=pr["edge_info"][order], kf_pose=pr["poses"], pt_pos=pr["points"],
+                mc=pr["mc"], cam=pr["cam"], covis_th=covis_th)
+
+
+def covisibles(m, k):
+    """GetVectorCovisibleKeyFrames of keyframe k: keyframes sharing >= covis_th good map
+    points, by decreasing weight (ties by index)."""
+    nk = len(m["kf_id"])
+    w = np.zeros(nk, np.int64)
+    for p in range(len(m["pt_bad"])):
+        if m["pt_bad"][p]:
+            continue
+        ks = set(m["obs_kf"][m["pt_obs_off"][p]:m["pt_obs_off"][p + 1]].tolist())
+        if k in ks:
+            for j in ks:
+                if j != k:
+                    w[j] += 1
+    cand = [j for j in range(nk) if w[j] >= m["covis_th"]]
+    return np.array(sorted(cand, key=lambda j: (-w[j], j)), np.int32)
+
+
+# ---------------------------------------------------------------------------
 # GPU solver binding
 # ---------------------------------------------------------------------------
 class Solver:
@@ -269,6 +408,28 @@ class Solver:
                                          ctypes.byref(rep)))
         return dict(poses=poses, points=points, edge_chi2=chi, report=rep,
                     stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
+
+    def local_ba_ex(self, pr, extra_obs=None, stop_flag=0):
+        """mcs_local_ba_ex: LocalBA rounds with the map-point bookkeeping (bad points, write-back
+        mask).  extra_obs: observations of each point from bad keyframes (or None)."""
+        from . import _check
+        s = as_struct(pr)
+        poses = pr["poses"].copy()
+        points = pr["points"].copy()
+        n = len(pr["edge_pose"])
+        inl = np.zeros(max(1, n), np.uint8)
+        pw = np.zeros(max(1, len(points)), np.uint8)
+        ex = None if extra_obs is None else np.ascontiguousarray(extra_obs, np.int32)
+        wb = ctypes.c_int32()
+        sf = None if stop_flag is None else ctypes.c_int32(int(stop_flag))
+        r1, r2 = BAReport(), BAReport()
+        _check(self._lib.mcs_local_ba_ex(self._h, ctypes.byref(s), None if ex is None else _p(ex),
+                                         _p(poses), _p(points), _p(inl), _p(pw), ctypes.byref(wb),
+                                         None if sf is None else ctypes.byref(sf),
+                                         ctypes.byref(r1), ctypes.byref(r2)))
+        return dict(poses=poses, points=points, edge_inlier=inl[:n].copy(),
+                    point_write=pw[:len(points)].copy(), write_back=wb.value,
+                    stop_flag=None if sf is None else sf.value, report1=r1, report2=r2)
 
     def local_ba(self, pr, stop_flag=0):
         """mcs_local_ba; stop_flag None = pbStopFlag NULL (g2o's auxiliary terminate flag)."""

@@ -28,6 +28,8 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <list>
+#include <map>
 #include <vector>
 
 #include "../include/mcs_ba.h"
@@ -644,15 +646,32 @@ int oracle_ba_partial_schur(const mcs_ba_problem* p, const double* pose_cnt, dou
   return n;
 }
 
-// cOptimizer::LocalBundleAdjustment (src/cOptimizer.cpp:771-903) after graph construction
-int oracle_local_ba(const mcs_ba_problem* p, double* poses, double* points, uint8_t* edge_inlier,
-                    int32_t* write_back, int32_t* stop_flag, mcs_ba_report* r1, mcs_ba_report* r2) {
+// cOptimizer::LocalBundleAdjustment (src/cOptimizer.cpp:771-903) after graph construction,
+// with cMapPoint's bookkeeping: EraseObservation (src/cMapPoint.cpp:120-152) turns a point
+// bad below 2 observations (extra_obs = observations from bad keyframes, which have no
+// edge), the culling loops skip bad points (:805-806, :836-837), the write-back needs a good
+// point with TotalNrObservations() > 1 (:166-178, :885-887) and >= 2 vertex edges (:895).
+int oracle_local_ba_ex(const mcs_ba_problem* p, const int32_t* extra_obs, double* poses,
+                       double* points, uint8_t* edge_inlier, uint8_t* point_write,
+                       int32_t* write_back, int32_t* stop_flag, mcs_ba_report* r1,
+                       mcs_ba_report* r2) {
   mcs_ba_options o;
   o.max_iterations = 10; o.gain_threshold = 1e-6; o.terminate_max_iter = 15; o.max_trials = 10;
   o.tau = 1e-5;
   const double huberK2 = p->huber_delta * p->huber_delta;
   std::vector<uint8_t> level(p->n_edges, 0);
   std::vector<double> chi(p->n_edges);
+  // per map point: its observation lists as the reference keeps them
+  struct MP { int good_obs; int bad_kf_obs; bool bad; int vertex_edges; };
+  std::vector<MP> mp(p->n_points);
+  for (int i = 0; i < p->n_points; i++) mp[i] = MP{0, extra_obs ? extra_obs[i] : 0, false, 0};
+  for (int e = 0; e < p->n_edges; e++) { mp[p->edge_point[e]].good_obs++; mp[p->edge_point[e]].vertex_edges++; }
+  auto erase_observation = [&](int i) {          // cMapPoint::EraseObservation
+    MP& m = mp[i];
+    m.good_obs--;
+    const int nrObs = m.good_obs + m.bad_kf_obs;
+    if (nrObs < 2) m.bad = true;                   // SetBadFlag (observations cleared)
+  };
   // pbStopFlag == NULL: g2o installs the terminate action's auxiliary flag as the force-stop
   // flag the first time the action stops (sparse_optimizer_terminate_action.cpp:64-72) and
   // nothing resets it, so it is shared by both rounds
@@ -662,21 +681,115 @@ int oracle_local_ba(const mcs_ba_problem* p, double* poses, double* points, uint
   if (!r1) r1 = &t1;
   if (!r2) r2 = &t2;
   *write_back = 0;
+  if (point_write) std::memset(point_write, 0, (size_t)p->n_points);
+  std::vector<char> vpEdges(p->n_edges, 1);      // NULL once an observation is erased
   for (int e = 0; e < p->n_edges; e++) edge_inlier[e] = 1;
   if (stop_flag && *stop_flag) return 0;
   oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), sf, r1);
   // optimize() == -1 == OptimizationAlgorithm::Fail: empty active graph (:784-788)
   if (r1->n_active_poses + r1->n_active_points == 0) return 0;
   if (stop_flag && *stop_flag) return 0;   // bDoMore = false: no culling, no write-back
-  for (int e = 0; e < p->n_edges; e++)
-    if (chi[e] > huberK2) { level[e] = 1; edge_inlier[e] = 0; }
+  for (int e = 0; e < p->n_edges; e++) {          // :798-817
+    if (mp[p->edge_point[e]].bad) continue;
+    if (chi[e] > huberK2) {
+      erase_observation(p->edge_point[e]);
+      level[e] = 1;
+      vpEdges[e] = 0;
+      edge_inlier[e] = 0;
+    }
+  }
   o.max_iterations = 15;
   oracle_ba_optimize(p, &o, poses, points, level.data(), chi.data(), sf, r2);
   if (r2->n_active_poses + r2->n_active_points == 0) return 0;   // :822-826
-  for (int e = 0; e < p->n_edges; e++)
-    if (edge_inlier[e] && chi[e] > huberK2) edge_inlier[e] = 0;
+  for (int e = 0; e < p->n_edges; e++) {          // :830-849
+    if (!vpEdges[e]) continue;
+    if (mp[p->edge_point[e]].bad) continue;
+    if (chi[e] > huberK2) {
+      erase_observation(p->edge_point[e]);
+      vpEdges[e] = 0;
+      edge_inlier[e] = 0;
+    }
+  }
   *write_back = 1;
+  if (point_write)                                 // :874-902
+    for (int i = 0; i < p->n_points; i++)
+      point_write[i] = !mp[i].bad && mp[i].good_obs > 1 && mp[i].vertex_edges >= 2;
   return 0;
+}
+
+int oracle_local_ba(const mcs_ba_problem* p, double* poses, double* points, uint8_t* edge_inlier,
+                    int32_t* write_back, int32_t* stop_flag, mcs_ba_report* r1, mcs_ba_report* r2) {
+  return oracle_local_ba_ex(p, nullptr, poses, points, edge_inlier, nullptr, write_back, stop_flag,
+                            r1, r2);
+}
+
+// Local keyframe / point / fixed keyframe selection and edge list of LocalBundleAdjustment
+// (src/cOptimizer.cpp:503-769), restated with the reference's containers and marks
+// (std::list, mnBALocalForKF / mnBAFixedForKF) over index arrays.  Same outputs as
+// mcs_local_ba_select (include/mcs_ba.h).  Returns 0, 1 (<= 1 local keyframe) or -2.
+int oracle_local_ba_select(const mcs_lba_map* m, int32_t cur, const int32_t* covis, int32_t n_covis,
+                           mcs_lba_graph* g) {
+  const long long pKF_id = m->kf_id[cur] + 1000000007LL;   // a mark value no keyframe holds yet
+  std::vector<long long> mnBALocalForKF(m->n_kf, -1), mnBAFixedForKF(m->n_kf, -1);
+  std::vector<long long> mpLocal(m->n_points, -1);
+  std::list<int> lLocalKeyFrames;
+  lLocalKeyFrames.push_back(cur);
+  mnBALocalForKF[cur] = pKF_id;
+  for (int i = 0; i < n_covis; i++) {
+    const int k = covis[i];
+    mnBALocalForKF[k] = pKF_id;
+    if (!m->kf_bad[k]) lLocalKeyFrames.push_back(k);
+  }
+  g->n_local = g->n_fixed = g->n_points = g->n_edges = 0;
+  for (int k : lLocalKeyFrames) g->local_kf[g->n_local++] = k;
+  if (lLocalKeyFrames.size() <= 1) return 1;
+  std::list<int> lLocalMapPoints;
+  for (int k : lLocalKeyFrames)
+    for (int q = m->kf_mp_off[k]; q < m->kf_mp_off[k + 1]; q++) {
+      const int pMP = m->kf_mp[q];
+      if (pMP >= 0)
+        if (!m->pt_bad[pMP])
+          if (mpLocal[pMP] != pKF_id) { lLocalMapPoints.push_back(pMP); mpLocal[pMP] = pKF_id; }
+    }
+  std::list<int> lFixedCameras;
+  for (int pMP : lLocalMapPoints)
+    for (int o = m->pt_obs_off[pMP]; o < m->pt_obs_off[pMP + 1]; o++) {
+      const int k = m->obs_kf[o];
+      if (mnBALocalForKF[k] != pKF_id && mnBAFixedForKF[k] != pKF_id) {
+        mnBAFixedForKF[k] = pKF_id;
+        if (!m->kf_bad[k]) lFixedCameras.push_back(k);
+      }
+    }
+  std::map<int, int> vertex;   // keyframe -> pose slot (g2o vertex of id mnId)
+  bool oneFixed = false;
+  int slot = 0;
+  for (int k : lLocalKeyFrames) {
+    oneFixed = m->kf_id[k] == 0;
+    g->pose_fixed[slot] = oneFixed;
+    vertex[k] = slot++;
+  }
+  if (!oneFixed && lFixedCameras.size() == 0) g->pose_fixed[vertex[*lLocalKeyFrames.begin()]] = 1;
+  for (int k : lFixedCameras) {
+    g->fixed_kf[g->n_fixed++] = k;
+    g->pose_fixed[slot] = 1;
+    vertex[k] = slot++;
+  }
+  int ne = 0, ip = 0;
+  for (int pMP : lLocalMapPoints) {
+    if (m->pt_bad[pMP]) continue;
+    g->points[g->n_points] = pMP;
+    int extra = 0;
+    for (int o = m->pt_obs_off[pMP]; o < m->pt_obs_off[pMP + 1]; o++) {
+      const int k = m->obs_kf[o];
+      if (m->kf_bad[k]) { extra++; continue; }
+      if (ne < g->edge_cap) { g->edge_obs[ne] = o; g->edge_pose[ne] = vertex[k]; g->edge_point[ne] = ip; }
+      ne++;
+    }
+    g->point_extra_obs[g->n_points++] = extra;
+    ip++;
+  }
+  g->n_edges = ne;
+  return ne > g->edge_cap ? -2 : 0;
 }
 
 // cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) after graph construction: one pose

@@ -215,7 +215,8 @@ def _ba_sigs():
     L = lib()
     for n, a in (("oracle_ba_edge", [_P] * 8),
                  ("oracle_ba_optimize", [_P] * 8),
-                 ("oracle_local_ba", [_P] * 8)):
+                 ("oracle_local_ba", [_P] * 8),
+                 ("oracle_local_ba_ex", [_P] * 10)):
         f = getattr(L, n)
         f.restype = _I
         f.argtypes = a
@@ -268,6 +269,44 @@ def local_ba(pr, stop_flag=0):
                       None if sf is None else C.byref(sf), C.byref(r1), C.byref(r2))
     return dict(poses=poses, points=points, edge_inlier=inl, write_back=wb.value,
                 stop_flag=None if sf is None else sf.value, report1=r1, report2=r2)
+
+
+def local_ba_ex(pr, extra_obs=None, stop_flag=0):
+    """oracle_local_ba_ex: LocalBA rounds with cMapPoint bookkeeping (restatement)."""
+    import ctypes as C
+    from mcs_amd import ba
+    L = _ba_sigs()
+    s = ba.as_struct(pr)
+    poses = pr["poses"].copy()
+    points = pr["points"].copy()
+    n = len(pr["edge_pose"])
+    inl = np.zeros(max(1, n), np.uint8)
+    pw = np.zeros(max(1, len(points)), np.uint8)
+    ex = None if extra_obs is None else np.ascontiguousarray(extra_obs, np.int32)
+    wb = C.c_int32()
+    sf = None if stop_flag is None else C.c_int32(int(stop_flag))
+    r1, r2 = ba.BAReport(), ba.BAReport()
+    L.oracle_local_ba_ex(C.byref(s), None if ex is None else _p(ex), _p(poses), _p(points),
+                         _p(inl), _p(pw), C.byref(wb), None if sf is None else C.byref(sf),
+                         C.byref(r1), C.byref(r2))
+    return dict(poses=poses, points=points, edge_inlier=inl[:n].copy(),
+                point_write=pw[:len(points)].copy(), write_back=wb.value,
+                stop_flag=None if sf is None else sf.value, report1=r1, report2=r2)
+
+
+def local_ba_select(m, cur, covis):
+    """oracle_local_ba_select (LocalBundleAdjustment assembly restated with std::list)."""
+    import ctypes as C
+    from mcs_amd import ba
+    L = lib()
+    f = L.oracle_local_ba_select
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+    st = ba.lba_map_struct(m)
+    cv = np.ascontiguousarray(covis, np.int32)
+    g, b = ba.lba_graph_buffers(m)
+    rc = f(C.byref(st), int(cur), _p(cv), len(cv), C.byref(g))
+    return ba.lba_graph_result(rc, g, b)
 
 
 def pose_optimization(pr, trace=0):

@@ -1,0 +1,155 @@
+"""LocalBundleAdjustment graph assembly and map-point bookkeeping.
+
+Reference: cOptimizer::LocalBundleAdjustment src/cOptimizer.cpp:503-769 (local / fixed keyframe
+selection, the `oneFixed` quirk :594-612, one edge per observation) and :798-903 (culling with
+cMapPoint::EraseObservation src/cMapPoint.cpp:120-152, write-back of points with more than one
+remaining observation and >= 2 edges).
+
+CPU: the product's mcs_local_ba_select equals the oracle restatement (std::list + marks) on
+synthetic maps, and hand-built maps pin each rule.  GPU: select -> mcs_local_ba_ex equals the
+oracle's select -> oracle_local_ba_ex: identical inlier / write-back sets, poses abs 1e-6,
+points with >= 3 observations abs 1e-5, 2-observation points abs 1e-3 (depth-ambiguous)."""
+import numpy as np
+import pytest
+
+from tests import oracle_bind as ob
+
+
+@pytest.fixture(scope="module")
+def bigmap():
+    from mcs_amd import ba
+    return ba.make_map(n_kf=24, n_points=3000, target_edges=18000, seed=5, bad_kf=(7, 20))
+
+
+def _same(g, o):
+    for k in g:
+        assert np.array_equal(np.asarray(g[k]), np.asarray(o[k])), k
+
+
+def _tiny_map(kf_id, kf_bad, kf_mp, pt_bad, pt_obs):
+    off = np.cumsum([0] + [len(x) for x in kf_mp]).astype(np.int32)
+    poff = np.cumsum([0] + [len(x) for x in pt_obs]).astype(np.int32)
+    return dict(kf_id=np.array(kf_id, np.int64), kf_bad=np.array(kf_bad, np.uint8),
+                kf_mp_off=off, kf_mp=np.array(sum(kf_mp, []), np.int32),
+                pt_bad=np.array(pt_bad, np.uint8), pt_obs_off=poff,
+                obs_kf=np.array(sum(pt_obs, []), np.int32))
+
+
+@pytest.mark.parametrize("ncov", [None, 3, 6, 10])
+def test_select_matches_oracle(built, bigmap, ncov):
+    from mcs_amd import ba
+    for cur in (23, 12, 3):
+        cv = ba.covisibles(bigmap, cur)
+        if ncov is not None:
+            cv = cv[:ncov]
+        g = ba.local_ba_select(bigmap, cur, cv)
+        o = ob.local_ba_select(bigmap, cur, cv)
+        _same(g, o)
+        if len(cv):
+            assert g["status"] == 0 and len(g["edge_obs"]) > 0
+
+
+def test_select_rules_by_hand(built):
+    """kf 0 = pKF; kf 1 covisible; kf 2 covisible but bad; kf 3 observer only; kf 4 bad observer.
+    points: 0 (kf0, kf1, kf3), 1 (kf1, kf2, kf4), 2 bad, 3 (kf2 only: not local)."""
+    from mcs_amd import ba
+    m = _tiny_map(kf_id=[40, 30, 20, 10, 5], kf_bad=[0, 0, 1, 0, 1],
+                  kf_mp=[[0, -1, 2], [1, 0], [1, 3], [0], [1]], pt_bad=[0, 0, 1, 0],
+                  pt_obs=[[0, 1, 3], [1, 2, 4], [0], [2]])
+    g = ba.local_ba_select(m, 0, [1, 2])
+    _same(g, ob.local_ba_select(m, 0, [1, 2]))
+    assert list(g["local_kf"]) == [0, 1]                 # bad covisible dropped
+    assert list(g["points"]) == [0, 1]                   # first appearance, bad point dropped
+    assert list(g["fixed_kf"]) == [3]                    # kf 2: local-marked; kf 4: bad
+    assert list(g["pose_fixed"]) == [0, 0, 1]            # fixed observer exists -> pKF free
+    assert list(g["point_extra_obs"]) == [0, 2]          # point 1 seen by bad kf 2 and kf 4
+    assert list(g["edge_obs"]) == [0, 1, 2, 3]           # bad-keyframe observations: no edge
+    assert list(g["edge_pose"]) == [0, 1, 2, 1]
+    # pKF = kf 1: kf 2 (bad, not covisible this time) and kf 4 are marked but not added,
+    # kf 3 observes point 0 and is the fixed observer, so pKF stays free
+    g2 = ba.local_ba_select(m, 1, [0])
+    _same(g2, ob.local_ba_select(m, 1, [0]))
+    assert list(g2["local_kf"]) == [1, 0] and list(g2["points"]) == [1, 0]
+    assert list(g2["fixed_kf"]) == [3] and list(g2["pose_fixed"]) == [0, 0, 1]
+    # single local keyframe: the reference returns without optimising
+    g3 = ba.local_ba_select(m, 3, [2])
+    assert g3["status"] == ba.MCS_LBA_EMPTY
+
+
+def test_one_fixed_quirk(built):
+    """`oneFixed` keeps only the LAST local keyframe's mnId == 0 test (:594)."""
+    from mcs_amd import ba
+    m = _tiny_map(kf_id=[7, 0, 9], kf_bad=[0, 0, 0], kf_mp=[[0], [0], [0]], pt_bad=[0],
+                  pt_obs=[[0, 1, 2]])
+    # mnId 0 is the last local keyframe: oneFixed, pKF stays free
+    g = ba.local_ba_select(m, 0, [2, 1])
+    _same(g, ob.local_ba_select(m, 0, [2, 1]))
+    assert list(g["pose_fixed"]) == [0, 0, 1]
+    # mnId 0 in the middle, no fixed observers: oneFixed is false -> pKF fixed as well
+    g = ba.local_ba_select(m, 0, [1, 2])
+    _same(g, ob.local_ba_select(m, 0, [1, 2]))
+    assert list(g["pose_fixed"]) == [1, 1, 0]
+    # no mnId 0 and no fixed observer: only pKF fixed
+    m["kf_id"] = np.array([7, 3, 9], np.int64)
+    g = ba.local_ba_select(m, 2, [0, 1])
+    assert list(g["pose_fixed"]) == [1, 0, 0]
+
+
+def test_select_capacity_error(built, bigmap):
+    from mcs_amd import ba, McsError
+    import ctypes
+    st = ba.lba_map_struct(bigmap)
+    g, b = ba.lba_graph_buffers(bigmap)
+    g.edge_cap = 10
+    cv = np.ascontiguousarray(ba.covisibles(bigmap, 23), np.int32)
+    from mcs_amd import lib
+    rc = lib().mcs_local_ba_select(ctypes.byref(st), 23, cv.ctypes.data_as(ctypes.c_void_p),
+                                   len(cv), ctypes.byref(g))
+    assert rc == -2 and g.n_edges > 10   # MCS_ERR_CAPACITY, count still reported
+
+
+def test_oracle_bookkeeping_two_observation_points(built):
+    """A 2-observation point losing one observation turns bad: its other edge is skipped by
+    the culling and it is not written back (oracle restatement on a crafted problem)."""
+    from mcs_amd import ba
+    pr = ba.make_problem(n_local=4, n_fixed=1, n_points=300, target_edges=1500, seed=9,
+                         outlier_frac=0.08)
+    o = ob.local_ba_ex(pr)
+    cnt = np.bincount(pr["edge_point"], minlength=len(pr["points"]))
+    erased = np.bincount(pr["edge_point"][o["edge_inlier"] == 0], minlength=len(pr["points"]))
+    assert o["write_back"] == 1
+    # a point whose erasures left < 2 observations is never written back
+    assert not np.any(o["point_write"] & (cnt - erased < 2))
+    # 2-observation points with both edges kept are written back
+    assert np.all(o["point_write"][(cnt == 2) & (erased == 0)] == 1)
+    # a 2-observation point never loses both edges: after the first it is bad and skipped
+    assert not np.any((cnt == 2) & (erased == 2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncov,stop", [(None, 0), (6, 0), (6, None)])
+def test_gpu_select_local_ba_matches_oracle(gpu, bigmap, ncov, stop):
+    from mcs_amd import ba
+    cur = 23
+    cv = ba.covisibles(bigmap, cur)
+    if ncov is not None:
+        cv = cv[:ncov]
+    g = ba.local_ba_select(bigmap, cur, cv)
+    _same(g, ob.local_ba_select(bigmap, cur, cv))
+    pr = ba.problem_from_graph(bigmap, g)
+    r = ba.Solver().local_ba_ex(pr, g["point_extra_obs"], stop_flag=stop)
+    o = ob.local_ba_ex(pr, g["point_extra_obs"], stop_flag=stop)
+    assert r["write_back"] == o["write_back"]
+    assert r["report1"].iterations == o["report1"].iterations
+    assert r["report2"].iterations == o["report2"].iterations
+    assert np.array_equal(r["edge_inlier"], o["edge_inlier"])
+    assert np.array_equal(r["point_write"], o["point_write"])
+    assert np.abs(r["poses"] - o["poses"]).max() < 1e-6
+    if not r["write_back"]:
+        return
+    cnt = np.bincount(pr["edge_point"], minlength=len(pr["points"]))
+    w3 = (r["point_write"] == 1) & (cnt >= 3)
+    w2 = (r["point_write"] == 1) & (cnt == 2)
+    assert np.abs(r["points"][w3] - o["points"][w3]).max() < 1e-5
+    if w2.any():
+        assert np.abs(r["points"][w2] - o["points"][w2]).max() < 1e-3
