@@ -115,6 +115,11 @@ SIGNATURES = {
     "mcs_ba_optimize": (ctypes.c_int, [_P] * 9),
     "mcs_local_ba": (ctypes.c_int, [_P] * 9),
     "mcs_local_ba_ex": (ctypes.c_int, [_P] * 11),
+    "mcs_keypoint_rays_device": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P, _P]),
+    "mcs_multiframe_concat_device": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _I32, _P,
+                                                    _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mcs_is_in_frustum_device": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _I32, _P, _P, _P,
+                                                _I32, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_local_ba_select": (ctypes.c_int, [_P, _I32, _P, _I32, _P]),
     "mcs_ba_linearize": (ctypes.c_int, [_P] * 5),
     "mcs_ba_xchg_doubles": (_I64, [_I32]),

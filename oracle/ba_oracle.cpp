@@ -847,4 +847,58 @@ int oracle_pose_optimization(const mcs_ba_problem* p, double* pose, uint8_t* out
   return N - nBad;
 }
 
+// cMultiFrame::isInFrustum (src/cMultiFrame.cpp:218-270) for every (point, camera): the
+// reference's 4x4 path (WorldToCamHom_fast, src/cam_system_omni.cpp:92-112), mirror-mask test
+// (src/cam_model_omni.cpp:165-180), distance invariance 0.8 / 1.2 (src/cMapPoint.cpp:498-508),
+// viewCos, lower_bound scale level.  Arrays as mcs_is_in_frustum_device (host memory).
+int oracle_is_in_frustum(const double* pose, const double* mc, const double* camv, int32_t C,
+                         const uint8_t* masks, int32_t mw, int32_t mh, const double* pts,
+                         const double* nrm, const double* dist, int32_t n, const double* scale,
+                         int32_t L, uint8_t* in_view, double* proj, int32_t* level,
+                         double* view_cos) {
+  for (int p = 0; p < n; p++)
+    for (int c = 0; c < C; c++) {
+      const long q = (long)p * C + c;
+      in_view[q] = 0;
+      double Mt[16], Mc[16], M[16], Mi[16];
+      cay2hom(pose, Mt);
+      cay2hom(mc + 6 * c, Mc);
+      mat44(Mt, Mc, M);
+      inv_mat(M, Mi);
+      const double* P = pts + 3 * p;
+      const double pt4[4] = {P[0], P[1], P[2], 1.0};
+      double r[4];
+      for (int i = 0; i < 4; i++) {
+        double s = 0;
+        for (int k = 0; k < 4; k++) s += Mi[4 * i + k] * pt4[k];
+        r[i] = s;
+      }
+      double u = 0.0, v = 0.0;
+      world_to_img(camv + 17 * c, r[0], r[1], r[2], u, v);
+      const int ur = (int)std::lrint(u), vr = (int)std::lrint(v);   // cvRound
+      if (ur >= mw || ur <= 0 || vr >= mh || vr <= 0) continue;
+      if (!(masks[(long)c * mw * mh + (long)vr * mw + ur] > 0)) continue;
+      const double maxDistance = 1.2 * dist[2 * p + 1];
+      const double minDistance = 0.8 * dist[2 * p];
+      const double PO[3] = {P[0] - M[3], P[1] - M[7], P[2] - M[11]};
+      double ss = 0;
+      for (int k = 0; k < 3; k++) ss += PO[k] * PO[k];
+      const double d = std::sqrt(ss);                                  // cv::norm
+      if (d < minDistance || d > maxDistance) continue;
+      const double* Pn = nrm + 3 * p;
+      double dot = 0;
+      for (int k = 0; k < 3; k++) dot += PO[k] * Pn[k];
+      const double viewCos = dot / d;
+      const double ratio = d / minDistance;
+      int lv = (int)(std::lower_bound(scale, scale + L, ratio) - scale);
+      if (lv >= L) lv = L - 1;
+      in_view[q] = 1;
+      proj[2 * q] = u;
+      proj[2 * q + 1] = v;
+      level[q] = lv;
+      view_cos[q] = viewCos;
+    }
+  return 0;
+}
+
 }  // extern "C"
