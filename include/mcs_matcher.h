@@ -64,6 +64,21 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
                                      int32_t th_low, double epi_thresh, int32_t* matches12,
                                      int32_t* n_matches);
 
+/* Same with mdBRIEF descriptor masks (cORBmatcher built with havingMasks = true, whose
+ * TH_LOW is floor(featDim), src/cORBmatcher.cpp:52-65): distances are
+ * DescriptorDistance64Masked(d1, d2, m1, m2) (src/cORBmatcher.cpp:1052-1056, 2457-2477).
+ * mask1 [n1][bytes], mask2 [n2][bytes] host, both required.  Both entries reject
+ * n2 >= 2^20 and cameras outside [0, ncams) with MCS_ERR_ARG. */
+int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t* mask1,
+                                            const int32_t* cam1, const uint8_t* has_mp1,
+                                            const double* rays1, int32_t n1,
+                                            const uint8_t* desc2, const uint8_t* mask2,
+                                            const int32_t* cam2, const uint8_t* has_mp2,
+                                            const double* rays2, int32_t n2, int32_t ncams,
+                                            const double* E, int32_t bytes, int32_t th_low,
+                                            double epi_thresh, int32_t* matches12,
+                                            int32_t* n_matches);
+
 /* ---- Projection-guided (windowed) matching -------------------------------------------
  * cMultiFrame feature grid (src/cMultiFrame.cpp:154-184, PosInGrid :342-353; 64 x 48 cells
  * per camera, include/cMultiFrame.h FRAME_GRID_COLS / FRAME_GRID_ROWS) and

@@ -292,32 +292,59 @@ __global__ __launch_bounds__(kHamThreads) void k_dense(const uint8_t* __restrict
   for (int j = 0; j < nt_tile; j++) D[(int64_t)qi * nb + t0 + j] = (uint16_t)ham_dist_v<W>(q, &tile[j * (W / 4)]);
 }
 
+// DescriptorDistance64Masked (src/cORBmatcher.cpp:2457-2477): (sum popc(x & m1) +
+// sum popc(x & m2)) / 2 over the whole descriptor, integer division of the total.
+template <int W>
+__device__ __forceinline__ int ham_dist_masked_v(const uint32_t (&q)[W], const uint32_t (&qm)[W],
+                                                 const uint4* t4, const uint4* m4) {
+  int d = 0;
+#pragma unroll
+  for (int w4 = 0; w4 < W / 4; w4++) {
+    const uint4 v = t4[w4], m = m4[w4];
+    const uint32_t x0 = q[4 * w4 + 0] ^ v.x, x1 = q[4 * w4 + 1] ^ v.y;
+    const uint32_t x2 = q[4 * w4 + 2] ^ v.z, x3 = q[4 * w4 + 3] ^ v.w;
+    d += __popc(x0 & qm[4 * w4 + 0]) + __popc(x0 & m.x);
+    d += __popc(x1 & qm[4 * w4 + 1]) + __popc(x1 & m.y);
+    d += __popc(x2 & qm[4 * w4 + 2]) + __popc(x2 & m.z);
+    d += __popc(x3 & qm[4 * w4 + 3]) + __popc(x3 & m.w);
+  }
+  return d >> 1;
+}
+
+template <int W>
+__device__ __forceinline__ void load_desc_row(uint32_t (&q)[W], const uint8_t* row) {
+  const uint4* qp = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+  for (int w4 = 0; w4 < W / 4; w4++) {
+    const uint4 v = qp[w4];
+    q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
+  }
+}
+
 // radius search for SearchForTriangulationRaw: candidates with dist <= th among trains of
 // the same camera without a map point.  pass 0 counts, pass 1 writes (dist<<20 | idx2).
-template <int W>
+// MASKED: mdBRIEF descriptor masks (havingMasks), DescriptorDistance64Masked.
+template <int W, bool MASKED>
 __global__ __launch_bounds__(kHamThreads) void k_radius(
-    const uint8_t* __restrict__ A, const int32_t* __restrict__ camA,
-    const uint8_t* __restrict__ hasA, int na, const uint8_t* __restrict__ B,
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA,
+    const int32_t* __restrict__ camA, const uint8_t* __restrict__ hasA, int na,
+    const uint8_t* __restrict__ B, const uint8_t* __restrict__ MB,
     const int32_t* __restrict__ camB, const uint8_t* __restrict__ hasB, int nb, int th,
     int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
     uint32_t* __restrict__ out) {
   __shared__ uint4 tile[kHamTile * (W / 4)];
+  __shared__ uint4 mtile[MASKED ? kHamTile * (W / 4) : 1];
   __shared__ int tcam[kHamTile];
   const int qi = blockIdx.x * kHamThreads + threadIdx.x;
-  uint32_t q[W];
+  uint32_t q[W], qm[W];
   int qc = -1;
   bool active = qi < na && !hasA[qi];
+#pragma unroll
+  for (int w = 0; w < W; w++) { q[w] = 0; qm[w] = 0; }
   if (qi < na) {
     qc = camA[qi];
-    const uint4* qp = reinterpret_cast<const uint4*>(A + (int64_t)qi * W * 4);
-#pragma unroll
-    for (int w4 = 0; w4 < W / 4; w4++) {
-      const uint4 v = qp[w4];
-      q[4 * w4] = v.x; q[4 * w4 + 1] = v.y; q[4 * w4 + 2] = v.z; q[4 * w4 + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int w = 0; w < W; w++) q[w] = 0;
+    load_desc_row<W>(q, A + (int64_t)qi * W * 4);
+    if (MASKED) load_desc_row<W>(qm, MA + (int64_t)qi * W * 4);
   }
   int cnt = 0;
   int pos = (offsets && qi < na) ? offsets[qi] : 0;
@@ -326,13 +353,18 @@ __global__ __launch_bounds__(kHamThreads) void k_radius(
     __syncthreads();
     const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
     for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
+    if (MASKED) {
+      const uint4* msrc = reinterpret_cast<const uint4*>(MB + (int64_t)t0 * W * 4);
+      for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) mtile[i] = msrc[i];
+    }
     for (int i = threadIdx.x; i < nt_tile; i += kHamThreads)
       tcam[i] = hasB[t0 + i] ? -2 : camB[t0 + i];
     __syncthreads();
     if (!active) continue;
     for (int j = 0; j < nt_tile; j++) {
       if (tcam[j] != qc) continue;
-      const int d = ham_dist_v<W>(q, &tile[j * (W / 4)]);
+      const int d = MASKED ? ham_dist_masked_v<W>(q, qm, &tile[j * (W / 4)], &mtile[j * (W / 4)])
+                           : ham_dist_v<W>(q, &tile[j * (W / 4)]);
       if (d <= th) {
         if (out) out[pos++] = ((uint32_t)d << 20) | (uint32_t)(t0 + j);
         cnt++;
@@ -438,26 +470,74 @@ int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts
   return MCS_OK;
 }
 
-int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
-                                     const uint8_t* has_mp1, const double* rays1, int32_t n1,
-                                     const uint8_t* desc2, const int32_t* cam2,
-                                     const uint8_t* has_mp2, const double* rays2, int32_t n2,
-                                     int32_t ncams, const double* E, int32_t bytes,
-                                     int32_t th_low, double epi_thresh, int32_t* matches12,
-                                     int32_t* n_matches) {
+}  // extern "C"
+
+namespace mcs {
+
+template <bool MASKED>
+static void launch_radius(int bytes, dim3 g, const uint8_t* dA, const uint8_t* dmA,
+                          const int32_t* dcA, const uint8_t* dhA, int n1, const uint8_t* dB,
+                          const uint8_t* dmB, const int32_t* dcB, const uint8_t* dhB, int n2,
+                          int th, int32_t* dcnt, const int32_t* doff, uint32_t* dout) {
+  if (bytes == 16)
+    hipLaunchKernelGGL((k_radius<4, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
+                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
+  else if (bytes == 32)
+    hipLaunchKernelGGL((k_radius<8, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
+                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
+  else
+    hipLaunchKernelGGL((k_radius<16, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
+                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
+}
+
+// CheckDistEpipolarLine (src/misc.cpp:54-70).  nom = (ray2^T E12) ray1 evaluated left to right
+// as cv::Matx does; (ray2^T E12)_c = sum_r ray2_r E_rc is exactly Etx2_c, so nom = Etx2 . ray1.
+static bool check_dist_epipolar_line(const double* r1, const double* r2, const double* Em,
+                                     double thresh) {
+  double Ex1[3], Etx2[3];
+  for (int r = 0; r < 3; r++) {
+    Ex1[r] = Em[3 * r] * r1[0] + Em[3 * r + 1] * r1[1] + Em[3 * r + 2] * r1[2];
+    Etx2[r] = r2[0] * Em[r] + r2[1] * Em[3 + r] + r2[2] * Em[6 + r];
+  }
+  const double nom = Etx2[0] * r1[0] + Etx2[1] * r1[1] + Etx2[2] * r1[2];
+  const double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
+                     Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
+  if (den == 0.0) return false;
+  return (nom * nom) / den < thresh;
+}
+
+static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
+                                    const int32_t* cam1, const uint8_t* has_mp1,
+                                    const double* rays1, int32_t n1, const uint8_t* desc2,
+                                    const uint8_t* mask2, const int32_t* cam2,
+                                    const uint8_t* has_mp2, const double* rays2, int32_t n2,
+                                    int32_t ncams, const double* E, int32_t bytes, int32_t th_low,
+                                    double epi_thresh, int32_t* matches12, int32_t* n_matches) {
   int rc = check_bytes(bytes);
   if (rc) return rc;
   if (!n_matches || (n1 > 0 && !matches12)) return MCS_ERR_ARG;
   *n_matches = 0;
   for (int i = 0; i < n1; i++) matches12[i] = -1;
   if (n1 <= 0 || n2 <= 0) return MCS_OK;
+  // candidates are packed (dist << 20 | idx2): train index must fit 20 bits
+  if (n2 >= (1 << 20)) { set_error("triangulation: at most 2^20 - 1 keypoints in KF2"); return MCS_ERR_ARG; }
+  if (!desc1 || !desc2 || !cam1 || !cam2 || !has_mp1 || !has_mp2 || !rays1 || !rays2 || !E ||
+      ncams <= 0)
+    return MCS_ERR_ARG;
+  const bool masked = mask1 != nullptr;
+  if (masked != (mask2 != nullptr)) { set_error("triangulation: masks for both keyframes or none"); return MCS_ERR_ARG; }
+  for (int i = 0; i < n1; i++)
+    if (cam1[i] < 0 || cam1[i] >= ncams) { set_error("triangulation: cam1 out of range"); return MCS_ERR_ARG; }
+  for (int i = 0; i < n2; i++)
+    if (cam2[i] < 0 || cam2[i] >= ncams) { set_error("triangulation: cam2 out of range"); return MCS_ERR_ARG; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     set_error("no HIP device visible (no CPU fallback)");
     return MCS_ERR_NO_DEVICE;
   }
   // ---- GPU: per-query candidate lists (same camera, no map point, dist <= th_low)
-  uint8_t *dA = nullptr, *dB = nullptr, *dhA = nullptr, *dhB = nullptr;
+  uint8_t *dA = nullptr, *dB = nullptr, *dmA = nullptr, *dmB = nullptr, *dhA = nullptr,
+          *dhB = nullptr;
   int32_t *dcA = nullptr, *dcB = nullptr, *dcnt = nullptr, *doff = nullptr;
   uint32_t* dout = nullptr;
   std::vector<int32_t> cnt(n1), off(n1 + 1, 0);
@@ -466,6 +546,12 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
   auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
   chk(hipMalloc((void**)&dA, (size_t)n1 * bytes));
   chk(hipMalloc((void**)&dB, (size_t)n2 * bytes));
+  if (masked) {
+    chk(hipMalloc((void**)&dmA, (size_t)n1 * bytes));
+    chk(hipMalloc((void**)&dmB, (size_t)n2 * bytes));
+    chk(hipMemcpy(dmA, mask1, (size_t)n1 * bytes, hipMemcpyHostToDevice));
+    chk(hipMemcpy(dmB, mask2, (size_t)n2 * bytes, hipMemcpyHostToDevice));
+  }
   chk(hipMalloc((void**)&dhA, n1));
   chk(hipMalloc((void**)&dhB, n2));
   chk(hipMalloc((void**)&dcA, 4 * (size_t)n1));
@@ -479,10 +565,15 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
   chk(hipMemcpy(dcA, cam1, 4 * (size_t)n1, hipMemcpyHostToDevice));
   chk(hipMemcpy(dcB, cam2, 4 * (size_t)n2, hipMemcpyHostToDevice));
   dim3 g((n1 + kHamThreads - 1) / kHamThreads);
-  if (e == hipSuccess) {
-    MCS_DISPATCH_W(bytes, k_radius, g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dcA, dhA, n1, dB,
-                   dcB, dhB, n2, th_low, dcnt, (const int32_t*)nullptr, (uint32_t*)nullptr);
+  auto launch = [&](const int32_t* o, uint32_t* out) {
+    if (masked)
+      launch_radius<true>(bytes, g, dA, dmA, dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th_low, dcnt, o, out);
+    else
+      launch_radius<false>(bytes, g, dA, dmA, dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th_low, dcnt, o, out);
     chk(hipGetLastError());
+  };
+  if (e == hipSuccess) {
+    launch(nullptr, nullptr);
     chk(hipMemcpy(cnt.data(), dcnt, 4 * (size_t)n1, hipMemcpyDeviceToHost));
   }
   if (e == hipSuccess) {
@@ -491,13 +582,11 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
     chk(hipMalloc((void**)&dout, 4 * cand.size()));
     chk(hipMemcpy(doff, off.data(), 4 * (size_t)n1, hipMemcpyHostToDevice));
     if (e == hipSuccess) {
-      MCS_DISPATCH_W(bytes, k_radius, g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dcA, dhA, n1,
-                     dB, dcB, dhB, n2, th_low, dcnt, (const int32_t*)doff, dout);
-      chk(hipGetLastError());
+      launch(doff, dout);
       chk(hipMemcpy(cand.data(), dout, 4 * (size_t)off[n1], hipMemcpyDeviceToHost));
     }
   }
-  void* bufs[] = {dA, dB, dhA, dhB, dcA, dcB, dcnt, doff, dout};
+  void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, dcnt, doff, dout};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (e != hipSuccess) { set_hip_error(e, "triangulation radius search", __FILE__, __LINE__); return MCS_ERR_HIP; }
@@ -522,20 +611,8 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
       const int d = (int)(c[k] >> 20), i2 = (int)(c[k] & 0xFFFFF);
       if (matched2[i2]) continue;
       if (d > th) break;
-      const int c2 = cam2[i2];
-      const double* Em = E + 9 * ((size_t)c1 * ncams + c2);
-      const double* r2 = rays2 + 3 * (size_t)i2;
-      // CheckDistEpipolarLine (src/misc.cpp:54-70)
-      double Ex1[3], Etx2[3];
-      for (int r = 0; r < 3; r++) {
-        Ex1[r] = Em[3 * r] * r1[0] + Em[3 * r + 1] * r1[1] + Em[3 * r + 2] * r1[2];
-        Etx2[r] = Em[r] * r2[0] + Em[3 + r] * r2[1] + Em[6 + r] * r2[2];
-      }
-      const double nom = r2[0] * Ex1[0] + r2[1] * Ex1[1] + r2[2] * Ex1[2];
-      const double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
-                         Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
-      if (den == 0.0) continue;
-      if ((nom * nom) / den < epi_thresh) {
+      const double* Em = E + 9 * ((size_t)c1 * ncams + cam2[i2]);
+      if (check_dist_epipolar_line(r1, rays2 + 3 * (size_t)i2, Em, epi_thresh)) {
         matched2[i2] = 1;
         matches12[i1] = i2;
         nm++;
@@ -545,6 +622,37 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
   }
   *n_matches = nm;
   return MCS_OK;
+}
+
+}  // namespace mcs
+
+extern "C" {
+
+int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
+                                     const uint8_t* has_mp1, const double* rays1, int32_t n1,
+                                     const uint8_t* desc2, const int32_t* cam2,
+                                     const uint8_t* has_mp2, const double* rays2, int32_t n2,
+                                     int32_t ncams, const double* E, int32_t bytes,
+                                     int32_t th_low, double epi_thresh, int32_t* matches12,
+                                     int32_t* n_matches) {
+  return search_for_triangulation(desc1, nullptr, cam1, has_mp1, rays1, n1, desc2, nullptr, cam2,
+                                  has_mp2, rays2, n2, ncams, E, bytes, th_low, epi_thresh,
+                                  matches12, n_matches);
+}
+
+int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t* mask1,
+                                            const int32_t* cam1, const uint8_t* has_mp1,
+                                            const double* rays1, int32_t n1,
+                                            const uint8_t* desc2, const uint8_t* mask2,
+                                            const int32_t* cam2, const uint8_t* has_mp2,
+                                            const double* rays2, int32_t n2, int32_t ncams,
+                                            const double* E, int32_t bytes, int32_t th_low,
+                                            double epi_thresh, int32_t* matches12,
+                                            int32_t* n_matches) {
+  if (!mask1 || !mask2) { set_error("triangulation: masked entry needs both masks"); return MCS_ERR_ARG; }
+  return search_for_triangulation(desc1, mask1, cam1, has_mp1, rays1, n1, desc2, mask2, cam2,
+                                  has_mp2, rays2, n2, ncams, E, bytes, th_low, epi_thresh,
+                                  matches12, n_matches);
 }
 
 }  // extern "C"

@@ -56,40 +56,61 @@ int oracle_hamming_top2(const uint8_t* q, int nq, const uint8_t* t, int nt, int 
   return 0;
 }
 
-static bool check_dist_epipolar_line(const double* r1, const double* r2, const double* E,
-                                     double thresh) {
-  // nom = ray2^T * E * ray1 ; Ex1 = E*ray1 ; Etx2 = E^T*ray2
-  double Ex1[3], Etx2[3];
-  for (int r = 0; r < 3; r++) {
-    Ex1[r] = E[3 * r] * r1[0] + E[3 * r + 1] * r1[1] + E[3 * r + 2] * r1[2];
-    Etx2[r] = E[r] * r2[0] + E[3 + r] * r2[1] + E[6 + r] * r2[2];
-  }
-  double nom = r2[0] * Ex1[0] + r2[1] * Ex1[1] + r2[2] * Ex1[2];
-  double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
-               Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
-  if (den == 0.0) return false;
-  return (nom * nom) / den < thresh;
+// cv::Matx products accumulate s = 0; s += a(i,k) * b(k,j) for k = 0.. (Matx_MatMulOp).
+static void matx_mul(const double* a, const double* b, double* c, int m, int l, int n) {
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < n; j++) {
+      double s = 0;
+      for (int k = 0; k < l; k++) s += a[i * l + k] * b[k * n + j];
+      c[i * n + j] = s;
+    }
 }
 
-int oracle_search_for_triangulation_raw(const uint8_t* desc1, int n1, const uint8_t* desc2,
-                                        int n2, int bytes, const int* cam1, const int* cam2,
-                                        const uint8_t* has_mp1, const uint8_t* has_mp2,
-                                        const double* rays1, const double* rays2,
-                                        const double* E /* ncams x ncams x 9 */, double thresh,
-                                        int ncams, int* matches12) {
-  const int TH_LOW = 2 * bytes;  // cORBmatcher ctor without masks (:61-63)
+static bool check_dist_epipolar_line(const double* r1, const double* r2, const double* E,
+                                     double thresh) {
+  // nom = ray2.t() * E12 * ray1 (left to right); Ex1 = E12 * ray1; Etx2 = E12.t() * ray2
+  double r2tE[3], nom, Ex1[3], Et[9], Etx2[3];
+  matx_mul(r2, E, r2tE, 1, 3, 3);
+  matx_mul(r2tE, r1, &nom, 1, 3, 1);
+  matx_mul(E, r1, Ex1, 3, 3, 1);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) Et[3 * r + c] = E[3 * c + r];
+  matx_mul(Et, r2, Etx2, 3, 3, 1);
+  const double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
+                     Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
+  if (den == 0.0) return false;
+  const double dsqr = (nom * nom) / den;
+  return dsqr < thresh;
+}
+
+// masks1 / masks2 nullable: the cORBmatcher was built with havingMasks (mdBRIEF), which also
+// selects the thresholds TH_LOW = floor(featDim) instead of 2 * featDim (:52-65).
+int oracle_search_for_triangulation_raw_ex(const uint8_t* desc1, const uint8_t* masks1, int n1,
+                                           const uint8_t* desc2, const uint8_t* masks2, int n2,
+                                           int bytes, const int* cam1, const int* cam2,
+                                           const uint8_t* has_mp1, const uint8_t* has_mp2,
+                                           const double* rays1, const double* rays2,
+                                           const double* E /* ncams x ncams x 9 */,
+                                           double thresh, int ncams, int* matches12) {
+  const bool havingMasks = masks1 != nullptr && masks2 != nullptr;
+  const int TH_LOW = havingMasks ? (int)std::floor((double)bytes) : 2 * bytes;
   std::vector<bool> vbMatched2(n2, false);
   int nmatches = 0;
   for (int i = 0; i < n1; i++) matches12[i] = -1;
   for (int idx1 = 0; idx1 < n1; ++idx1) {
     if (has_mp1[idx1]) continue;
+    const uint64_t* d1 = (const uint64_t*)(desc1 + (size_t)idx1 * bytes);
+    const uint64_t* m1 = havingMasks ? (const uint64_t*)(masks1 + (size_t)idx1 * bytes) : nullptr;
     std::vector<std::pair<int, size_t>> vDistIndex;
     std::vector<int> vDistCamIndex;
     for (int idx2 = 0; idx2 < n2; ++idx2) {
       if (vbMatched2[idx2] || has_mp2[idx2]) continue;
       if (cam1[idx1] != cam2[idx2]) continue;
-      int dist = oracle_descriptor_distance64((const uint64_t*)(desc1 + (size_t)idx1 * bytes),
-                                              (const uint64_t*)(desc2 + (size_t)idx2 * bytes), bytes);
+      const uint64_t* d2 = (const uint64_t*)(desc2 + (size_t)idx2 * bytes);
+      int dist = havingMasks
+          ? oracle_descriptor_distance64_masked(d1, d2, m1,
+                (const uint64_t*)(masks2 + (size_t)idx2 * bytes), bytes)
+          : oracle_descriptor_distance64(d1, d2, bytes);
       if (dist > TH_LOW) continue;
       vDistIndex.push_back(std::make_pair(dist, (size_t)idx2));
       vDistCamIndex.push_back(cam2[idx2]);
@@ -112,6 +133,17 @@ int oracle_search_for_triangulation_raw(const uint8_t* desc1, int n1, const uint
     }
   }
   return nmatches;
+}
+
+int oracle_search_for_triangulation_raw(const uint8_t* desc1, int n1, const uint8_t* desc2,
+                                        int n2, int bytes, const int* cam1, const int* cam2,
+                                        const uint8_t* has_mp1, const uint8_t* has_mp2,
+                                        const double* rays1, const double* rays2,
+                                        const double* E, double thresh, int ncams,
+                                        int* matches12) {
+  return oracle_search_for_triangulation_raw_ex(desc1, nullptr, n1, desc2, nullptr, n2, bytes,
+                                                cam1, cam2, has_mp1, has_mp2, rays1, rays2, E,
+                                                thresh, ncams, matches12);
 }
 
 }  // extern "C"

@@ -39,6 +39,7 @@ _SIGS = {
     "oracle_descriptor_distance64_masked": (_I, [_P, _P, _P, _P, _I]),
     "oracle_hamming_top2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
     "oracle_search_for_triangulation_raw": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
+    "oracle_search_for_triangulation_raw_ex": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
     "oracle_frame_grid": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "oracle_window_candidates": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I]),
     # DBoW2 vocabulary oracle

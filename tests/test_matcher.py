@@ -165,3 +165,107 @@ def test_search_for_triangulation_raw(gpu, seed):
     assert nref > 50
     assert nm.value == nref
     assert np.array_equal(got, ref)
+
+
+def _oracle_tri(d1, d2, cam1, cam2, has1, has2, r1, r2, E, thresh, m1=None, m2=None):
+    ref = np.zeros(len(d1), np.int32)
+    nb = d1.shape[1]
+    n = ob.lib().oracle_search_for_triangulation_raw_ex(
+        _p(d1), None if m1 is None else _p(m1), len(d1), _p(d2), None if m2 is None else _p(m2),
+        len(d2), nb, _p(cam1), _p(cam2), _p(has1), _p(has2), _p(np.ascontiguousarray(r1)),
+        _p(np.ascontiguousarray(r2)), _p(np.ascontiguousarray(E)), thresh, E.shape[0], _p(ref))
+    return n, ref
+
+
+def _masks(n, nbytes, seed, keep=0.8):
+    bits = (np.random.default_rng(seed).random((n, nbytes * 8)) < keep).astype(np.uint8)
+    return np.packbits(bits, axis=1)
+
+
+def test_triangulation_rejects_oversized_train(built):
+    """Candidates pack (dist << 20 | idx2): KF2 must hold fewer than 2^20 keypoints; the check
+    runs before any buffer is touched or a device is needed."""
+    import mcs_amd
+    got = np.zeros(4, np.int32)
+    nm = ctypes.c_int32()
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw(
+        None, None, None, None, 4, None, None, None, None, 1 << 20, 3, None, 32, 64, 0.3, _p(got),
+        ctypes.byref(nm))
+    assert rc == -1 and np.all(got == -1) and nm.value == 0
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw_masked(
+        None, None, None, None, None, 4, None, None, None, None, None, 1 << 20, 3, None, 32, 32,
+        0.3, _p(got), ctypes.byref(nm))
+    assert rc == -1
+
+
+def test_oracle_triangulation_unmasked_entry_agrees(built):
+    """The _ex oracle with no masks is the original restatement (TH_LOW = 2 * featDim)."""
+    d1, d2, cam1, cam2, has1, has2, r1, r2, E = _tri_problem(3, n1=300, n2=280)
+    n_ex, ref_ex = _oracle_tri(d1, d2, cam1, cam2, has1, has2, r1, r2, E, 0.3)
+    ref = np.zeros(len(d1), np.int32)
+    n = ob.lib().oracle_search_for_triangulation_raw(
+        _p(d1), len(d1), _p(d2), len(d2), 32, _p(cam1), _p(cam2), _p(has1), _p(has2),
+        _p(np.ascontiguousarray(r1)), _p(np.ascontiguousarray(r2)), _p(np.ascontiguousarray(E)),
+        0.3, 3, _p(ref))
+    assert n == n_ex and np.array_equal(ref, ref_ex) and n > 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,nbytes", [(0, 32), (4, 16), (5, 64)])
+def test_search_for_triangulation_raw_masked(gpu, seed, nbytes):
+    """havingMasks (mdBRIEF): DescriptorDistance64Masked and TH_LOW = floor(featDim)."""
+    import mcs_amd
+    d1, d2, cam1, cam2, has1, has2, r1, r2, E = _tri_problem(seed, n1=1200, n2=1100, nbytes=nbytes)
+    m1 = _masks(len(d1), nbytes, seed + 10)
+    m2 = _masks(len(d2), nbytes, seed + 11)
+    thresh = 0.3
+    nref, ref = _oracle_tri(d1, d2, cam1, cam2, has1, has2, r1, r2, E, thresh, m1, m2)
+    got = np.zeros(len(d1), np.int32)
+    nm = ctypes.c_int32()
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw_masked(
+        _p(d1), _p(m1), _p(cam1), _p(has1), _p(np.ascontiguousarray(r1)), len(d1),
+        _p(d2), _p(m2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), len(d2), 3,
+        _p(np.ascontiguousarray(E)), nbytes, nbytes, thresh, _p(got), ctypes.byref(nm))
+    assert rc == 0
+    assert nref > 30
+    assert nm.value == nref
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_config_b_size_matching(gpu):
+    """Config-B scale (2000 keypoints per frame, BASELINE configs[1]): batched top-2 between two
+    2000-keypoint sets and SearchForTriangulationRaw over 2000 x 2000, both vs the oracle."""
+    import torch
+    import mcs_amd
+    n = 2000
+    rng = np.random.default_rng(77)
+    a = _descs(n, 32, 70)
+    b = _descs(n, 32, 71)
+    perm = rng.permutation(n)
+    b[perm[:n // 2]] = _noisy_copy(a[:n // 2], rng.integers(0, 30, n // 2), 72)
+    sets = np.stack([a, b])
+    counts = np.array([n, n], np.int32)
+    pairs = np.array([[0, 1], [1, 0]], np.int32)
+    d = torch.from_numpy(sets).cuda()
+    dc = torch.from_numpy(counts).cuda()
+    dp = torch.from_numpy(pairs).cuda()
+    out = [torch.zeros((2, n), dtype=torch.int32, device="cuda") for _ in range(4)]
+    rc = mcs_amd.lib().mcs_hamming_top2_batch_device(d.data_ptr(), dc.data_ptr(), dp.data_ptr(),
+                                                     2, n, 32, *[o.data_ptr() for o in out], None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    for p, (qs, ts) in enumerate(pairs):
+        bi, bd, sd = _oracle_top2(sets[qs], sets[ts])
+        assert np.array_equal(out[0][p].cpu().numpy(), bi)
+        assert np.array_equal(out[1][p].cpu().numpy(), bd)
+        assert np.array_equal(out[3][p].cpu().numpy(), sd)
+    d1, d2, cam1, cam2, has1, has2, r1, r2, E = _tri_problem(78, n1=n, n2=n, ncams=3)
+    nref, ref = _oracle_tri(d1, d2, cam1, cam2, has1, has2, r1, r2, E, 0.3)
+    got = np.zeros(n, np.int32)
+    nm = ctypes.c_int32()
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw(
+        _p(d1), _p(cam1), _p(has1), _p(np.ascontiguousarray(r1)), n,
+        _p(d2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), n, 3,
+        _p(np.ascontiguousarray(E)), 32, 64, 0.3, _p(got), ctypes.byref(nm))
+    assert rc == 0 and nm.value == nref and np.array_equal(got, ref) and nref > 100
