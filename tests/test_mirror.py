@@ -79,7 +79,40 @@ def test_oracle_mask_properties_lafida():
         c = m[0]
         assert c[int(round(v0)), int(round(u0))] == 255       # centre inside
         assert c[0, 0] == 0 and c[-1, -1] == 0                 # image corners outside
-        assert np.array_equal(c, c) and set(np.unique(c)) <= {0, 255}
+        assert set(np.unique(c)) <= {0, 255}
+        _check_disc(c, row=v0, col=u0, radius=v0 + 22.0)
+
+
+def _check_disc(m, row, col, radius):
+    """255 strictly inside the disc (1 px margin), 0 strictly outside, and the mask is mirror-
+    symmetric about the centre row / column wherever both sides are in the image."""
+    h, w = m.shape
+    i = np.arange(h)[:, None]
+    j = np.arange(w)[None, :]
+    dist = np.sqrt((i - row) ** 2 + (j - col) ** 2)
+    assert (m[dist < radius - 1] == 255).all()
+    assert (m[dist > radius + 1] == 0).all()
+    r0, c0 = int(round(row)), int(round(col))
+    if abs(row - r0) < 1e-6 and abs(col - c0) < 1e-6:
+        k = min(r0, h - 1 - r0)
+        assert np.array_equal(m[r0 - k:r0], m[r0 + 1:r0 + k + 1][::-1])
+        k = min(c0, w - 1 - c0)
+        assert np.array_equal(m[:, c0 - k:c0], m[:, c0 + 1:c0 + k + 1][:, ::-1])
+
+
+def test_mirror_mask_centre_is_row_v0_col_u0():
+    """The reference swaps the names (src/cam_model_omni.cpp:189-190): the disc is centred at
+    row = Camera.v0, column = Camera.u0 with radius Camera.v0 + 22 at level 0.  With u0 != v0 the
+    swapped reading would give a different disc: pin the real one."""
+    u0, v0, w, h = 300.0, 200.0, 754, 480
+    m = oracle_masks(u0, v0, w, h)
+    _check_disc(m[0], row=200.0, col=300.0, radius=222.0)
+    assert m[0][200, 517] == 255     # 217 px right of the centre, inside r = 222
+    assert m[0][479, 300] == 0       # 279 px below: outside (the swapped disc would hold it)
+    # level 1: centre ceil(200/2), ceil(300/2); radius 100 + 10
+    _check_disc(m[1], row=100.0, col=150.0, radius=110.0)
+    for a, b in zip(m, numpy_masks(u0, v0, w, h)):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_layout_and_point_lookup_host():

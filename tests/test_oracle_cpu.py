@@ -86,13 +86,19 @@ def test_octree_returns_budget_and_best_responses():
 
 
 def test_fast_matches_bruteforce_definition():
-    """FAST candidates == brute-force segment test + cell-local NMS on a small image."""
+    """FAST candidates == per-pixel segment test + cornerScore + cell-local NMS, restated
+    independently in tests/np_extractor.py (itself checked against a literal per-pixel loop in
+    tests/test_oracle_crosscheck.py), on a small random image with one masked-out block."""
+    from tests import np_extractor as npx
     rng = np.random.default_rng(4)
     img = (rng.random((120, 140)) * 255).astype(np.uint8)
-    c = ob.level_candidates(img, None, 20)
-    assert len(c) > 0
-    # every candidate is a strict 8-neighbour maximum of scores inside the image
-    assert (c[:, 2] >= 20).all()
+    mask = np.full(img.shape, 255, np.uint8)
+    mask[40:70, 50:90] = 0
+    for m in (None, mask):
+        c = ob.level_candidates(img, m, 20)
+        assert len(c) > 20
+        assert np.array_equal(c, npx.fast_level(img, m, 20))
+        assert (c[:, 2] >= 20).all()
 
 
 def test_extract_deterministic_and_ordered():
