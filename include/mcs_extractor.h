@@ -139,6 +139,18 @@ int mcs_extractor_enable_timing(mcs_extractor* h, int32_t enable);
 int mcs_extractor_read_timing(mcs_extractor* h, float* ms_per_stage, int32_t* ncalls,
                               int32_t reset);
 
+/* HarrisResponses (src/mdBRIEFextractorOct.cpp:86-132), opt-in: the reference never calls it
+ * from ComputeKeyPointsOctTree (scoreType is stored, unused), so it is not part of
+ * mcs_extract*; callers that want Harris responses compute them here.  d_level_ptrs
+ * [n_levels] device addresses of u8 level images, d_level_geom [n_levels][3] = {w, h, pitch};
+ * d_kps [n] in LEVEL coordinates with octave = level; reads outside a level use its
+ * BORDER_REFLECT_101 mirror (the reference's padded levels).  Out: d_response [n] floats with
+ * the reference's float expression order.  block_size in [1, 45]. */
+int mcs_harris_responses_device(const uint64_t* d_level_ptrs, const int32_t* d_level_geom,
+                                int32_t n_levels, const mcs_keypoint* d_kps, int32_t n,
+                                int32_t block_size, float harris_k, float* d_response,
+                                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,6 +96,7 @@ SIGNATURES = {
     "mcs_extractor_levels": (ctypes.c_int, [_P, _P, _P, _P]),
     "mcs_extract": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _P, _I32, _P, _P, _P]),
     "mcs_extractor_set_masks_device": (ctypes.c_int, [_P, _P, _I32, _P]),
+    "mcs_harris_responses_device": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, ctypes.c_float, _P, _P]),
     "mcs_extract_batch_device": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_extractor_read_stage": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _I64, _P]),
     "mcs_extractor_set_cam_models": (ctypes.c_int, [_P, _P, _I32]),

@@ -704,6 +704,41 @@ int oracle_octree(const int* xys, int n, int minX, int maxX, int minY, int maxY,
   return 0;
 }
 
+// HarrisResponses (:86-132) on one level: the level is padded by EDGE_THRESHOLD px of
+// BORDER_REFLECT_101 as ComputePyramid does (:1185-1197) and read through the reference's
+// pointer arithmetic (ofs table, ptr0 = row y0 - r, column x0 - r).  xy [n][2] level coords.
+int oracle_harris_responses(const uint8_t* img, int w, int h, const float* xy, int n,
+                            int blockSize, float harris_k, float* out) {
+  const int B = EDGE_THRESHOLD, pw = w + 2 * B, ph = h + 2 * B;
+  std::vector<uint8_t> pad((size_t)pw * ph);
+  auto refl = [](int p, int len) { p = p < 0 ? -p : p; return p >= len ? 2 * len - 2 - p : p; };
+  for (int y = 0; y < ph; y++)
+    for (int x = 0; x < pw; x++) pad[(size_t)y * pw + x] = img[(size_t)refl(y - B, h) * w + refl(x - B, w)];
+  const uint8_t* ptr00 = pad.data() + (size_t)B * pw + B;   // the level's ROI origin
+  const int step = pw;
+  const int r = blockSize / 2;
+  const float scale = 1.f / ((1 << 2) * blockSize * 255.f);
+  const float scale_sq_sq = scale * scale * scale * scale;
+  std::vector<int> ofs((size_t)blockSize * blockSize);
+  for (int i = 0; i < blockSize; i++)
+    for (int j = 0; j < blockSize; j++) ofs[i * blockSize + j] = i * step + j;
+  for (int p = 0; p < n; p++) {
+    const int x0 = (int)std::lrint(xy[2 * p]), y0 = (int)std::lrint(xy[2 * p + 1]);
+    const uint8_t* ptr0 = ptr00 + (y0 - r) * step + x0 - r;
+    int a = 0, b = 0, c = 0;
+    for (int k = 0; k < blockSize * blockSize; k++) {
+      const uint8_t* ptr = ptr0 + ofs[k];
+      int Ix = (ptr[1] - ptr[-1]) * 2 + (ptr[-step + 1] - ptr[-step - 1]) + (ptr[step + 1] - ptr[step - 1]);
+      int Iy = (ptr[step] - ptr[-step]) * 2 + (ptr[step - 1] - ptr[-step - 1]) + (ptr[step + 1] - ptr[-step + 1]);
+      a += Ix * Ix;
+      b += Iy * Iy;
+      c += Ix * Iy;
+    }
+    out[p] = ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+  }
+  return 0;
+}
+
 float oracle_ic_angle(const uint8_t* img, int w, int h, int cx, int cy, int* m01, int* m10) {
   Img im; im.create(w, h); std::memcpy(im.d.data(), img, (size_t)w * h);
   static std::vector<int> umax = make_umax();

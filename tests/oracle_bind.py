@@ -30,6 +30,7 @@ _SIGS = {
     "oracle_level_candidates": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
     "oracle_octree": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P]),
     "oracle_ic_angle": (_F, [_P, _I, _I, _I, _I, _P, _P]),
+    "oracle_harris_responses": (_I, [_P, _I, _I, _P, _I, _I, _F, _P]),
     "oracle_extract": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _P, _P, _I, _P]),
     "oracle_extract_ex": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
     "oracle_cam_world_to_img": (_I, [_P, _D, _D, _D, _P]),
