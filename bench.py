@@ -102,6 +102,46 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     return nkp / dt / 1e3, sample, ncams
 
 
+def single_multiframe_latency(ex, d_img, d_midx, d_kps, d_cnt, d_desc, ncams, stream, reps):
+    """Latency of one cMultiFrame extraction (the NC cameras of one multi-frame, one batched
+    call, inputs resident in HBM), wall clock around launch + stream synchronise; median and
+    p90 over `reps` calls.  Complements the batched throughput."""
+    import torch
+    ex.enable_timing(False)
+    ts = []
+    for r in range(reps + 2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ex.extract_batch_device(d_img.data_ptr(), ncams, d_midx.data_ptr(), d_kps.data_ptr(),
+                                d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        if r >= 2:
+            ts.append((time.perf_counter() - t0) * 1e3)
+    ts.sort()
+    return {"multiframe_extract_ms_median": round(ts[len(ts) // 2], 4),
+            "multiframe_extract_ms_p90": round(ts[int(0.9 * (len(ts) - 1))], 4),
+            "reps": reps, "cameras": ncams, "keypoints": int(d_cnt[:ncams].sum().item())}
+
+
+def host_cpu_info():
+    """CPU model and thread count of the host the CPU baseline ran on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "host_threads_visible": avail,
+            "oracle_build": "g++ -O3 -ffp-contract=off -fno-fast-math (portable x86-64, no -march)"}
+
+
 def _oracle_top2(ob, q, t):
     import ctypes
     n = len(q)
@@ -390,6 +430,8 @@ def main():
                     help="config D multi-frames per step (8 cams 1024^2, camera per GPU); 0 = off")
     ap.add_argument("--bow-reps", type=int, default=10, help="timed DBoW2 transform launches; 0 = off")
     ap.add_argument("--d-unique", type=int, default=2, help="distinct rendered config D multi-frames")
+    ap.add_argument("--latency-reps", type=int, default=20,
+                    help="single multi-frame extraction latency samples; 0 = off")
     ap.add_argument("--selftest-dist", action="store_true",
                     help="CPU (gloo) rehearsal of the multi-rank launch and collectives only")
     args = ap.parse_args()
@@ -481,6 +523,8 @@ def main():
 
     kp_per_step = int(d_cnt.sum().item())
     dt_max, kp_tot = reduce_over_ranks(dt, kp_per_step * args.steps, dev, world)
+    latency = single_multiframe_latency(ex, d_img, d_midx, d_kps, d_cnt, d_desc, NC, stream,
+                                        args.latency_reps) if args.latency_reps > 0 else None
     value = kp_tot / dt_max / 1e3
 
     wh, _ = ex.levels()
@@ -543,6 +587,7 @@ def main():
         v, sample, cores = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
         cpu = {"value": round(v, 3), "unit": "kfeatures/s", "cores": cores, "kind": "port",
                "sample": sample}
+        cpu.update(host_cpu_info())
 
     if rank == 0:
         out = {
@@ -573,6 +618,7 @@ def main():
             "config_d": cfg_d,
             "bow": bow,
             "cpu_baseline_bow": cpu_bow,
+            "latency": latency,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),
         }

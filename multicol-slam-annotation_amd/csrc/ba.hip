@@ -402,19 +402,31 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d, double lam) {
   }
 }
 
+__device__ __forceinline__ double readlane0_d(double v) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 0);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 0);
+  return __hiloint2double(hi, lo);
+}
+
 // reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lam0 I)
 //   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T;
 // diagonal blocks also form bschur_i = b_i - sum_e Hpl_e db(point(e)).
-// The pair list of a block is split over 256 threads (fixed stride) + block tree sum.
+// One wave per block (four blocks per workgroup, no barriers): lane L accumulates pairs
+// L, L+64, ... (and the diagonal's edges the same way) in registers, then a fixed xor
+// butterfly over the lanes that can hold data (levels whose partners are all past the list
+// only add zeros and are skipped) leaves the sums in lane 0.  The block's pair list averages
+// ~90 pairs at config E, so a wave, not a 256-thread tree, is the right unit.
 // lam0 = lambda on rank 0 and 0 elsewhere (the sharded sum then holds lambda once).
-__global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam0) {
-  __shared__ double sm[42 * 4];
-  const int blk = blockIdx.x, t = threadIdx.x;
+__global__ __launch_bounds__(256) void k_schur(Dev d, double lam0, int nblk) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int blk = blockIdx.x * 4 + w;
+  if (blk >= nblk) return;
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
+  const int q0 = d.pr_ptr[blk], q1 = d.pr_ptr[blk + 1];
   double acc[42];
 #pragma unroll
   for (int v = 0; v < 42; v++) acc[v] = 0.0;
-  for (int q = d.pr_ptr[blk] + t; q < d.pr_ptr[blk + 1]; q += kRedNT) {
+  for (int q = q0 + lane; q < q1; q += 64) {
     const double* Y = d.y + 18 * d.pr_e1[q];
     const double* B = d.hpl + 18 * d.pr_e2[q];
     double y[18], bb[18];
@@ -426,8 +438,11 @@ __global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam0) {
       for (int c = 0; c < 6; c++)
         acc[6 * a + c] += y[3 * a] * bb[3 * c] + y[3 * a + 1] * bb[3 * c + 1] + y[3 * a + 2] * bb[3 * c + 2];
   }
+  int nact = q1 - q0;
   if (bi == bj) {
-    for (int q = d.ps_ptr[bi] + t; q < d.ps_ptr[bi + 1]; q += kRedNT) {
+    const int e0 = d.ps_ptr[bi], e1 = d.ps_ptr[bi + 1];
+    nact = max(nact, e1 - e0);
+    for (int q = e0 + lane; q < e1; q += 64) {
       const int e = d.ps_edges[q];
       const int lh = d.point_h[d.e_point[e]];
       if (lh < 0) continue;   // fixed point (pose-only BA): no Schur term
@@ -438,16 +453,27 @@ __global__ __launch_bounds__(kRedNT) void k_schur(Dev d, double lam0) {
       for (int a = 0; a < 6; a++) acc[36 + a] += B[3 * a] * g0 + B[3 * a + 1] * g1 + B[3 * a + 2] * g2;
     }
   }
-  block_sum_vec<42>(acc, sm);
-  if (t < 36) {
-    const int a = t / 6, c = t % 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    if (nact <= o) continue;    // wave-uniform
+#pragma unroll
+    for (int v = 0; v < 42; v++) acc[v] += __shfl_xor(acc[v], o);
+  }
+  double mine = 0.0;
+#pragma unroll
+  for (int v = 0; v < 42; v++) {
+    const double sv = readlane0_d(acc[v]);
+    if (lane == v) mine = sv;
+  }
+  if (lane < 36) {
+    const int a = lane / 6, c = lane % 6;
     if (bi == bj && c > a) return;   // lower triangle of the diagonal block only
     double s0 = 0.0;
     if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam0; }
-    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - sm[t * 4];
-  } else if (t < 42 && bi == bj) {
-    const int a = t - 36;
-    d.bs[6 * bi + a] = d.bp[6 * bi + a] - sm[t * 4];
+    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - mine;
+  } else if (lane < 42 && bi == bj) {
+    const int a = lane - 36;
+    d.bs[6 * bi + a] = d.bp[6 * bi + a] - mine;
   }
 }
 
@@ -863,8 +889,9 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d, lambda);
         MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
         if (s.np) {
-          hipLaunchKernelGGL(k_schur, dim3((unsigned)s.blk_i.size()), dim3(kRedNT), 0, st, d,
-                             sh.rank == 0 ? lambda : 0.0);
+          const int nblk = (int)s.blk_i.size();
+          hipLaunchKernelGGL(k_schur, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, d,
+                             sh.rank == 0 ? lambda : 0.0, nblk);
           MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
           rec(3);
           if ((rc = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc;   // S tiles | bs

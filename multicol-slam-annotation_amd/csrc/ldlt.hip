@@ -21,26 +21,104 @@ namespace ldlt {
 
 namespace {
 
-constexpr int LS = TB + 1;   // LDS row stride in doubles (breaks the power-of-two stride)
+// LDS row stride in doubles.  66 = 2 (mod 32): the MFMA operand reads (lane (r, k) of a
+// 16 x 4 sub-block at r * LS + k) hit 32 distinct bank pairs per half-wave (conflict-free);
+// the row-per-lane accesses of the panel elimination are 2-way.
+constexpr int LS = TB + 2;
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void load_tile(double* s, const double* __restrict__ g) {
-  for (int e = threadIdx.x; e < TB * TB; e += 256) s[(e >> 6) * LS + (e & 63)] = g[e];
+// Tiles move global -> registers -> LDS in two phases so that all of a thread's loads (of
+// every tile it needs) are in flight together: 8 x 16-byte loads per tile per thread.
+__device__ __forceinline__ void fetch_tile(d2 (&v)[8], const double* __restrict__ g) {
+  const d2* g2 = reinterpret_cast<const d2*>(g);
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = g2[threadIdx.x + 256 * i];
 }
-
-// diagonal tile: only the lower triangle is defined (the strict upper part of the storage is
-// never written by the producers and may hold stale bits), so it is loaded as 0
-__device__ __forceinline__ void load_tile_lower(double* s, const double* __restrict__ g) {
-  for (int e = threadIdx.x; e < TB * TB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    s[r * LS + c] = (c <= r) ? g[e] : 0.0;
+__device__ __forceinline__ void put_tile(double* s, const d2 (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = 2 * (threadIdx.x + 256 * i);
+    *reinterpret_cast<d2*>(&s[(e >> 6) * LS + (e & 63)]) = v[i];
   }
 }
+// diagonal tile: only the lower triangle is defined (the strict upper part of the storage is
+// never written by the producers and may hold stale bits), so it is stored as 0
+__device__ __forceinline__ void put_tile_lower(double* s, const d2 (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = 2 * (threadIdx.x + 256 * i);
+    const int r = e >> 6, c = e & 63;
+    d2 w = v[i];
+    if (c > r) w.x = 0.0;
+    if (c + 1 > r) w.y = 0.0;
+    *reinterpret_cast<d2*>(&s[r * LS + c]) = w;
+  }
+}
+__device__ __forceinline__ void load_tile_lower(double* s, const double* __restrict__ g) {
+  d2 v[8];
+  fetch_tile(v, g);
+  put_tile_lower(s, v);
+}
+
+#ifdef MCS_LDLT_PROBE
+__device__ long long g_ldlt_stamps[16];
+#define LDLT_STAMP(i) do { if (threadIdx.x == 0) g_ldlt_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+// per (step, workgroup) phase clocks of k_panel: [k][wg][8]
+__device__ long long g_panel_stamps[32 * 256 * 8];
+#define PANEL_STAMP(i) do { if (threadIdx.x == 0 && k < 32 && blockIdx.x < 256) \
+    g_panel_stamps[((size_t)k * 256 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define LDLT_STAMP(i) do { } while (0)
+#define PANEL_STAMP(i) do { } while (0)
+#endif
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
   return __hiloint2double(hi, lo);
+}
+
+// X = L_BB^-1 of the unit-lower 16x16 diagonal block at (B, B), by one wave: lane column
+// c = lane & 15 (four copies), column-oriented substitution (once x[k] is final it updates
+// every later row: a 15-deep FMA chain instead of 120); the per-row accumulation order is
+// still k ascending.  L entries are uniform LDS reads (broadcast).  Lanes 0..15 write X.
+__device__ __forceinline__ void inv_diag16(const double* sA, double* sI, int B) {
+  const int l = threadIdx.x & 63, c = l & 15;
+  double x[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) x[r] = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < 15; k++)
+#pragma unroll
+    for (int r = k + 1; r < 16; r++) x[r] = __builtin_fma(-sA[(B + r) * LS + B + k], x[k], x[r]);
+  if (l < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) sI[(B + r) * LS + B + c] = x[r];
+  }
+}
+
+// off-diagonal block X_ij = -X_ii (sum_{k=j}^{i-1} L_ik X_kj) of L^-1 (one wave, MFMA); the
+// inner sum stays in accumulator layout, which is the B-operand layout of the outer product
+__device__ __forceinline__ void offdiag_block(const double* sA, double* sI, int i, int j) {
+  const int l = threadIdx.x & 63, r16 = l & 15, k4 = l >> 4;
+  d4 s = {0.0, 0.0, 0.0, 0.0};
+  for (int k = j; k < i; k++) {
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 4) {
+      const double av = sA[(16 * i + r16) * LS + 16 * k + k0 + k4];   // L_ik[m][kk]
+      const double bv = sI[(16 * k + k0 + k4) * LS + 16 * j + r16];   // X_kj[kk][n]
+      s = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, s, 0, 0, 0);
+    }
+  }
+  d4 xo = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const double av = sI[(16 * i + r16) * LS + 16 * i + 4 * r + k4];  // X_ii[m][4r + kk]
+    xo = __builtin_amdgcn_mfma_f64_16x16x4f64(av, s[r], xo, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) sI[(16 * i + k4 + 4 * r) * LS + 16 * j + r16] = -xo[r];
 }
 
 // LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, blocked by 16-column panels.
@@ -67,6 +145,7 @@ __device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
       double a[16];
 #pragma unroll
       for (int c = 0; c < 16; c++) a[c] = sA[l * LS + P + c];
+#ifdef MCS_LDLT_FACTOR_V1
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int J = P + j;
@@ -79,8 +158,40 @@ __device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
         if (l >= J) sA[l * LS + J] = (l > J) ? lj : cj;
         if (l >= P + 16) sA[J * LS + l] = cj;
       }
+#else
+      // column broadcast through LDS (sI is scratch until the L^-1 phase): the wave writes its
+      // unscaled column once and reads the pivot and the panel rows back with uniform
+      // addresses (in-order LDS within one wave, no barrier); the pivot's reciprocal is one
+      // v_rcp_f64 + two Newton steps instead of a per-lane IEEE division
+      double* sc = sI + 63 * LS;   // row 63 of sI: written last (block row 3)
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int J = P + j;
+        const double cj = a[j];
+        sc[l] = cj;
+        __builtin_amdgcn_wave_barrier();
+        double cm[16];
+#pragma unroll
+        for (int m = j; m < 16; m++) cm[m] = sc[P + m];
+        __builtin_amdgcn_wave_barrier();
+        const double dj = cm[j];
+        double r = __builtin_amdgcn_rcp(dj);
+        r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
+        r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
+        const double lj = cj * r;
+#pragma unroll
+        for (int m = j + 1; m < 16; m++) a[m] = __builtin_fma(-lj, cm[m], a[m]);
+        if (dj == 0.0 && l == 0) *fail = 1;
+        if (l >= J) sA[l * LS + J] = (l > J) ? lj : cj;
+        if (l >= P + 16) sA[J * LS + l] = cj;
+      }
+#endif
+    } else if (w == p - 1) {
+      // the previous panel's diagonal block is final: invert it while this panel runs
+      inv_diag16(sA, sI, 16 * (p - 1));
     }
     __syncthreads();
+    LDLT_STAMP(2 * p);
     const int nb = 3 - p;
     for (int b = w; b < nb * (nb + 1) / 2; b += 4) {
       int q = 0, s = b;
@@ -97,50 +208,22 @@ __device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
       for (int r = 0; r < 4; r++) sA[(16 * bi + k4 + 4 * r) * LS + 16 * bj + r16] -= acc[r];
     }
     __syncthreads();
+    LDLT_STAMP(2 * p + 1);
   }
-  // L^-1, diagonal blocks: wave w solves L_ww x = e_c for column c = lane & 15
-  {
-    const int B = 16 * w;
-    double x[16];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      double s = (r == r16) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < r; k++) s = __builtin_fma(-sA[(B + r) * LS + B + k], x[k], s);
-      x[r] = s;
-    }
-    if (l < 16) {
-#pragma unroll
-      for (int r = 0; r < 16; r++) sI[(B + r) * LS + B + r16] = x[r];
-    }
-    for (int e = t; e < TB * TB; e += 256) {
-      const int rr = e >> 6, cc = e & 63;
-      if ((cc >> 4) > (rr >> 4)) sI[rr * LS + cc] = 0.0;
-    }
+  // L^-1: diagonal blocks 0..2 were inverted during the next panel; block 3 now (wave 3),
+  // while wave 0 forms the off-diagonal block X_10 (it needs X_00, X_11 only) and the other
+  // waves clear the upper blocks
+  if (w == 3) inv_diag16(sA, sI, 48);
+  else if (w == 0) offdiag_block(sA, sI, 1, 0);
+  for (int e = t; e < TB * TB; e += 256) {
+    const int rr = e >> 6, cc = e & 63;
+    if ((cc >> 4) > (rr >> 4)) sI[rr * LS + cc] = 0.0;
   }
   __syncthreads();
-  // off-diagonal blocks, one block row at a time (row i needs the rows above it)
-  for (int i = 1; i < 4; i++) {
-    if (w < i) {
-      const int j = w;
-      d4 s = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; k++) {
-#pragma unroll
-        for (int k0 = 0; k0 < 16; k0 += 4) {
-          const double av = sA[(16 * i + r16) * LS + 16 * k + k0 + k4];   // L_ik[m][kk]
-          const double bv = sI[(16 * k + k0 + k4) * LS + 16 * j + r16];   // X_kj[kk][n]
-          s = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, s, 0, 0, 0);
-        }
-      }
-      d4 xo = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const double av = sI[(16 * i + r16) * LS + 16 * i + 4 * r + k4];  // X_ii[m][4r + kk]
-        xo = __builtin_amdgcn_mfma_f64_16x16x4f64(av, s[r], xo, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++) sI[(16 * i + k4 + 4 * r) * LS + 16 * j + r16] = -xo[r];
-    }
+  LDLT_STAMP(8);
+  // remaining off-diagonal blocks, one block row at a time (row i needs the rows above it)
+  for (int i = 2; i < 4; i++) {
+    if (w < i) offdiag_block(sA, sI, i, w);
     __syncthreads();
   }
 }
@@ -153,13 +236,35 @@ __device__ __forceinline__ void gemm_xyt(const double* X, const double* Y, d4 (&
   const int r16 = l & 15, k4 = l >> 4;
 #pragma unroll
   for (int q = 0; q < 4; q++) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
+#pragma unroll
   for (int k0 = 0; k0 < TB; k0 += 4) {
     const double bv = Y[(16 * w + r16) * LS + k0 + k4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const double av = X[(16 * q + r16) * LS + k0 + k4];
       acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+    }
+  }
+}
+
+// acc = X Linv^T with Linv unit lower (zero above the diagonal): output block (q, c) only
+// needs k < 16 (c + 1).  Wave w computes row block q = w for the four column blocks
+// (acc[c]); with the k loop fully unrolled the triangular bounds are static: 40 MFMAs per
+// wave instead of 64, every wave the same.
+__device__ __forceinline__ void gemm_xlt(const double* X, const double* Li, d4 (&acc)[4]) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = l & 15, k4 = l >> 4;
+#pragma unroll
+  for (int c = 0; c < 4; c++) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < TB; k0 += 4) {
+    const double av = X[(16 * w + r16) * LS + k0 + k4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (k0 < 16 * (c + 1)) {
+        const double bv = Li[(16 * c + r16) * LS + k0 + k4];
+        acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[c], 0, 0, 0);
+      }
     }
   }
 }
@@ -199,15 +304,34 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
     j = k + 1 + (q - ii * (ii + 1) / 2);
   }
   const bool rhs = (wg == 0) || (i == j);
+  PANEL_STAMP(0);
   if (t == 0) fail = 0;
-  load_tile_lower(sK, A + toff(k, k));
+  const int l = t & 63, w = t >> 6, r16 = l & 15, k4 = l >> 4;
+  // every global read of the workgroup in flight together: A_kk, A_ik, A_jk, b_k and the
+  // A_ij entries this thread updates at the end (accumulator layout, kept in registers)
+  d2 vK[8], vX[8], vY[8];
+  double aij[4][4];
+  fetch_tile(vK, A + toff(k, k));
   if (wg > 0) {
-    load_tile(sX, A + toff(i, k));
-    if (j != i) load_tile(sY, A + toff(j, k));
+    fetch_tile(vX, A + toff(i, k));
+    if (j != i) fetch_tile(vY, A + toff(j, k));
+    const double* Aij = A + toff(i, j);
+    const int col = 16 * w + r16;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) aij[q][r] = Aij[(16 * q + k4 + 4 * r) * TB + col];
   }
   if (rhs && t < TB) sv[t] = b[k * TB + t];
+  put_tile_lower(sK, vK);
+  if (wg > 0) {
+    put_tile(sX, vX);
+    if (j != i) put_tile(sY, vY);
+  }
   __syncthreads();
+  PANEL_STAMP(1);
   factor_tile(sK, sI, &fail);
+  PANEL_STAMP(2);
   if (rhs) {
     const double u = gemv_row(sI, sv);
     if ((t & 3) == 0) su[t >> 2] = u;
@@ -220,26 +344,28 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
     if (t == 0 && fail) *flag = 1;
     return;
   }
-  const int l = t & 63, w = t >> 6, r16 = l & 15, k4 = l >> 4;
   d4 wi[4], wj[4];
-  gemm_xyt(sX, sI, wi);
-  if (j != i) gemm_xyt(sY, sI, wj);
+  gemm_xlt(sX, sI, wi);
+  if (j != i) gemm_xlt(sY, sI, wj);
   __syncthreads();
+  PANEL_STAMP(3);
   {
-    const int col = 16 * w + r16;
-    const double invd = 1.0 / sK[col * LS + col];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
+    for (int c = 0; c < 4; c++) {
+      const int col = 16 * c + r16;
+      const double invd = 1.0 / sK[col * LS + col];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int row = 16 * q + k4 + 4 * r;
-        sX[row * LS + col] = wi[q][r] * invd;
-        sY[row * LS + col] = (j != i) ? wj[q][r] : wi[q][r];
+        const int row = 16 * w + k4 + 4 * r;
+        sX[row * LS + col] = wi[c][r] * invd;
+        sY[row * LS + col] = (j != i) ? wj[c][r] : wi[c][r];
       }
+    }
   }
   __syncthreads();
   d4 p[4];
   gemm_xyt(sX, sY, p);
+  PANEL_STAMP(4);
   {
     double* Aij = A + toff(i, j);
     const int col = 16 * w + r16;
@@ -248,7 +374,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = 16 * q + k4 + 4 * r;
-        Aij[row * TB + col] -= p[q][r];
+        Aij[row * TB + col] = aij[q][r] - p[q][r];
       }
   }
   if (i == j) {
@@ -257,6 +383,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
     const double s = gemv_row(sX, su);
     if ((t & 3) == 0) b[i * TB + (t >> 2)] -= s;
   }
+  PANEL_STAMP(5);
 }
 
 // L^T x = z, one workgroup of 1024 threads, left-looking:

@@ -2,6 +2,7 @@
 // 64x64 tile): s_memtime (shader clock) and s_memrealtime (100 MHz) around the phases, and
 // L, D, L^-1 compared with a host LDL^T of the same tile.  Exit status 1 on a mismatch.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/bench/ldlt_probe.hip -o tools/bench/ldlt_probe
+#define MCS_LDLT_PROBE 1
 #include "../../multicol-slam-annotation_amd/csrc/ldlt.hip"
 #include <cmath>
 #include <cstdio>
@@ -13,7 +14,7 @@ __global__ __launch_bounds__(256) void k_probe(const double* A, double* outL, do
                                                long long* stamps) {
   extern __shared__ double sm[];
   double* sK = sm;
-  double* sI = sK + TB * 65;
+  double* sI = sK + TB * LS;
   __shared__ int fail;
   long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) fail = 0;
@@ -24,12 +25,13 @@ __global__ __launch_bounds__(256) void k_probe(const double* A, double* outL, do
   long long t2 = __builtin_amdgcn_s_memtime(), r2 = __builtin_amdgcn_s_memrealtime();
   for (int e = threadIdx.x; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
-    outL[e] = c <= r ? sK[r * 65 + c] : 0.0;
-    outI[e] = sI[r * 65 + c];
+    outL[e] = c <= r ? sK[r * LS + c] : 0.0;
+    outI[e] = sI[r * LS + c];
   }
   if (threadIdx.x == 0) {
     stamps[0] = t1 - t0; stamps[1] = t2 - t1; stamps[2] = t2 - t0; stamps[3] = r2 - r0;
     stamps[4] = fail;
+    for (int i = 0; i < 9; i++) stamps[5 + i] = g_ldlt_stamps[i] - t1;
   }
 }
 
@@ -58,17 +60,20 @@ int main() {
   double *dA, *dL, *dI;
   long long* dS;
   (void)hipMalloc(&dA, 4096 * 8); (void)hipMalloc(&dL, 4096 * 8); (void)hipMalloc(&dI, 4096 * 8);
-  (void)hipMalloc(&dS, 64);
+  (void)hipMalloc(&dS, 16 * 8);
   (void)hipMemcpy(dA, h.data(), 4096 * 8, hipMemcpyHostToDevice);
-  const size_t lds = 2 * 64 * 65 * 8;
+  const size_t lds = 2 * 64 * LS * 8;
   (void)hipFuncSetAttribute((const void*)k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   bool ok = true;
   for (int rep = 0; rep < 3; rep++) {
     hipLaunchKernelGGL(k_probe, dim3(1), dim3(256), lds, 0, dA, dL, dI, dS);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("launch failed\n"); return 2; }
-    long long s[5];
+    long long s[14];
     std::vector<double> oL(4096), oI(4096);
-    (void)hipMemcpy(s, dS, 40, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(s, dS, 14 * 8, hipMemcpyDeviceToHost);
+    std::printf("phase stamps (cyc from factor start): panel/update p0..p3, Linv diag:");
+    for (int i = 0; i < 9; i++) std::printf(" %lld", s[5 + i]);
+    std::printf("\n");
     (void)hipMemcpy(oL.data(), dL, 4096 * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(oI.data(), dI, 4096 * 8, hipMemcpyDeviceToHost);
     double eL = 0, eD = 0, eI = 0, eU = 0;

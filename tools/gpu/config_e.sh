@@ -13,3 +13,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 S=$(find $OUT/prof -name '*kernel_stats.csv' | head -1); cp "$S" $OUT/kernel_stats.csv
 head -12 $OUT/kernel_stats.csv | cut -c1-200
 python3 -c "import json; d=json.load(open('$OUT/bench.json')); print(json.dumps(d['globalba']))"
+T=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
+[ -n "$T" ] && python3 tools/ktrace_by_grid.py "$T" k_panel k_backward k_schur k_point_trial k_edges > $OUT/by_grid.txt && cat $OUT/by_grid.txt
+true
