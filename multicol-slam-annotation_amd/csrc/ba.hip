@@ -263,7 +263,39 @@ __global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
   }
 }
 
-// deterministic single-workgroup sum / max|.| of n doubles -> out[0]
+// deterministic sum / max|.| of n doubles -> out[0], two stages with fixed orders:
+// k_reduce_part: workgroup g owns the contiguous chunk [g*chunk, (g+1)*chunk), each thread
+// 8 strided accumulators (loads in flight, short add chains), a fixed tree over the block;
+// k_reduce: one workgroup over the partials.  Small inputs skip the first stage.
+constexpr int kRedPartMax = 256;
+template <bool MAX>
+__global__ __launch_bounds__(256) void k_reduce_part(const double* __restrict__ v, int n, int chunk,
+                                                     double* __restrict__ part) {
+  __shared__ double s[256];
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int b0 = g * chunk, b1 = min(n, b0 + chunk);
+  double acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) acc[u] = 0.0;
+  for (int i = b0 + t; i < b1; i += 8 * 256) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = i + u * 256;
+      if (q < b1) acc[u] = MAX ? fmax(acc[u], fabs(v[q])) : acc[u] + v[q];
+    }
+  }
+  double a = acc[0];
+#pragma unroll
+  for (int u = 1; u < 8; u++) a = MAX ? fmax(a, acc[u]) : a + acc[u];
+  s[t] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) s[t] = MAX ? fmax(s[t], s[t + o]) : s[t] + s[t + o];
+    __syncthreads();
+  }
+  if (t == 0) part[g] = s[0];
+}
+
 template <bool MAX>
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, int n, double* out) {
   __shared__ double s[1024];
@@ -276,6 +308,19 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, i
     __syncthreads();
   }
   if (threadIdx.x == 0) *out = s[0];
+}
+
+// launch helper: part = kRedPartMax doubles of scratch (stream-ordered reuse is safe)
+template <bool MAX>
+void reduce_dev(const double* v, int n, double* out, double* part, hipStream_t st) {
+  if (n <= 32768) {
+    hipLaunchKernelGGL(k_reduce<MAX>, dim3(1), dim3(1024), 0, st, v, n, out);
+    return;
+  }
+  const int chunk = std::max(8 * 256, (n + kRedPartMax - 1) / kRedPartMax);
+  const int g = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_reduce_part<MAX>, dim3(g), dim3(256), 0, st, v, n, chunk, part);
+  hipLaunchKernelGGL(k_reduce<MAX>, dim3(1), dim3(1024), 0, st, (const double*)part, g, out);
 }
 
 // per active point: Hll (3x3), b_l over its edges in edge order; diag -> red (for lambda init)
@@ -821,6 +866,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
   lw.z = dz((size_t)ldlt::TB * T);
   double* d_scalar = dz(8);
+  double* d_part = dz(kRedPartMax);
   int* d_flag = (int*)c->alloc(16);
   if (he != hipSuccess || !d_flag) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
 
@@ -833,7 +879,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
 
   auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate (all ranks)
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
+    reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
     MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
     MCS_HIP_CHECK(hipStreamSynchronize(st));
     double v[2] = {c->pinned[3], (double)(*stop != 0)};
@@ -872,8 +918,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       bool lin_pending = c->timing;
       if ((rc = allreduce(MCS_REDUCE_SUM, X.hdiag, 12 * (size_t)s.np))) return rc;   // hdiag | bpf
       if (i == 0) {
-        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
-        hipLaunchKernelGGL(k_reduce<true>, dim3(1), dim3(1024), 0, st, (const double*)d.hdiag, 6 * s.np, d_scalar + 2);
+        reduce_dev<true>(d.red, s.nl, d_scalar + 1, d_part, st);
+        reduce_dev<true>(d.hdiag, 6 * s.np, d_scalar + 2, d_part, st);
         MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 16, hipMemcpyDeviceToHost, st));
         MCS_HIP_CHECK(hipStreamSynchronize(st));
         double mx = std::max(c->pinned[1], c->pinned[2]);
@@ -902,10 +948,10 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         }
         rec(5);
         hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d, lambda);
-        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.red, s.nl, d_scalar + 1);
-        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)(d.red + s.nl), s.np, d_scalar + 2);
+        reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
+        reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
         hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-        hipLaunchKernelGGL(k_reduce<false>, dim3(1), dim3(1024), 0, st, (const double*)d.rchi, d.nae, d_scalar);
+        reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
         MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
         MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
         rec(6);
