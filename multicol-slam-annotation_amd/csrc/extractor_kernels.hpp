@@ -43,11 +43,17 @@ inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
   const int n = (dw + 243) / 244;
   a.core = ((dw + n - 1) / n + 3) & ~3;
   a.tiles_x = (dw + a.core - 1) / a.core;
-  const long target = 16384;
+#ifndef MCS_PYR_TARGET
+#define MCS_PYR_TARGET 16384
+#endif
+  const long target = MCS_PYR_TARGET;
   const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
   const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
   int rows = (dh + segs - 1) / segs;
-  rows = std::min(64, std::max(8, rows));
+#ifndef MCS_PYR_MAXROWS
+#define MCS_PYR_MAXROWS 64
+#endif
+  rows = std::min(MCS_PYR_MAXROWS, std::max(8, rows));
   a.seg_rows = rows;
   a.tiles_y = (dh + rows - 1) / rows;
 }

@@ -27,7 +27,10 @@
 
 namespace mcs {
 
-constexpr int kCellsPerWave = 8;
+#ifndef MCS_FAST_CPW
+#define MCS_FAST_CPW 8
+#endif
+constexpr int kCellsPerWave = MCS_FAST_CPW;
 
 __device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
@@ -38,8 +41,11 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 //   smap  [(ww+2)*(wh+2)]   score + 1 for corners, 0 otherwise (window raster + zero ring)
 //   surv  u16[ww*wh]        compass-test survivors (y<<8 | x), then the corners in place
 // NT = tile dwords prefetched per lane (>= ceil(tile_dwords / 64)).
+#ifndef MCS_FAST_OCC
+#define MCS_FAST_OCC 1
+#endif
 template <int NT>
-__global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
+__global__ __launch_bounds__(256, MCS_FAST_OCC) void k_fast_cells(FastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
   // the wave index as a scalar: the cell run, its descriptors and every per-cell quantity
   // are wave-uniform (SGPRs and scalar branches)

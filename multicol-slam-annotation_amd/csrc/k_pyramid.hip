@@ -57,13 +57,19 @@ __device__ __forceinline__ uint32_t div50(uint32_t n) { return (n * 20972u) >> 2
 // No workgroup barriers: every wave works alone.  Everything derived from the work unit is
 // wave-uniform and kept scalar (readfirstlane of the wave index and of table reads).
 constexpr int kStageDW = 192;    // staged source row (dwords), scale <= 2.2
-constexpr int kPF = 4;           // source rows in flight per wave
+#ifndef MCS_PYR_KPF
+#define MCS_PYR_KPF 4
+#endif
+constexpr int kPF = MCS_PYR_KPF;  // source rows in flight per wave
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // NDW = staged dwords per lane per source row: 1 (level 0), 2 (scale <= 1.5), 3 (scale <= 2.2)
+#ifndef MCS_PYR_OCC
+#define MCS_PYR_OCC 1
+#endif
 template <bool RESIZE, int NDW>
-__global__ __launch_bounds__(256) void k_pyr_rows(PyrArgs a) {
+__global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
   __shared__ uint32_t lds_stage[4][kStageDW];
   // wave index as a scalar: everything derived from the work unit is wave-uniform, and the
   // compiler must know it (SGPRs, scalar branches) or it keeps all of it in VGPRs
