@@ -221,6 +221,10 @@ struct Dev {
   const int32_t* pt_ptr; const int32_t* pt_edges;     // CSR active points -> active edges
   const int32_t* ps_ptr; const int32_t* ps_edges;     // CSR active poses  -> active edges
   const int32_t* blk_i; const int32_t* blk_j;         // lower pose blocks (i >= j)
+  const int32_t* it_blk; const int32_t* it_chunk; const int32_t* it_slot;  // k_schur items
+  const int32_t* fin_blk; const int32_t* fin_slot0; const int32_t* fin_nch;  // k_schur_fin
+  double* schur_part;                                 // [slots][42]
+  const double* lam_dev;                              // [0] lambda, [1] lambda on rank 0 else 0
   const int32_t* pr_ptr; const int32_t* pr_e1; const int32_t* pr_e2;  // edge pairs per block
   int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
@@ -410,8 +414,9 @@ __global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
 // One thread per (point, edge) entry of the point CSR: D = Hll + lambda I -> Dinv (cofactors,
 // recomputed per entry: identical bits), Y_e = Hpl_e Dinv; the first entry of each point
 // also stores Dinv and db = Dinv b_l.
-__global__ __launch_bounds__(256) void k_point_trial(Dev d, double lam) {
+__global__ __launch_bounds__(256) void k_point_trial(Dev d) {
   const int q = blockIdx.x * 256 + threadIdx.x;
+  const double lam = d.lam_dev[0];
   if (q >= d.npe) return;
   const int e = d.pt_edges[q];
   const int l = d.point_h[d.e_point[e]];
@@ -456,18 +461,40 @@ __device__ __forceinline__ double readlane0_d(double v) {
 // reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lam0 I)
 //   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T;
 // diagonal blocks also form bschur_i = b_i - sum_e Hpl_e db(point(e)).
-// One wave per block (four blocks per workgroup, no barriers): lane L accumulates pairs
-// L, L+64, ... (and the diagonal's edges the same way) in registers, then a fixed xor
-// butterfly over the lanes that can hold data (levels whose partners are all past the list
-// only add zeros and are skipped) leaves the sums in lane 0.  The block's pair list averages
-// ~90 pairs at config E, so a wave, not a 256-thread tree, is the right unit.
+// Work items (host-built, `build_schur_items`): item = (block, chunk c of nch); chunk c covers
+// pairs [q0 + c*CH, ...) and, on a diagonal block, pose edges [e0 + c*CH, ...).  One wave per
+// item: lane L accumulates entries L, L+64, ... in registers, a fixed xor butterfly over the
+// lanes that can hold data (levels whose partners are all past the chunk add zeros and are
+// skipped) leaves the 42 sums in lane 0.  A block with one chunk (config E: ~90 pairs per
+// block) writes S / bschur directly; otherwise the chunk's sums go to a partial slot and
+// k_schur_fin adds the slots in chunk order (config C: 55 blocks of thousands of pairs, so a
+// block per wave would leave the GPU idle).  Every order is fixed: bitwise reproducible.
 // lam0 = lambda on rank 0 and 0 elsewhere (the sharded sum then holds lambda once).
-__global__ __launch_bounds__(256) void k_schur(Dev d, double lam0, int nblk) {
+constexpr int kSchurChunk = 256;
+
+__device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double lam0, int lane,
+                                            double v) {
+  if (lane < 36) {
+    const int a = lane / 6, c = lane % 6;
+    if (bi == bj && c > a) return;   // lower triangle of the diagonal block only
+    double s0 = 0.0;
+    if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam0; }
+    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - v;
+  } else if (lane < 42 && bi == bj) {
+    const int a = lane - 36;
+    d.bs[6 * bi + a] = d.bp[6 * bi + a] - v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
+  const double lam0 = d.lam_dev[1];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int blk = blockIdx.x * 4 + w;
-  if (blk >= nblk) return;
+  const int it = blockIdx.x * 4 + w;
+  if (it >= nitem) return;
+  const int blk = d.it_blk[it], c = d.it_chunk[it], slot = d.it_slot[it];
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
-  const int q0 = d.pr_ptr[blk], q1 = d.pr_ptr[blk + 1];
+  const int q0 = min(d.pr_ptr[blk] + c * kSchurChunk, d.pr_ptr[blk + 1]);
+  const int q1 = min(q0 + kSchurChunk, d.pr_ptr[blk + 1]);
   double acc[42];
 #pragma unroll
   for (int v = 0; v < 42; v++) acc[v] = 0.0;
@@ -480,12 +507,13 @@ __global__ __launch_bounds__(256) void k_schur(Dev d, double lam0, int nblk) {
 #pragma unroll
     for (int a = 0; a < 6; a++)
 #pragma unroll
-      for (int c = 0; c < 6; c++)
-        acc[6 * a + c] += y[3 * a] * bb[3 * c] + y[3 * a + 1] * bb[3 * c + 1] + y[3 * a + 2] * bb[3 * c + 2];
+      for (int cc = 0; cc < 6; cc++)
+        acc[6 * a + cc] += y[3 * a] * bb[3 * cc] + y[3 * a + 1] * bb[3 * cc + 1] + y[3 * a + 2] * bb[3 * cc + 2];
   }
   int nact = q1 - q0;
   if (bi == bj) {
-    const int e0 = d.ps_ptr[bi], e1 = d.ps_ptr[bi + 1];
+    const int e0 = min(d.ps_ptr[bi] + c * kSchurChunk, d.ps_ptr[bi + 1]);
+    const int e1 = min(e0 + kSchurChunk, d.ps_ptr[bi + 1]);
     nact = max(nact, e1 - e0);
     for (int q = e0 + lane; q < e1; q += 64) {
       const int e = d.ps_edges[q];
@@ -510,23 +538,29 @@ __global__ __launch_bounds__(256) void k_schur(Dev d, double lam0, int nblk) {
     const double sv = readlane0_d(acc[v]);
     if (lane == v) mine = sv;
   }
-  if (lane < 36) {
-    const int a = lane / 6, c = lane % 6;
-    if (bi == bj && c > a) return;   // lower triangle of the diagonal block only
-    double s0 = 0.0;
-    if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam0; }
-    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - mine;
-  } else if (lane < 42 && bi == bj) {
-    const int a = lane - 36;
-    d.bs[6 * bi + a] = d.bp[6 * bi + a] - mine;
-  }
+  if (slot < 0) schur_write(d, bi, bj, lam0, lane, mine);
+  else if (lane < 42) d.schur_part[(size_t)slot * 42 + lane] = mine;
+}
+
+// blocks split into several chunks: sum the chunk slots in chunk order, then write
+__global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nfin) {
+  const double lam0 = d.lam_dev[1];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + w;
+  if (f >= nfin) return;
+  const int blk = d.fin_blk[f], s0 = d.fin_slot0[f], n = d.fin_nch[f];
+  double v = 0.0;
+  if (lane < 42)
+    for (int c = 0; c < n; c++) v += d.schur_part[(size_t)(s0 + c) * 42 + lane];
+  schur_write(d, d.blk_i[blk], d.blk_j[blk], lam0, lane, v);
 }
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p); point = backup + x_l; model-decrease terms:
 // red[k] (points, k < nl) and red[nl + i] (poses) summed separately (poses are replicated
 // across shards, points are not).
-__global__ __launch_bounds__(256) void k_update(Dev d, double lam) {
+__global__ __launch_bounds__(256) void k_update(Dev d) {
   const int k = blockIdx.x * 256 + threadIdx.x;
+  const double lam = d.lam_dev[0];
   if (k < d.nl) {
     double c[3] = {d.bl[3 * k], d.bl[3 * k + 1], d.bl[3 * k + 2]};
     for (int q = d.pt_ptr[k]; q < d.pt_ptr[k + 1]; q++) {
@@ -606,7 +640,9 @@ namespace {
 
 struct HostStruct {
   std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
-      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2;
+      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, fin_blk,
+      fin_slot0, fin_nch;
+  int n_slots = 0;
   int np = 0, nl = 0;
 };
 
@@ -687,6 +723,27 @@ void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_
     s.pr_e1[q] = e1;
     s.pr_e2[q] = e2;
   });
+  // k_schur work items: chunks of kSchurChunk pairs (and, on diagonal blocks, pose edges)
+  s.it_blk.clear(); s.it_chunk.clear(); s.it_slot.clear();
+  s.fin_blk.clear(); s.fin_slot0.clear(); s.fin_nch.clear();
+  s.n_slots = 0;
+  for (size_t b = 0; b < nblk; b++) {
+    const int np_ = s.pr_ptr[b + 1] - s.pr_ptr[b];
+    int ne = 0;
+    if (s.blk_i[b] == s.blk_j[b]) ne = s.ps_ptr[s.blk_i[b] + 1] - s.ps_ptr[s.blk_i[b]];
+    const int nch = std::max(1, (std::max(np_, ne) + kSchurChunk - 1) / kSchurChunk);
+    if (nch > 1) {
+      s.fin_blk.push_back((int32_t)b);
+      s.fin_slot0.push_back(s.n_slots);
+      s.fin_nch.push_back(nch);
+    }
+    for (int c = 0; c < nch; c++) {
+      s.it_blk.push_back((int32_t)b);
+      s.it_chunk.push_back(c);
+      s.it_slot.push_back(nch > 1 ? s.n_slots + c : -1);
+    }
+    if (nch > 1) s.n_slots += nch;
+  }
 }
 
 template <typename T>
@@ -851,6 +908,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   d.npe = (int)s.pt_edges.size();
   d.ps_ptr = up(c, s.ps_ptr, he); d.ps_edges = up(c, s.ps_edges, he);
   d.blk_i = up(c, s.blk_i, he); d.blk_j = up(c, s.blk_j, he);
+  d.it_blk = up(c, s.it_blk, he); d.it_chunk = up(c, s.it_chunk, he); d.it_slot = up(c, s.it_slot, he);
+  d.fin_blk = up(c, s.fin_blk, he); d.fin_slot0 = up(c, s.fin_slot0, he); d.fin_nch = up(c, s.fin_nch, he);
   d.pr_ptr = up(c, s.pr_ptr, he); d.pr_e1 = up(c, s.pr_e1, he); d.pr_e2 = up(c, s.pr_e2, he);
   auto dz = [&](size_t cnt_) { double* q = (double*)c->alloc(std::max<size_t>(1, cnt_) * 8); if (!q) he = hipErrorOutOfMemory; return q; };
   d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
@@ -861,12 +920,15 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   d.S = sh.xchg + X.S; d.bs = sh.xchg + X.bs; d.hdiag = sh.xchg + X.hdiag; d.bpf = sh.xchg + X.bpf;
   d.xp = dz((size_t)ldlt::TB * T);
   d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
+  d.schur_part = dz((size_t)s.n_slots * 42);
   ldlt::Work lw;
   lw.L = dz(ldlt::tile_doubles(T));
   lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
   lw.z = dz((size_t)ldlt::TB * T);
   double* d_scalar = dz(8);
   double* d_part = dz(kRedPartMax);
+  double* d_lam = dz(2);
+  d.lam_dev = d_lam;
   int* d_flag = (int*)c->alloc(16);
   if (he != hipSuccess || !d_flag) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
 
@@ -894,6 +956,48 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     MCS_HIP_CHECK(hipMemcpyAsync(dl, sl, 24 * (size_t)p->n_points, hipMemcpyDeviceToDevice, st));
     return MCS_OK;
   };
+  // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda from pinned[6..7]
+  auto enqueue_trial = [&]() -> int {
+    int rc2;
+    MCS_HIP_CHECK(hipMemcpyAsync(d_lam, c->pinned + 6, 16, hipMemcpyHostToDevice, st));
+    if ((rc2 = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc2;  // push
+    rec(2);
+    hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d);
+    MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
+    if (s.np) {
+      const int nitem = (int)s.it_blk.size(), nfin = (int)s.fin_blk.size();
+      hipLaunchKernelGGL(k_schur, dim3((unsigned)((nitem + 3) / 4)), dim3(256), 0, st, d, nitem);
+      if (nfin)
+        hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nfin + 3) / 4)), dim3(256), 0, st, d, nfin);
+      MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
+      rec(3);
+      if ((rc2 = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc2;   // S tiles | bs
+      rec(4);
+      MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
+    } else {
+      rec(3); rec(4);
+    }
+    rec(5);
+    hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d);
+    reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
+    reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
+    hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
+    reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
+    rec(6);
+    return MCS_OK;
+  };
+  // graph replay of the trial: one rank (no exchange callback inside), no stage timing, and
+  // the LDL^T kernel attributes already set (the first trial of a call runs eagerly)
+  const bool use_graph = !sharded && !c->timing;
+  bool graph_ok = true;
+  int trial_no = 0;
+  hipGraphExec_t graph_exec = nullptr;
+  struct GraphGuard {
+    hipGraphExec_t* g;
+    ~GraphGuard() { if (*g) (void)hipGraphExecDestroy(*g); }
+  } graph_guard{&graph_exec};
   double chi0 = 0;
   if ((s.np + nl_glob) == 0 || nae_glob == 0) {
     if (rep) rep->chi2_initial = rep->chi2_final = 0;
@@ -930,31 +1034,32 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       double rho = 0;
       int qmax = 0;
       do {
-        if ((rc = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc;  // push
-        rec(2);
-        hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d, lambda);
-        MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
-        if (s.np) {
-          const int nblk = (int)s.blk_i.size();
-          hipLaunchKernelGGL(k_schur, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, d,
-                             sh.rank == 0 ? lambda : 0.0, nblk);
-          MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
-          rec(3);
-          if ((rc = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc;   // S tiles | bs
-          rec(4);
-          MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
-        } else {
-          rec(3); rec(4);
+        c->pinned[6] = lambda;
+        c->pinned[7] = sh.rank == 0 ? lambda : 0.0;
+        if (use_graph && !graph_exec && graph_ok && trial_no > 0) {
+          // the trial sequence is fixed within this call: capture it once, replay it per trial
+          // (lambda reaches the kernels through the captured pinned -> device copy)
+          hipGraph_t g = nullptr;
+          if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            graph_ok = false;
+          } else {
+            const int erc = enqueue_trial();
+            const hipError_t ce = hipStreamEndCapture(st, &g);
+            if (erc != MCS_OK || ce != hipSuccess || !g ||
+                hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0) != hipSuccess) {
+              graph_ok = false;
+              graph_exec = nullptr;
+              (void)hipGetLastError();
+            }
+            if (g) (void)hipGraphDestroy(g);
+          }
         }
-        rec(5);
-        hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d, lambda);
-        reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
-        reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
-        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-        reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
-        rec(6);
+        if (use_graph && graph_exec) {
+          MCS_HIP_CHECK(hipGraphLaunch(graph_exec, st));
+        } else if ((rc = enqueue_trial())) {
+          return rc;
+        }
+        trial_no++;
         MCS_HIP_CHECK(hipStreamSynchronize(st));
         if (c->timing) {
           if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
