@@ -98,20 +98,29 @@ __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
   return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)((uintptr_t)g & 3));
 }
 
-// Blurred patch (+-21 around the keypoint) staged with 16-byte loads: blurred levels have a
-// 64-byte-aligned pitch, so every row shares the misalignment mis = (cx - 21) & 15 and
-// 4 aligned chunks of 16 bytes cover the 43 bytes of a row.
+// Blurred patch (+-21 around the keypoint) staged in LDS rows of kBlrRow bytes.
+// Default: 16-byte loads (blurred levels have a 64-byte-aligned pitch, so every row shares
+// mis = (cx - 21) & 15 and 4 aligned 16-byte chunks cover a row: 64-byte LDS rows).
+// MCS_DESC_BLR48 (tuning variant, measured slower: 1.11 vs 0.89 ms/step): 12 aligned dwords
+// per row into 48-byte LDS rows, less LDS per keypoint but three times the load count.
+#ifndef MCS_DESC_BLR48
 constexpr int kBlrRow = 64;
+constexpr int kBlrAlign = 15;
+#else
+constexpr int kBlrRow = 48;
+constexpr int kBlrAlign = 3;
+#endif
 
-// IC moments of the raw patch staged in LDS (see c_icw); one half-wave (32 lanes) per
-// keypoint, sums reduced within the half (xor offsets < 32 never cross halves)
-__device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
+// IC moments of the raw patch (see c_icw); one half-wave (32 lanes) per keypoint: lane hl
+// holds patch dwords q = hl + 32k in registers (each dword is used by one lane only, so the
+// raw patch needs no LDS), sums reduced within the half (xor offsets < 32 never cross halves)
+__device__ __forceinline__ float ic_angle_regs(const uint32_t (&raw)[10], int hl) {
   uint32_t a10 = 0, aS = 0, a01 = 0;
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     const int q = hl + 32 * k;
     if (q < kRawH * kRawW) {
-      const uint32_t px = rawp[q];
+      const uint32_t px = raw[k];
       const uint32_t d1 = __builtin_amdgcn_udot4(c_icw[0][q], px, 0u, false);
       const uint32_t d0 = __builtin_amdgcn_udot4(c_icw[1][q], px, 0u, false);
       a10 += d1;
@@ -131,11 +140,21 @@ __device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
   return fast_atan2_dev((float)m01, (float)m10);
 }
 
+// same from a raw patch staged in LDS (dBRIEF path)
+__device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
+  uint32_t raw[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    const int q = hl + 32 * k;
+    raw[k] = (q < kRawH * kRawW) ? rawp[q] : 0u;
+  }
+  return ic_angle_regs(raw, hl);
+}
+
 // Two keypoints per wave, one per 32-lane half: the per-keypoint scalar work (level lookup,
 // fastAtan2, double sincos, keypoint record) runs once for both, the 8-32 test words of a
 // descriptor come from one 64-bit ballot per 32 tests (low half / high half).
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
-  __shared__ uint32_t s_raw[8][kRawH * kRawW];
   __shared__ __attribute__((aligned(16))) uint8_t s_blr[8][kBlrH * kBlrRow];
   // wave index as a scalar: the pair, its level and counts are wave-uniform
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -163,19 +182,22 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
                                 : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
   const uint8_t* blr = a.blur + (int64_t)f * a.blur_fstride + L.img_off;
-  // ---- stage both patches (independent loads, issued together)
-  const int mis = (cx - 21) & 15;
+  // ---- raw patch into registers, blurred patch into LDS (independent loads, issued together)
+  const int mis = (cx - 21) & kBlrAlign;
+  uint32_t raw[10];
   {
     const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
 #pragma unroll
     for (int k = 0; k < 10; k++) {
       const int q = hl + 32 * k;
+      raw[k] = 0u;
       if (q < kRawH * kRawW) {
         const int r = q / kRawW, c = q - kRawW * r;
-        s_raw[slot][q] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+        raw[k] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
       }
     }
     const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21 - mis);
+#ifndef MCS_DESC_BLR48
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       const int q = hl + 32 * k;        // chunk q: row q >> 2, 16-byte chunk q & 3
@@ -184,10 +206,30 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
         *reinterpret_cast<uint4*>(&s_blr[slot][(q >> 2) * kBlrRow + 16 * (q & 3)]) = v;
       }
     }
+#else
+    uint32_t bv[17];
+#pragma unroll
+    for (int k = 0; k < 17; k++) {      // dword q: row q / 12, dword q % 12
+      const int q = hl + 32 * k;
+      bv[k] = 0u;
+      if (q < kBlrH * 12) {
+        const int r = q / 12, c = q - 12 * r;
+        bv[k] = *reinterpret_cast<const uint32_t*>(b0 + (int64_t)r * bp + 4 * c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 17; k++) {
+      const int q = hl + 32 * k;
+      if (q < kBlrH * 12) {
+        const int r = q / 12, c = q - 12 * r;
+        *reinterpret_cast<uint32_t*>(&s_blr[slot][r * kBlrRow + 4 * c]) = bv[k];
+      }
+    }
+#endif
   }
   dev::wave_sync();
   // ---- IC_Angle: integer moments over the circular r=16 patch
-  const float angle = ic_angle_lds(s_raw[slot], hl);
+  const float angle = ic_angle_regs(raw, hl);
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
