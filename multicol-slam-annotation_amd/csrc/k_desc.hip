@@ -104,7 +104,10 @@ __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
 // MCS_DESC_BLR48 (tuning variant, measured slower: 1.11 vs 0.89 ms/step): 12 aligned dwords
 // per row into 48-byte LDS rows, less LDS per keypoint but three times the load count.
 #ifndef MCS_DESC_BLR48
-constexpr int kBlrRow = 64;
+#ifndef MCS_DESC_BLR_PITCH
+#define MCS_DESC_BLR_PITCH 64
+#endif
+constexpr int kBlrRow = MCS_DESC_BLR_PITCH;
 constexpr int kBlrAlign = 15;
 #else
 constexpr int kBlrRow = 48;

@@ -49,7 +49,7 @@ def main(fetch_csv, write_csv, out_json):
     k = out["kernels"]
     # per extractor call (= one k_fast_cells launch): every k_pyr_rows<true> launch of the call
     # (one per level 1..L-1: resize + fused blur) + the FAST launch
-    fa = k.get("k_fast_cells")
+    fa = next((v for n, v in k.items() if n.startswith("k_fast_cells")), None)
     rs = [v for n, v in k.items() if n.startswith("k_pyr_rows<true")]
     if rs and fa and fa["launches"]:
         calls = fa["launches"]

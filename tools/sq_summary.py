@@ -9,12 +9,14 @@ from collections import defaultdict
 
 acc = defaultdict(lambda: defaultdict(float))
 cnt = defaultdict(set)
-for row in csv.DictReader(open(sys.argv[1])):
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+path = args[0]
+for row in csv.DictReader(open(path)):
     k = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("mcs::", "")
     acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
     cnt[k].add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))
-print("# " + sys.argv[1])
-if "SQ_WAVE_CYCLES" in next(iter(acc.values()), {}):
+print("# " + path)
+if "SQ_ACTIVE_INST_ANY" in next(iter(acc.values()), {}):
     print("%-28s %6s %9s %8s %8s %8s %7s %7s %7s" % ("kernel", "disp", "waves", "valu/w", "lds/w",
                                                      "salu/w", "act%", "stall%", "park%"))
     for k, c in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
@@ -24,6 +26,20 @@ if "SQ_WAVE_CYCLES" in next(iter(acc.values()), {}):
             k[:28], len(cnt[k]), w, c.get("SQ_INSTS_VALU", 0) / w, c.get("SQ_INSTS_LDS", 0) / w,
             c.get("SQ_INSTS_SALU", 0) / w, 100 * c.get("SQ_ACTIVE_INST_ANY", 0) / wc,
             100 * c.get("SQ_WAIT_INST_ANY", 0) / wc, 100 * c.get("SQ_WAIT_ANY", 0) / wc))
+if "SQ_LDS_IDX_ACTIVE" in next(iter(acc.values()), {}):
+    # pass B: VALU-issue share of wave time, LDS bank-conflict cycles per LDS-array cycle,
+    # and SQ_LEVEL_WAVES / SQ_BUSY_CYCLES (mean resident waves per sampled SQ while busy)
+    print("%-28s %9s %8s %10s %10s %9s" % ("kernel", "waves", "valu%", "ldsconf/acc", "lvl/busy", "salu_cyc/w"))
+    for k, c in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+        w = c.get("SQ_WAVES", 0) or 1
+        wc = c.get("SQ_WAVE_CYCLES", 0) or 1
+        idx = c.get("SQ_LDS_IDX_ACTIVE", 0)
+        bc = c.get("SQ_LDS_BANK_CONFLICT", 0)
+        busy = c.get("SQ_BUSY_CYCLES", 0) or 1
+        print("%-28s %9d %8.1f %10.3f %10.2f %9.0f" % (
+            k[:28], w, 100 * c.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+            bc / (idx - bc) if idx > bc else 0.0, c.get("SQ_LEVEL_WAVES", 0) / busy,
+            c.get("SQ_INST_CYCLES_SALU", 0) / w))
 if "--all" in sys.argv:
     for k, c in sorted(acc.items()):
         if not k.startswith(("k_", "pyr", "fast", "ldlt", "ba::", "voc")) and "k_" not in k:
