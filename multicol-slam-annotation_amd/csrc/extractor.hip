@@ -41,6 +41,7 @@ struct mcs_extractor {
   int32_t* d_xofs = nullptr; int16_t* d_alpha = nullptr;
   int32_t* d_yofs = nullptr; int16_t* d_beta = nullptr;
   mcs::CellDesc* d_cells = nullptr;
+  mcs::FastUnit* d_units = nullptr;
   // workspace
   uint8_t* d_pyr = nullptr;      // [F][pyr_frame_bytes]   raw levels 1..L-1 (pitch align64)
   uint8_t* d_blur = nullptr;     // [F][img_frame_bytes]   blurred levels 0..L-1
@@ -124,7 +125,24 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   stage_mark(h, 1, st);
   launch_pyr_blur(pyr_args(0), false, false, st);  // blur of level 0 (the input frames)
   stage_mark(h, 2, st);
-  // K2: FAST cells
+  // K2: FAST (row-streaming runs of cells; -DMCS_FAST_CELLS selects the per-cell kernel)
+#ifndef MCS_FAST_CELLS
+  {
+    FastRowArgs fa;
+    fa.img0 = d_images; fa.img0_fstride = img0_fs;
+    fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
+    fa.mask_bits = mask_bits;
+    fa.mask_index = d_mask_index;
+    fa.units = h->d_units; fa.nunits = (int)pl.fast_units.size();
+    fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
+    fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
+    fa.cell_counts = h->d_cell_counts;
+    fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
+    fa.nframes = F;
+    fill_level_ptrs(pl, fa.lp);
+    launch_fast_rows(fa, st);
+  }
+#else
   {
     FastArgs fa;
     fa.img0 = d_images; fa.img0_fstride = img0_fs;
@@ -140,6 +158,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     fast_lds_layout(pl.max_win_w, pl.max_win_h, fa);
     launch_fast_cells(fa, st);
   }
+#endif
   MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));
   stage_mark(h, 3, st);
   // K3: octree
@@ -244,6 +263,7 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
   ALLOC(h->d_yofs, pl.yofs.size());
   ALLOC(h->d_beta, pl.beta.size());
   ALLOC(h->d_cells, pl.cells.size());
+  ALLOC(h->d_units, pl.fast_units.size());
   ALLOC(h->d_pyr, F * pl.pyr_frame_bytes);
   ALLOC(h->d_blur, F * pl.img_frame_bytes);
   ALLOC(h->d_slots, F * pl.slots_per_frame);
@@ -266,6 +286,7 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
   if (e == hipSuccess) e = hipMemcpy(h->d_yofs, pl.yofs.data(), pl.yofs.size() * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(h->d_beta, pl.beta.data(), pl.beta.size() * 2, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(h->d_cells, pl.cells.data(), pl.cells.size() * sizeof(CellDesc), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(h->d_units, pl.fast_units.data(), pl.fast_units.size() * sizeof(FastUnit), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     set_hip_error(e, "upload plan tables", __FILE__, __LINE__);
     mcs_extractor_destroy(h);
@@ -278,7 +299,7 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
 void mcs_extractor_destroy(mcs_extractor* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_pyr, h->d_blur,
+  void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_units, h->d_pyr, h->d_blur,
                   h->d_slots, h->d_cell_counts, h->d_cand, h->d_cnode, h->d_sel, h->d_sel_count,
                   h->d_mask_pyr, h->d_mask_bits, h->d_mask_single, h->d_bits_single, h->d_in,
                   h->d_kps, h->d_desc, h->d_count, h->d_dmask, h->d_cams};

@@ -96,6 +96,23 @@ inline void fast_lds_layout(int max_ww, int max_wh, FastArgs& a) {
 }
 void launch_fast_cells(const FastArgs& a, hipStream_t st);
 
+// ---- K2 (row-streaming form): FAST over runs of cells, one wave per FastUnit
+struct FastRowArgs {
+  const uint8_t* img0; int64_t img0_fstride;
+  const uint8_t* pyr; int64_t pyr_fstride;
+  const uint64_t* mask_bits;                     // [mask][cell][64] (nullable = no mask)
+  const int32_t* mask_index;
+  const FastUnit* units; int nunits;
+  const CellDesc* cells; int ncells;
+  uint32_t* slots; int64_t slots_fstride;
+  int32_t* cell_counts;
+  int threshold;
+  uint32_t kk, rbits;
+  int nframes;
+  LevelPtrs lp;
+};
+void launch_fast_rows(const FastRowArgs& a, hipStream_t st);
+
 // ---- K3: octree
 struct OctArgs {
   LevelPlan lv[kMaxLevels];

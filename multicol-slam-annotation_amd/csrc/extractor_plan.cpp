@@ -76,7 +76,7 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
   int64_t pyr_off = 0, img_off = 0, mask_off = 0;
   auto align = [](int64_t v, int64_t a) { return (v + a - 1) / a * a; };
   int32_t slot = 0, sel = 0;
-  pl.cells.clear(); pl.xofs.clear(); pl.yofs.clear(); pl.alpha.clear(); pl.beta.clear();
+  pl.cells.clear(); pl.fast_units.clear(); pl.xofs.clear(); pl.yofs.clear(); pl.alpha.clear(); pl.beta.clear();
   pl.xtab_off.assign(p.nlevels, 0); pl.ytab_off.assign(p.nlevels, 0);
   pl.max_cells_level = 0;
   for (int l = 0; l < p.nlevels; l++) {
@@ -154,6 +154,36 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     }
     L.cell_end = (int32_t)pl.cells.size();
     L.cand_cap = slot - L.cand_off;
+    // k_fast_rows work units: every cell row split into the fewest equal runs of cells whose
+    // detection span (+3 px halo each side) fits one wave's lanes 0..62
+    for (int c = L.cell_begin; c < L.cell_end;) {
+      int e = c;
+      while (e < L.cell_end && pl.cells[e].wy0 == pl.cells[c].wy0) e++;
+      const int n = e - c;
+      auto fits = [&](int a, int b) {
+        const int xa = (pl.cells[a].wx0 - 3) & ~3;
+        return pl.cells[b - 1].wx1 + 3 <= xa + kFastUnitSpan;
+      };
+      for (int runs = 1; runs <= n; runs++) {
+        const int per = (n + runs - 1) / runs;
+        bool ok = true;
+        for (int a = c; a < e && ok; a += per) ok = fits(a, std::min(e, a + per));
+        if (!ok) continue;
+        for (int a = c; a < e; a += per) {
+          const int b = std::min(e, a + per);
+          FastUnit u;
+          u.level = (int16_t)l; u.ncells = (int16_t)(b - a);
+          u.wy0 = pl.cells[a].wy0; u.wy1 = pl.cells[a].wy1;
+          u.ux0 = pl.cells[a].wx0; u.ux1 = pl.cells[b - 1].wx1;
+          u.xa = (int16_t)((u.ux0 - 3) & ~3);
+          u.wcell = (int16_t)wCell;
+          u.cell0 = a;
+          pl.fast_units.push_back(u);
+        }
+        break;
+      }
+      c = e;
+    }
     pl.max_cells_level = std::max(pl.max_cells_level, L.cell_end - L.cell_begin);
     if (L.cell_end - L.cell_begin > kMaxCellsPerLevel) {
       set_error("too many FAST cells in one level");

@@ -28,6 +28,20 @@ struct CellDesc {
   int32_t slot_cap;            // ceil(ww/2)*ceil(wh/2): max survivors of strict 8-NMS
 };
 
+// One work unit of the row-streaming FAST kernel (k_fast_rows): a run of consecutive cells of
+// one cell row of one level.  Lane L of the wave holds columns [xa + 4L, xa + 4L + 4); the run
+// is sized so that every detection pixel's 7x7 neighbourhood lies in lanes 0..62
+// (ux0 - 3 >= xa, ux1 + 3 <= xa + 252).  Cell k of the run starts at ux0 + k * wcell (every
+// cell of a level is wcell wide except a clamped last one, which ends at ux1).
+struct FastUnit {
+  int16_t level, ncells;
+  int16_t wy0, wy1;    // detection rows of the cell row
+  int16_t ux0, ux1;    // detection columns [first cell wx0, last cell wx1)
+  int16_t xa, wcell;
+  int32_t cell0;       // global index of the run's first cell
+};
+constexpr int kFastUnitSpan = 252;   // lanes 0..62 x 4 px
+
 struct LevelPlan {
   int32_t w, h;               // level size (cvRound(W / 1.2^l))
   int32_t pitch;              // row pitch of raw level l (level 0: the input width) and of
@@ -54,6 +68,7 @@ struct Plan {
   double scale_factor = 1.2;  // double((float)p.scale_factor)  (:147)
   LevelPlan lv[kMaxLevels];
   std::vector<CellDesc> cells;
+  std::vector<FastUnit> fast_units;
   int64_t pyr_frame_bytes = 0;   // levels 1..L-1
   int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred levels, padded pitch)
   int64_t mask_frame_bytes = 0;  // levels 0..L-1 (mask pyramid, pitch bpitch)

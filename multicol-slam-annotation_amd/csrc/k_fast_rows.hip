@@ -1,0 +1,329 @@
+// K2, row-streaming form: FAST-9/16 + cell-local 3x3 non-max suppression + runByPixelsMask
+// over a run of consecutive cells of one cell row (FastUnit), one wave per run.
+//
+// Reference: ComputeKeyPointsOctTree src/mdBRIEFextractorOct.cpp:874-949, which runs
+// FastFeatureDetector(th, nonmax, TYPE_9_16)::detect on every 30 px cell ROI (OpenCV semantics
+// of FAST_t<16>, cornerScore<16> and NMS-before-mask pinned in SURVEY A.4).
+//
+// Why one pass over the run gives the per-cell results: the corner test and cornerScore of a
+// pixel read only its 16-circle, never the ROI, and with the one threshold t a corner's score
+// max(t, dark, bright) - 1 is max(dark, bright) - 1.  The ROI decides only which neighbours
+// take part in the NMS: those inside the same cell's detection window (rows outside it and
+// columns across a cell border count as non-corners).  So every pixel is tested once, and
+// only the NMS looks at cell borders.
+//
+// The run is streamed in bands of kBand detection rows:
+//   load  the band's new raw rows (one dword per lane, issued one band ahead) enter a
+//         register window (rows y0-3 .. y0+kBand+2) and a 16-row LDS ring; with a 256 B row
+//         stride the ring address of pixel (y, x) + (dy, dx) is ((y << 8 | x) + (dy << 8) + dx)
+//         & 0xFFF
+//   A     compass pre-test per quad from the register window, 4 pixels per lane
+//         (k_fast_cells phase A), survivors -> list in raster order
+//   B     exact test + score of the survivors in full 64-lane batches from the ring: score + 1
+//         into an 8-row score ring, corners compacted in place (raster order)
+//   C     NMS of every corner whose lower neighbour row is scored (the band's last row waits
+//         for the next band), the mask bit, and the append to the cell's slot list: raster
+//         order within a cell, the order OpenCV's FAST emits them in.
+#include "common.hpp"
+#include "extractor_kernels.hpp"
+
+namespace mcs {
+
+namespace {
+constexpr int kBand = 4;
+// LDS: the four waves' raw rings (16 x 256 B, 4 KB aligned), then their score rings (8 x 256 B,
+// 2 KB aligned), then their lists (carried corners, then the band's survivors, compacted in
+// place into its corners).  The alignment lets a ring address be (offset & mask) | base.
+constexpr int kRingBytes = 4096, kScoreBytes = 2048;
+constexpr int kListCap = 256 + kBand * 256;
+constexpr int kScoreBase = 4 * kRingBytes, kListBase = kScoreBase + 4 * kScoreBytes;
+constexpr int kLdsBytes = kListBase + 4 * 2 * kListCap;
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// packed f16 min3 / max3 (v_pk_minimum3_f16 / v_pk_maximum3_f16 on gfx950); all operands are
+// integers in [-255, 255] here, exact in f16
+__device__ __forceinline__ h2 hmin3(h2 a, h2 b, h2 c) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
+__device__ __forceinline__ int fr_max3(int a, int b, int c) { return max(max(a, b), c); }
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
+  __shared__ __attribute__((aligned(4096))) uint8_t lds[kLdsBytes];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t ring_base = (uint32_t)wv * kRingBytes;
+  const uint32_t sc_base = kScoreBase + (uint32_t)wv * kScoreBytes;
+  uint32_t* const ring32 = reinterpret_cast<uint32_t*>(lds + ring_base);
+  uint8_t* const sc8 = lds + sc_base;
+  uint16_t* const list = reinterpret_cast<uint16_t*>(lds + kListBase + wv * 2 * kListCap);
+  // score-ring byte of pixel e = (y << 8 | x) moved by (dy, dx)
+  auto sc_at = [&](int e, int dy, int dx) -> uint8_t& {
+    return lds[((uint32_t)(e + dy * 256 + dx) & 0x7FFu) | sc_base];
+  };
+  int f, item;
+  if (!xcd_frame_map(blockIdx.x, a.nframes, (a.nunits + 3) / 4, &f, &item)) return;
+  const int ui = item * 4 + wv;
+  if (ui >= a.nunits) return;
+  const FastUnit u = a.units[ui];
+  const int level = u.level, nc = u.ncells, wh = u.wy1 - u.wy0;
+  int32_t* const cnt_out = a.cell_counts + (int64_t)f * a.ncells + u.cell0;
+  if (wh <= 0) {
+    if (lane < nc) cnt_out[lane] = 0;
+    return;
+  }
+  const uint64_t* const mbits =
+      a.mask_bits ? a.mask_bits + ((int64_t)(a.mask_index ? a.mask_index[f] : 0) * a.ncells + u.cell0) *
+                                      kMaskBitRows
+                  : nullptr;
+  const int t = a.threshold;
+  const int xa = u.xa, wc = u.wcell, span = u.ux1 - u.ux0;
+  const uint32_t magic = 65536u / (uint32_t)wc + 1u;   // cx / wc for cx < 256, wc <= 64
+  const int pitch = a.lp.pitch[level];
+  const uint8_t* const img = (level == 0) ? a.img0 + (int64_t)f * a.img0_fstride
+                                          : a.pyr + (int64_t)f * a.pyr_fstride + a.lp.pyr_off[level];
+  const uint8_t* const row0 = img + (int64_t)(u.wy0 - 3) * pitch + xa;
+  const int nraw = wh + 6;   // raw rows y_rel in [0, wh + 6); detection rows [3, wh + 3)
+
+  // top bit of byte k: pixel xa + 4 lane + k is a detection pixel of the run
+  uint32_t detm = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int x = xa + 4 * lane + k;
+    detm |= (x >= u.ux0 && x < u.ux1) ? (0x80u << (8 * k)) : 0u;
+  }
+  const int slot_off = lane < nc ? a.cells[u.cell0 + lane].slot_off : 0;   // lane k: cell k
+  uint32_t* const outf = a.slots + (int64_t)f * a.slots_fstride;
+  int cnt = 0;                                                            // lane k: cell k
+
+  // raw row r (y_rel) of the run: one aligned dword per lane, the row's byte offset undone by
+  // alignbyte with the next lane's dword (lane 63 is never consumed)
+  auto load_row = [&](int r) -> uint32_t {
+    return dev::align_down4(row0 + (int64_t)min(r, nraw - 1) * pitch)[lane];
+  };
+  auto fix_row = [&](int r, uint32_t own) -> uint32_t {
+    const uint32_t sh = (uint32_t)((uintptr_t)(row0 + (int64_t)min(r, nraw - 1) * pitch) & 3);
+    const uint32_t nxt = __builtin_amdgcn_update_dpp(0u, own, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
+    return __builtin_amdgcn_alignbyte(nxt, own, sh);
+  };
+  auto put_row = [&](int r, uint32_t v) { ring32[((r & 15) << 6) + lane] = v; };
+
+  // the score ring starts zeroed: rows outside the detection window read as non-corners
+  *reinterpret_cast<uint4*>(sc8 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
+  *reinterpret_cast<uint4*>(sc8 + 1024 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
+  // register window: rows y0 - 3 .. y0 + 2 of the current band (the compass reads registers;
+  // the exact test reads the ring)
+  uint32_t w[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) w[i] = load_row(i);
+  uint32_t pf[kBand];
+#pragma unroll
+  for (int i = 0; i < kBand; i++) pf[i] = load_row(6 + i);
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    w[i] = fix_row(i, w[i]);
+    put_row(i, w[i]);
+  }
+
+  const int nbands = (wh + kBand - 1) / kBand;
+  int ncarry = 0;   // corners of the previous band's last row, at the front of the list
+  for (int b = 0; b < nbands; b++) {
+    const int y0 = 3 + b * kBand, y1 = min(y0 + kBand, 3 + wh);
+    // rows y0 + 3 .. y0 + kBand + 2 arrive; the next band's rows go in flight
+    uint32_t rows[6 + kBand];
+#pragma unroll
+    for (int i = 0; i < 6; i++) rows[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < kBand; i++) {
+      rows[6 + i] = fix_row(y0 + 3 + i, pf[i]);
+      put_row(y0 + 3 + i, rows[6 + i]);
+    }
+    if (b + 1 < nbands) {
+#pragma unroll
+      for (int i = 0; i < kBand; i++) pf[i] = load_row(y0 + kBand + 3 + i);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) w[i] = rows[kBand + i];
+    // zero this band's score rows (kBand x 256 B: one 16-byte store per lane) and the row
+    // below them: on the last band that row lies below the window and must read as zero (its
+    // ring slot held row y0 - 4, which no NMS of this band reads)
+    *reinterpret_cast<uint4*>(sc8 + (((y0 + (lane >> 4)) & 7) << 8) + 16 * (lane & 15)) =
+        make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint32_t*>(sc8 + (((y0 + kBand) & 7) << 8) + 4 * lane) = 0u;
+
+    // ---- A: compass pre-test (k_fast_cells phase A) from the register window, survivors
+    // appended after the carried corners in raster order
+    int ns = 0;
+    const uint64_t lt = dev::lanemask_lt();
+#pragma unroll
+    for (int i = 0; i < kBand; i++) {
+      const int y = y0 + i;
+      const uint32_t c1 = rows[i + 3], up = rows[i] /* q8 */, dn = rows[i + 6] /* q0 */;
+      const uint32_t L = __builtin_amdgcn_update_dpp(0u, c1, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
+      const uint32_t R = __builtin_amdgcn_update_dpp(0u, c1, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
+      const uint32_t rt = __builtin_amdgcn_alignbyte(R, c1, 3u);   // q4: x+3..x+6
+      const uint32_t lf = __builtin_amdgcn_alignbyte(c1, L, 1u);   // q12: x-3..x
+      const uint32_t nv = ~c1;
+      auto dk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c1, ~q, a.rbits), a.kk, 0u); };
+      auto bk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(q, nv, a.rbits), a.kk, 0u); };
+      const uint32_t s = (y < y1) ? ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
+                                      ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm)
+                                  : 0u;
+      const bool s0 = (s & 0x80u) != 0, s1 = (s & 0x8000u) != 0;
+      const bool s2 = (s & 0x800000u) != 0, s3 = (s & 0x80000000u) != 0;
+      const uint64_t b0 = __ballot(s0), b1 = __ballot(s1), b2 = __ballot(s2), b3 = __ballot(s3);
+      int pos = ncarry + ns + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+      const int idx = (y << 8) | (4 * lane);
+      if (s0) list[pos] = (uint16_t)idx;
+      pos += s0;
+      if (s1) list[pos] = (uint16_t)(idx + 1);
+      pos += s1;
+      if (s2) list[pos] = (uint16_t)(idx + 2);
+      pos += s2;
+      if (s3) list[pos] = (uint16_t)(idx + 3);
+      ns += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+    }
+    dev::wave_sync();
+
+    // ---- B: exact FAST test + score of the survivors, two per lane (batch j0: survivors
+    // j0 + lane and j0 + 64 + lane in the low / high halves).  With d_k = v - p_k, cornerScore's
+    // darkest 9-arc max_k min(d_k..d_k+8) is v - min_k max(p_k..p_k+8) and the brightest
+    // max_k min(p_k..p_k+8) - v; both extrema run on the raw pixel pairs as f16 bit patterns
+    // (0..255 are f16 denormals, ordered like the integers; the kernel keeps f16 denormals) by
+    // packed min3/max3 doubling.  corner <=> dark > t or bright > t, score + 1 =
+    // max(t, dark, bright).  Corners are compacted in place behind the carried ones (write
+    // index <= read index, all reads of a batch precede its writes): raster order is kept.
+    int ncorn = ncarry, nlast = 0;   // nlast: corners on the band's last row
+    for (int j0 = 0; j0 < ns; j0 += 128) {
+      const int ja = j0 + lane, jb = j0 + 64 + lane;
+      const int ea = list[ncarry + min(ja, ns - 1)], eb = list[ncarry + min(jb, ns - 1)];
+      // ring rows y-3 .. y+3 of both survivors, pointing at column x - 3
+      uint32_t ra[7], rb[7];
+#pragma unroll
+      for (int i = 0; i < 7; i++) {
+        ra[i] = ((uint32_t)(ea + (i - 3) * 256 - 3) & 0xFFFu) | ring_base;
+        rb[i] = ((uint32_t)(eb + (i - 3) * 256 - 3) & 0xFFFu) | ring_base;
+      }
+      auto pix = [&](int dy, int dx) -> h2 {
+        const uint32_t pa = lds[ra[dy + 3] + dx + 3], pb = lds[rb[dy + 3] + dx + 3];
+        return __builtin_bit_cast(h2, pa | (pb << 16));
+      };
+      h2 p[16];
+      // circle (dx,dy): (0,3),(1,3),(2,2),(3,1),(3,0),(3,-1),(2,-2),(1,-3),(0,-3),(-1,-3),
+      //                 (-2,-2),(-3,-1),(-3,0),(-3,1),(-2,2),(-1,3)
+      p[0] = pix(3, 0);   p[1] = pix(3, 1);   p[2] = pix(2, 2);   p[3] = pix(1, 3);
+      p[4] = pix(0, 3);   p[5] = pix(-1, 3);  p[6] = pix(-2, 2);  p[7] = pix(-3, 1);
+      p[8] = pix(-3, 0);  p[9] = pix(-3, -1); p[10] = pix(-2, -2); p[11] = pix(-1, -3);
+      p[12] = pix(0, -3); p[13] = pix(1, -3); p[14] = pix(2, -2); p[15] = pix(3, -1);
+      const int va = lds[ra[3] + 3], vb = lds[rb[3] + 3];
+      h2 mx[16], mn[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        mx[k] = hmax3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+        mn[k] = hmin3(p[k], p[(k + 1) & 15], p[(k + 2) & 15]);
+      }
+      h2 amx[16], amn[16];   // max / min over the 9-arc starting at k
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        amx[k] = hmax3(mx[k], mx[(k + 3) & 15], mx[(k + 6) & 15]);
+        amn[k] = hmin3(mn[k], mn[(k + 3) & 15], mn[(k + 6) & 15]);
+      }
+#pragma unroll
+      for (int n = 16; n > 1; n = (n + 2) / 3) {   // 16 -> 6 -> 2 -> 1: min_k amx, max_k amn
+#pragma unroll
+        for (int k = 0; k < (n + 2) / 3; k++) {
+          const h2 x1 = amx[3 * k], y1v = amn[3 * k];
+          const h2 x2 = 3 * k + 1 < n ? amx[3 * k + 1] : x1, y2 = 3 * k + 1 < n ? amn[3 * k + 1] : y1v;
+          const h2 x3 = 3 * k + 2 < n ? amx[3 * k + 2] : x1, y3 = 3 * k + 2 < n ? amn[3 * k + 2] : y1v;
+          amx[k] = hmin3(x1, x2, x3);
+          amn[k] = hmax3(y1v, y2, y3);
+        }
+      }
+      const uint32_t bmx = __builtin_bit_cast(uint32_t, amx[0]), bmn = __builtin_bit_cast(uint32_t, amn[0]);
+      const int dark_a = va - (int)(bmx & 0xFFFFu), dark_b = vb - (int)(bmx >> 16);
+      const int bright_a = (int)(bmn & 0xFFFFu) - va, bright_b = (int)(bmn >> 16) - vb;
+      const bool ca = ja < ns && (dark_a > t || bright_a > t);
+      const bool cb = jb < ns && (dark_b > t || bright_b > t);
+      if (ca) sc_at(ea, 0, 0) = (uint8_t)max(max(t, dark_a), bright_a);   // score + 1
+      if (cb) sc_at(eb, 0, 0) = (uint8_t)max(max(t, dark_b), bright_b);
+      const uint64_t bal_a = __ballot(ca);
+      if (ca) list[ncorn + __popcll(bal_a & lt)] = (uint16_t)ea;
+      ncorn += __popcll(bal_a);
+      const uint64_t bal_b = __ballot(cb);
+      if (cb) list[ncorn + __popcll(bal_b & lt)] = (uint16_t)eb;
+      ncorn += __popcll(bal_b);
+      nlast += __popcll(__ballot(ca && (ea >> 8) == y1 - 1)) + __popcll(__ballot(cb && (eb >> 8) == y1 - 1));
+    }
+    dev::wave_sync();
+
+    // ---- C: NMS (3x3 within the cell) + runByPixelsMask + append to the cell's slots
+    const bool last_band = b + 1 == nbands;
+    const int nproc = last_band ? ncorn : ncorn - nlast;
+    for (int j0 = 0; j0 < nproc; j0 += 64) {
+      const int j = j0 + lane;
+      bool keep = false;
+      int k = 0;
+      uint32_t rec = 0;
+      if (j < nproc) {
+        const int e = list[j], y = e >> 8, x = e & 0xFF;
+        const int cx = xa + x - u.ux0;
+        k = (int)(((uint32_t)cx * magic) >> 16);
+        const int cs = k * wc, ce = min(cs + wc, span);
+        auto sv = [&](int dy, int dx) -> int { return sc_at(e, dy, dx); };
+        const int e0 = sv(0, 0);
+        int mx = max(sv(-1, 0), sv(1, 0));
+        if (cx > cs) mx = max(mx, fr_max3(sv(-1, -1), sv(0, -1), sv(1, -1)));
+        if (cx + 1 < ce) mx = max(mx, fr_max3(sv(-1, 1), sv(0, 1), sv(1, 1)));
+        keep = e0 >= 2 && e0 > mx;   // score > 0 and > every in-cell neighbour's score
+        if (mbits && keep) keep = ((mbits[(int64_t)k * kMaskBitRows + (y - 3)] >> (cx - cs)) & 1u) != 0;
+        rec = (uint32_t)(xa + x - kMinBorder) | ((uint32_t)(u.wy0 + y - 3 - kMinBorder) << 12) |
+              ((uint32_t)(e0 - 1) << 24);
+      }
+      uint64_t bk = __ballot(keep);
+      while (bk) {   // one pass per distinct cell among the batch's keypoints
+        const int kc = __builtin_amdgcn_readlane(k, (int)__builtin_ctzll(bk));
+        const bool mine = keep && k == kc;
+        const uint64_t bm = __ballot(mine);
+        const int base = __builtin_amdgcn_readlane(cnt, kc) + __builtin_amdgcn_readlane(slot_off, kc);
+        if (mine) outf[base + __popcll(bm & lt)] = rec;
+        if (lane == kc) cnt += __popcll(bm);
+        bk &= ~bm;
+      }
+    }
+    ncarry = 0;
+    if (!last_band && nlast > 0) {   // the band's last-row corners move to the front
+      uint32_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int jj = lane + 64 * i;
+        v[i] = jj < nlast ? list[nproc + jj] : 0u;
+      }
+      dev::wave_sync();
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int jj = lane + 64 * i;
+        if (jj < nlast) list[jj] = (uint16_t)v[i];
+      }
+      ncarry = nlast;
+    }
+    dev::wave_sync();
+  }
+  if (lane < nc) cnt_out[lane] = cnt;
+}
+
+void launch_fast_rows(const FastRowArgs& a_in, hipStream_t st) {
+  FastRowArgs a = a_in;
+  // byte-wise compare constants of the compass pre-test (k_fast.hip, launch_fast_cells)
+  const int t = a.threshold;
+  const uint32_t r = (uint32_t)(t & 1), K = (uint32_t)(t + 256 + (int)r) / 2;
+  a.rbits = r * 0x01010101u;
+  a.kk = (K <= 255 ? (~(K - 1) & 0xFFu) : 0u) * 0x01010101u;
+  const unsigned g = xcd_grid(a.nframes, (a.nunits + 3) / 4);
+  hipLaunchKernelGGL(k_fast_rows, dim3(g), dim3(256), 0, st, a);
+}
+
+}  // namespace mcs
