@@ -533,12 +533,13 @@ def main():
     stage_ms = {}
     if ncalls:
         stage_ms = {k: v / ncalls for k, v in stages.items()}
-        # pyramid + FAST = k_pyr_rows<true> x (L-1) (resize + fused blur) + k_fast_cells; the
-        # level-0 blur launch is not part of the algorithmic bytes and is not timed
+        # pyramid + FAST = k_pyr_rows<true> x (L-1) (resize + fused blur) + k_fast_rows (all
+        # levels, one launch); the level-0 blur launch is not part of the algorithmic bytes
+        #  and is not timed
         t_pf = (stage_ms["pyramid"] + stage_ms["fast"]) / 1e3
         achieved = bpf * F / t_pf / 1e9
         roofline = {"kernel": "pyramid+fast: k_pyr_rows<true> x %d (resize + 5x5 blur) + "
-                              "k_fast_cells (FAST-9/16 + cell-local NMS + mask)" % (len(wh) - 1),
+                              "k_fast_rows (FAST-9/16 + cell-local NMS + mask)" % (len(wh) - 1),
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None, "alg_bytes_per_call": bpf * F}

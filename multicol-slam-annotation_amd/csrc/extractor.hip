@@ -118,47 +118,35 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     a.nframes = F;
     return a;
   };
-  stage_mark(h, 0, st);
-  // K1+K5: resize chain, each level blurred in the same pass
+  // K2 arguments (row-streaming FAST; one launch per level, units of a level are contiguous)
+  FastRowArgs fa;
+  fa.img0 = d_images; fa.img0_fstride = img0_fs;
+  fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
+  fa.mask_pyr = mask_pyr; fa.mask_fstride = pl.mask_frame_bytes;
+  fa.mask_index = d_mask_index;
+  fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
+  fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
+  fa.cell_counts = h->d_cell_counts;
+  fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
+  fa.nframes = F;
+  fill_level_ptrs(pl, fa.lp);
+  (void)mask_bits;
   const bool wide = pl.scale_factor > 1.5;
+  // Schedule (one stream): the resize chain K1+K5 level by level, the level-0 blur, then FAST
+  // of every level in one launch.  (FAST per level on a second stream beside the chain was
+  // measured slower: 1.85 -> 2.0-2.1 ms per step; the chain then loses its Infinity-Cache
+  // reuse of level l-1 and its CU slots.)
+  stage_mark(h, 0, st);
   for (int l = 1; l < nl; l++) launch_pyr_blur(pyr_args(l), true, wide, st);
   stage_mark(h, 1, st);
   launch_pyr_blur(pyr_args(0), false, false, st);  // blur of level 0 (the input frames)
   stage_mark(h, 2, st);
-  // K2: FAST (row-streaming runs of cells; -DMCS_FAST_CELLS selects the per-cell kernel)
-#ifndef MCS_FAST_CELLS
   {
-    FastRowArgs fa;
-    fa.img0 = d_images; fa.img0_fstride = img0_fs;
-    fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
-    fa.mask_bits = mask_bits;
-    fa.mask_index = d_mask_index;
-    fa.units = h->d_units; fa.nunits = (int)pl.fast_units.size();
-    fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
-    fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
-    fa.cell_counts = h->d_cell_counts;
-    fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
-    fa.nframes = F;
-    fill_level_ptrs(pl, fa.lp);
-    launch_fast_rows(fa, st);
+    FastRowArgs fl = fa;
+    fl.units = h->d_units;
+    fl.nunits = (int)pl.fast_units.size();
+    launch_fast_rows(fl, st);
   }
-#else
-  {
-    FastArgs fa;
-    fa.img0 = d_images; fa.img0_fstride = img0_fs;
-    fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
-    fa.mask_bits = mask_bits;
-    fa.mask_index = d_mask_index;
-    fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
-    fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
-    fa.cell_counts = h->d_cell_counts;
-    fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
-    fa.nframes = F;
-    fill_level_ptrs(pl, fa.lp);
-    fast_lds_layout(pl.max_win_w, pl.max_win_h, fa);
-    launch_fast_cells(fa, st);
-  }
-#endif
   MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));
   stage_mark(h, 3, st);
   // K3: octree

@@ -100,7 +100,7 @@ void launch_fast_cells(const FastArgs& a, hipStream_t st);
 struct FastRowArgs {
   const uint8_t* img0; int64_t img0_fstride;
   const uint8_t* pyr; int64_t pyr_fstride;
-  const uint64_t* mask_bits;                     // [mask][cell][64] (nullable = no mask)
+  const uint8_t* mask_pyr; int64_t mask_fstride;  // mask pyramids (nullable = no mask)
   const int32_t* mask_index;
   const FastUnit* units; int nunits;
   const CellDesc* cells; int ncells;

@@ -154,6 +154,7 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     }
     L.cell_end = (int32_t)pl.cells.size();
     L.cand_cap = slot - L.cand_off;
+    pl.unit_begin[l] = (int32_t)pl.fast_units.size();
     // k_fast_rows work units: every cell row split into the fewest equal runs of cells whose
     // detection span (+3 px halo each side) fits one wave's lanes 0..62
     for (int c = L.cell_begin; c < L.cell_end;) {
@@ -210,6 +211,7 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     L.sel_cap = cap;
     sel += cap;
   }
+  for (int l = p.nlevels; l <= kMaxLevels; l++) pl.unit_begin[l] = (int32_t)pl.fast_units.size();
   pl.pyr_frame_bytes = pyr_off;
   pl.img_frame_bytes = img_off;
   pl.mask_frame_bytes = mask_off;

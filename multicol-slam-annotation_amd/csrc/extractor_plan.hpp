@@ -68,7 +68,8 @@ struct Plan {
   double scale_factor = 1.2;  // double((float)p.scale_factor)  (:147)
   LevelPlan lv[kMaxLevels];
   std::vector<CellDesc> cells;
-  std::vector<FastUnit> fast_units;
+  std::vector<FastUnit> fast_units;       // sorted by level
+  int32_t unit_begin[kMaxLevels + 1] = {};  // first unit of each level
   int64_t pyr_frame_bytes = 0;   // levels 1..L-1
   int64_t img_frame_bytes = 0;   // levels 0..L-1 (blurred levels, padded pitch)
   int64_t mask_frame_bytes = 0;  // levels 0..L-1 (mask pyramid, pitch bpitch)

@@ -76,10 +76,12 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     if (lane < nc) cnt_out[lane] = 0;
     return;
   }
-  const uint64_t* const mbits =
-      a.mask_bits ? a.mask_bits + ((int64_t)(a.mask_index ? a.mask_index[f] : 0) * a.ncells + u.cell0) *
-                                      kMaskBitRows
-                  : nullptr;
+  // mask rows of the run (the level of the frame's mask pyramid, pitch bpitch: aligned dwords)
+  const uint8_t* const mrow0 =
+      a.mask_pyr ? a.mask_pyr + (int64_t)(a.mask_index ? a.mask_index[f] : 0) * a.mask_fstride +
+                       a.lp.mask_off[level] + (int64_t)(u.wy0 - 3) * a.lp.bpitch[level] + u.xa
+                 : nullptr;
+  const int mpitch = a.lp.bpitch[level];
   const int t = a.threshold;
   const int xa = u.xa, wc = u.wcell, span = u.ux1 - u.ux0;
   const uint32_t magic = 65536u / (uint32_t)wc + 1u;   // cx / wc for cx < 256, wc <= 64
@@ -111,6 +113,11 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     return __builtin_amdgcn_alignbyte(nxt, own, sh);
   };
   auto put_row = [&](int r, uint32_t v) { ring32[((r & 15) << 6) + lane] = v; };
+  // mask bytes of raw row r (all 0xFF without a mask)
+  auto load_mrow = [&](int r) -> uint32_t {
+    if (!mrow0) return 0xFFFFFFFFu;
+    return reinterpret_cast<const uint32_t*>(mrow0 + (int64_t)min(max(r, 0), nraw - 1) * mpitch)[lane];
+  };
 
   // the score ring starts zeroed: rows outside the detection window read as non-corners
   *reinterpret_cast<uint4*>(sc8 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
@@ -123,6 +130,12 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   uint32_t pf[kBand];
 #pragma unroll
   for (int i = 0; i < kBand; i++) pf[i] = load_row(6 + i);
+  // mask rows y0 - 1 .. y0 + kBand of the current band (m) and the next band's new ones (mpf)
+  uint32_t m[kBand + 2], mpf[kBand];
+#pragma unroll
+  for (int i = 0; i < kBand + 2; i++) m[i] = load_mrow(2 + i);
+#pragma unroll
+  for (int i = 0; i < kBand; i++) mpf[i] = load_mrow(kBand + 4 + i);
 #pragma unroll
   for (int i = 0; i < 6; i++) {
     w[i] = fix_row(i, w[i]);
@@ -142,9 +155,17 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       rows[6 + i] = fix_row(y0 + 3 + i, pf[i]);
       put_row(y0 + 3 + i, rows[6 + i]);
     }
+    if (b > 0) {   // mask rows y0 - 1 .. y0 + kBand
+#pragma unroll
+      for (int i = 0; i < 2; i++) m[i] = m[kBand + i];
+#pragma unroll
+      for (int i = 0; i < kBand; i++) m[2 + i] = mpf[i];
+    }
     if (b + 1 < nbands) {
 #pragma unroll
       for (int i = 0; i < kBand; i++) pf[i] = load_row(y0 + kBand + 3 + i);
+#pragma unroll
+      for (int i = 0; i < kBand; i++) mpf[i] = load_mrow(y0 + kBand + 1 + i);
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) w[i] = rows[kBand + i];
@@ -154,6 +175,19 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     *reinterpret_cast<uint4*>(sc8 + (((y0 + (lane >> 4)) & 7) << 8) + 16 * (lane & 15)) =
         make_uint4(0u, 0u, 0u, 0u);
     *reinterpret_cast<uint32_t*>(sc8 + (((y0 + kBand) & 7) << 8) + 4 * lane) = 0u;
+
+    // A band whose mask rows y0 - 1 .. y0 + kBand are all zero emits nothing, and nothing it
+    // scores is read by an NMS that can emit (the neighbour bands' corners on rows y0 - 1 and
+    // y1 are masked out too): skip it, dropping the carried corners.
+    {
+      uint32_t any = 0;
+#pragma unroll
+      for (int i = 0; i < kBand + 2; i++) any |= m[i];
+      if (__ballot(any != 0) == 0) {
+        ncarry = 0;
+        continue;
+      }
+    }
 
     // ---- A: compass pre-test (k_fast_cells phase A) from the register window, survivors
     // appended after the carried corners in raster order
@@ -279,9 +313,21 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
         if (cx > cs) mx = max(mx, fr_max3(sv(-1, -1), sv(0, -1), sv(1, -1)));
         if (cx + 1 < ce) mx = max(mx, fr_max3(sv(-1, 1), sv(0, 1), sv(1, 1)));
         keep = e0 >= 2 && e0 > mx;   // score > 0 and > every in-cell neighbour's score
-        if (mbits && keep) keep = ((mbits[(int64_t)k * kMaskBitRows + (y - 3)] >> (cx - cs)) & 1u) != 0;
         rec = (uint32_t)(xa + x - kMinBorder) | ((uint32_t)(u.wy0 + y - 3 - kMinBorder) << 12) |
               ((uint32_t)(e0 - 1) << 24);
+      }
+      // runByPixelsMask: the mask byte of (y, x) from the lane holding column x of mask row y
+      // (row y - (y0 - 1) of the register window m)
+      {
+        const int e = list[min(j, nproc - 1)];
+        const int ri = ((e >> 8) & 0x7F) - (y0 - 1), x = e & 0xFF;
+        uint32_t mw = 0;
+#pragma unroll
+        for (int i = 0; i <= kBand; i++) {
+          const uint32_t mi = (uint32_t)__builtin_amdgcn_ds_bpermute((x >> 2) << 2, (int)m[i]);
+          mw = ri == i ? mi : mw;
+        }
+        keep = keep && ((mw >> (8 * (x & 3))) & 0xFFu) != 0;
       }
       uint64_t bk = __ballot(keep);
       while (bk) {   // one pass per distinct cell among the batch's keypoints

@@ -15,7 +15,7 @@ from collections import defaultdict
 d = defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Kernel_Name"]
-    if "pyr_fast" in n:
+    if "k_pyr_rows" in n or "k_fast_rows" in n:
         d[n.split("(")[0]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, v in d.items():
     print(k, len(v), "us:", [round(x, 1) for x in v[:16]])
