@@ -30,14 +30,19 @@
 namespace mcs {
 
 namespace {
-constexpr int kBand = 4;
+#ifndef MCS_FAST_BAND
+#define MCS_FAST_BAND 4
+#endif
+constexpr int kBand = MCS_FAST_BAND;   // detection rows per band (4 or 8)
+static_assert(kBand == 4 || kBand == 8, "band height");
+constexpr int kScoreRows = kBand + 2 <= 8 ? 8 : 16;
 // LDS: the four waves' raw rings (16 x 256 B, 4 KB aligned), then their score rings (8 x 256 B,
 // 2 KB aligned), then their lists (carried corners, then the band's survivors, compacted in
 // place into its corners).  The alignment lets a ring address be (offset & mask) | base.
-constexpr int kRingBytes = 4096, kScoreBytes = 2048;
+constexpr int kRingBytes = 4096, kScoreBytes = kScoreRows * 256;
 constexpr int kListCap = 256 + kBand * 256;
 constexpr int kScoreBase = 4 * kRingBytes, kListBase = kScoreBase + 4 * kScoreBytes;
-constexpr int kLdsBytes = kListBase + 4 * 2 * kListCap;
+constexpr int kLdsBytes = kListBase + 4 * 2 * (kListCap + 2);   // + a dummy slot per list
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -60,10 +65,10 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   const uint32_t sc_base = kScoreBase + (uint32_t)wv * kScoreBytes;
   uint32_t* const ring32 = reinterpret_cast<uint32_t*>(lds + ring_base);
   uint8_t* const sc8 = lds + sc_base;
-  uint16_t* const list = reinterpret_cast<uint16_t*>(lds + kListBase + wv * 2 * kListCap);
+  uint16_t* const list = reinterpret_cast<uint16_t*>(lds + kListBase + wv * 2 * (kListCap + 2));
   // score-ring byte of pixel e = (y << 8 | x) moved by (dy, dx)
   auto sc_at = [&](int e, int dy, int dx) -> uint8_t& {
-    return lds[((uint32_t)(e + dy * 256 + dx) & 0x7FFu) | sc_base];
+    return lds[((uint32_t)(e + dy * 256 + dx) & (uint32_t)(kScoreBytes - 1)) | sc_base];
   };
   int f, item;
   if (!xcd_frame_map(blockIdx.x, a.nframes, (a.nunits + 3) / 4, &f, &item)) return;
@@ -120,8 +125,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   };
 
   // the score ring starts zeroed: rows outside the detection window read as non-corners
-  *reinterpret_cast<uint4*>(sc8 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
-  *reinterpret_cast<uint4*>(sc8 + 1024 + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int i = 0; i < kScoreBytes / 1024; i++)
+    *reinterpret_cast<uint4*>(sc8 + 1024 * i + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
   // register window: rows y0 - 3 .. y0 + 2 of the current band (the compass reads registers;
   // the exact test reads the ring)
   uint32_t w[6];
@@ -172,9 +178,11 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     // zero this band's score rows (kBand x 256 B: one 16-byte store per lane) and the row
     // below them: on the last band that row lies below the window and must read as zero (its
     // ring slot held row y0 - 4, which no NMS of this band reads)
-    *reinterpret_cast<uint4*>(sc8 + (((y0 + (lane >> 4)) & 7) << 8) + 16 * (lane & 15)) =
-        make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint32_t*>(sc8 + (((y0 + kBand) & 7) << 8) + 4 * lane) = 0u;
+#pragma unroll
+    for (int i = 0; i < kBand / 4; i++)
+      *reinterpret_cast<uint4*>(sc8 + (((y0 + 4 * i + (lane >> 4)) & (kScoreRows - 1)) << 8) + 16 * (lane & 15)) =
+          make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint32_t*>(sc8 + (((y0 + kBand) & (kScoreRows - 1)) << 8) + 4 * lane) = 0u;
 
     // A band whose mask rows y0 - 1 .. y0 + kBand are all zero emits nothing, and nothing it
     // scores is read by an NMS that can emit (the neighbour bands' corners on rows y0 - 1 and
@@ -207,19 +215,23 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       const uint32_t s = (y < y1) ? ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
                                       ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm)
                                   : 0u;
-      const bool s0 = (s & 0x80u) != 0, s1 = (s & 0x8000u) != 0;
-      const bool s2 = (s & 0x800000u) != 0, s3 = (s & 0x80000000u) != 0;
-      const uint64_t b0 = __ballot(s0), b1 = __ballot(s1), b2 = __ballot(s2), b3 = __ballot(s3);
-      int pos = ncarry + ns + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+      // compaction: the lane's survivor count c (0..4) as three ballots of its bits gives the
+      // lane's exclusive prefix by mbcnt; the four entries are written unconditionally, those
+      // of non-survivors to a dummy slot
+      const uint32_t c = (uint32_t)__builtin_popcount(s);
+      const uint64_t q0 = __ballot(c & 1u), q1 = __ballot(c & 2u), q2 = __ballot(c & 4u);
+      auto mbcnt = [](uint64_t m) {
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      };
+      const int pos0 = ncarry + ns + mbcnt(q0) + 2 * mbcnt(q1) + 4 * mbcnt(q2);
+      ns += __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
+      const int k0 = (s >> 7) & 1, k1 = (s >> 15) & 1, k2 = (s >> 23) & 1, k3 = s >> 31;
+      const int pos1 = pos0 + k0, pos2 = pos1 + k1, pos3 = pos2 + k2;
       const int idx = (y << 8) | (4 * lane);
-      if (s0) list[pos] = (uint16_t)idx;
-      pos += s0;
-      if (s1) list[pos] = (uint16_t)(idx + 1);
-      pos += s1;
-      if (s2) list[pos] = (uint16_t)(idx + 2);
-      pos += s2;
-      if (s3) list[pos] = (uint16_t)(idx + 3);
-      ns += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+      list[k0 ? pos0 : kListCap] = (uint16_t)idx;
+      list[k1 ? pos1 : kListCap] = (uint16_t)(idx + 1);
+      list[k2 ? pos2 : kListCap] = (uint16_t)(idx + 2);
+      list[k3 ? pos3 : kListCap] = (uint16_t)(idx + 3);
     }
     dev::wave_sync();
 

@@ -47,9 +47,9 @@ def main(fetch_csv, write_csv, out_json):
             "write": (sum(w) / len(w) * 1024) if w else None,
         }
     k = out["kernels"]
-    # per extractor call (= one k_fast_cells launch): every k_pyr_rows<true> launch of the call
+    # per extractor call (= one k_fast_rows launch): every k_pyr_rows<true> launch of the call
     # (one per level 1..L-1: resize + fused blur) + the FAST launch
-    fa = next((v for n, v in k.items() if n.startswith("k_fast_cells")), None)
+    fa = next((v for n, v in k.items() if n.startswith("k_fast_rows") or n.startswith("k_fast_cells")), None)
     rs = [v for n, v in k.items() if n.startswith("k_pyr_rows<true")]
     if rs and fa and fa["launches"]:
         calls = fa["launches"]
