@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <new>
@@ -609,6 +610,19 @@ struct mcs_ba_ctx {
   size_t next = 0;
   double* pinned = nullptr;   // host-pinned readback scalars
   int32_t* pinned_i = nullptr;
+  // host-pinned staging of a call's packed problem upload (grow-only)
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0;
+  uint8_t* stage_get(size_t bytes) {
+    if (bytes > stage_cap) {
+      if (stage) (void)hipHostFree(stage);
+      stage = nullptr; stage_cap = 0;
+      const size_t cap = std::max(bytes, (size_t)1 << 20);
+      if (hipHostMalloc((void**)&stage, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+      stage_cap = cap;
+    }
+    return stage;
+  }
   // optional stage timing (mcs_ba_enable_timing): HIP events on st around each stage,
   // accumulated after the per-trial synchronisation the LM control needs anyway
   bool timing = false;
@@ -762,6 +776,38 @@ T* up_raw(mcs_ba_ctx* c, const T* src, size_t n, hipError_t& e) {
   return d;
 }
 
+// The problem arrays of a call, packed into one device block through one pinned staging
+// buffer and ONE host-to-device copy (some thirty pageable copies cost ~0.4 ms per call on a
+// config-C LocalBA round).  add() records where each array's device pointer goes; flush()
+// fills the pointers.
+struct Packer {
+  struct Item { void** dst; const void* src; size_t bytes, off; };
+  std::vector<Item> items;
+  size_t total = 0;
+  template <typename D, typename T>
+  void add(D** dst, const T* src, size_t n) {
+    static_assert(sizeof(D) == sizeof(T), "element type");
+    items.push_back({reinterpret_cast<void**>(const_cast<void*>(static_cast<const void*>(dst))), src,
+                     src ? n * sizeof(T) : 0, total});
+    total += (std::max<size_t>(1, n) * sizeof(T) + 255) & ~(size_t)255;
+  }
+  template <typename D, typename T>
+  void add(D** dst, const std::vector<T>& v) { add(dst, v.data(), v.size()); }
+  hipError_t flush(mcs_ba_ctx* c) {
+    uint8_t* d = (uint8_t*)c->alloc(std::max<size_t>(total, 256));
+    if (!d) return hipErrorOutOfMemory;
+    hipError_t e = hipStreamSynchronize(c->st);   // the staging buffer is free again
+    if (e != hipSuccess) return e;
+    uint8_t* h = c->stage_get(std::max<size_t>(total, 256));
+    if (!h) return hipErrorOutOfMemory;
+    for (const Item& it : items) {
+      if (it.bytes) std::memcpy(h + it.off, it.src, it.bytes);
+      *it.dst = d + it.off;
+    }
+    return total ? hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, c->st) : hipSuccess;
+  }
+};
+
 unsigned gb(int n) { return (unsigned)std::max(1, (n + 255) / 256); }
 
 // Exchange-buffer layout (offsets in doubles) for T tiles and np active poses; the head of
@@ -886,31 +932,37 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   Dev d;
   std::memset(&d, 0, sizeof(d));
   const int NE = p->n_edges;
-  d.mc = up_raw(c, p->mc, 6 * (size_t)p->n_cams, he);
-  d.cam = up_raw(c, p->cam, 17 * (size_t)p->n_cams, he);
-  d.e_pose = up_raw(c, p->edge_pose, NE, he);
-  d.e_point = up_raw(c, p->edge_point, NE, he);
-  d.e_cam = up_raw(c, p->edge_cam, NE, he);
-  d.e_meas = up_raw(c, p->edge_meas, 2 * (size_t)NE, he);
-  d.e_info = up_raw(c, p->edge_info, NE, he);
+  double *d_poses = nullptr, *d_points = nullptr, *d_poses_bk = nullptr, *d_points_bk = nullptr;
+  {
+    Packer pk;
+    pk.add(&d.mc, p->mc, 6 * (size_t)p->n_cams);
+    pk.add(&d.cam, p->cam, 17 * (size_t)p->n_cams);
+    pk.add(&d.e_pose, p->edge_pose, (size_t)NE);
+    pk.add(&d.e_point, p->edge_point, (size_t)NE);
+    pk.add(&d.e_cam, p->edge_cam, (size_t)NE);
+    pk.add(&d.e_meas, p->edge_meas, 2 * (size_t)NE);
+    pk.add(&d.e_info, p->edge_info, (size_t)NE);
+    pk.add(&d_poses, (const double*)poses, 6 * (size_t)p->n_poses);
+    pk.add(&d_points, (const double*)points, 3 * (size_t)p->n_points);
+    pk.add(&d_poses_bk, (const double*)poses, 6 * (size_t)p->n_poses);
+    pk.add(&d_points_bk, (const double*)points, 3 * (size_t)p->n_points);
+    pk.add(&d.aedge, s.aedge);
+    pk.add(&d.pose_h, s.pose_h); pk.add(&d.point_h, s.point_h);
+    pk.add(&d.hpose_vtx, s.hpose_vtx); pk.add(&d.hpt_vtx, s.hpt_vtx);
+    pk.add(&d.pt_ptr, s.pt_ptr); pk.add(&d.pt_edges, s.pt_edges);
+    pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
+    pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
+    pk.add(&d.it_blk, s.it_blk); pk.add(&d.it_chunk, s.it_chunk); pk.add(&d.it_slot, s.it_slot);
+    pk.add(&d.fin_blk, s.fin_blk); pk.add(&d.fin_slot0, s.fin_slot0); pk.add(&d.fin_nch, s.fin_nch);
+    pk.add(&d.pr_ptr, s.pr_ptr); pk.add(&d.pr_e1, s.pr_e1); pk.add(&d.pr_e2, s.pr_e2);
+    he = pk.flush(c);
+  }
   d.delta = p->huber_delta;
   d.dsqr = p->huber_delta * p->huber_delta;
-  double* d_poses = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
-  double* d_points = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
-  double* d_poses_bk = up_raw(c, (const double*)poses, 6 * (size_t)p->n_poses, he);
-  double* d_points_bk = up_raw(c, (const double*)points, 3 * (size_t)p->n_points, he);
   d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
-  d.aedge = up(c, s.aedge, he); d.nae = (int)s.aedge.size();
-  d.pose_h = up(c, s.pose_h, he); d.point_h = up(c, s.point_h, he);
-  d.hpose_vtx = up(c, s.hpose_vtx, he); d.hpt_vtx = up(c, s.hpt_vtx, he);
+  d.nae = (int)s.aedge.size();
   d.np = s.np; d.nl = s.nl;
-  d.pt_ptr = up(c, s.pt_ptr, he); d.pt_edges = up(c, s.pt_edges, he);
   d.npe = (int)s.pt_edges.size();
-  d.ps_ptr = up(c, s.ps_ptr, he); d.ps_edges = up(c, s.ps_edges, he);
-  d.blk_i = up(c, s.blk_i, he); d.blk_j = up(c, s.blk_j, he);
-  d.it_blk = up(c, s.it_blk, he); d.it_chunk = up(c, s.it_chunk, he); d.it_slot = up(c, s.it_slot, he);
-  d.fin_blk = up(c, s.fin_blk, he); d.fin_slot0 = up(c, s.fin_slot0, he); d.fin_nch = up(c, s.fin_nch, he);
-  d.pr_ptr = up(c, s.pr_ptr, he); d.pr_e1 = up(c, s.pr_e1, he); d.pr_e2 = up(c, s.pr_e2, he);
   auto dz = [&](size_t cnt_) { double* q = (double*)c->alloc(std::max<size_t>(1, cnt_) * 8); if (!q) he = hipErrorOutOfMemory; return q; };
   d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
   d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
@@ -990,7 +1042,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   };
   // graph replay of the trial: one rank (no exchange callback inside), no stage timing, and
   // the LDL^T kernel attributes already set (the first trial of a call runs eagerly)
-  const bool use_graph = !sharded && !c->timing;
+  static const bool graph_env = !(std::getenv("MCS_BA_NO_GRAPH") && std::getenv("MCS_BA_NO_GRAPH")[0] == '1');
+  const bool use_graph = graph_env && !sharded && !c->timing;
   bool graph_ok = true;
   int trial_no = 0;
   hipGraphExec_t graph_exec = nullptr;
@@ -1181,6 +1234,7 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
   c->release();
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_i) (void)hipHostFree(c->pinned_i);
+  if (c->stage) (void)hipHostFree(c->stage);
   if (c->st) (void)hipStreamDestroy(c->st);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   delete c;

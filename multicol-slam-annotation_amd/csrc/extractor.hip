@@ -1,12 +1,12 @@
 // Host orchestration of the MI355X feature extractor (C-ABI of include/mcs_extractor.h):
 // pyramid+blur -> FAST cells -> octree -> orientation + rotated BRIEF, batched over many
-// camera-frames resident in HBM.  Kernels: k_pyramid.hip, k_fast.hip, k_octree.hip,
+// camera-frames resident in HBM.  Kernels: k_pyramid.hip, k_fast_rows.hip, k_octree.hip,
 // k_desc.hip.
 //
 // Reference path (billamiable/MultiCol-SLAM-Annotation):
 //   mdBRIEFextractorOct::operator()        src/mdBRIEFextractorOct.cpp:1244-1337
 //   ComputePyramid                         :1158-1201   -> k_pyr_rows, k_mask_nearest
-//   ComputeKeyPointsOctTree (FAST part)    :863-949     -> k_fast_cells
+//   ComputeKeyPointsOctTree (FAST part)    :863-949     -> k_fast_rows
 //   DistributeOctTree / DivideNode         :569-861     -> k_octree
 //   computeOrientation / IC_Angle          :221-248     -> k_orient_desc (part 1)
 //   boxFilter 5x5                          :1301        -> k_pyr_rows (fused)
@@ -52,8 +52,8 @@ struct mcs_extractor {
   uint32_t* d_sel = nullptr;     // [F][sel_per_frame]     octree selection per level
   int32_t* d_sel_count = nullptr;  // [F][nlevels]
   // masks: registered set + single-call slot, each with per-cell window bitmaps
-  uint8_t* d_mask_pyr = nullptr; uint64_t* d_mask_bits = nullptr; int n_masks = 0;
-  uint8_t* d_mask_single = nullptr; uint64_t* d_bits_single = nullptr;
+  uint8_t* d_mask_pyr = nullptr; int n_masks = 0;
+  uint8_t* d_mask_single = nullptr;
   // single-frame staging
   uint8_t* d_in = nullptr;
   mcs_keypoint* d_kps = nullptr; uint8_t* d_desc = nullptr; int32_t* d_count = nullptr;
@@ -89,7 +89,7 @@ static inline void stage_mark(mcs_extractor* h, int stage, hipStream_t st) {
 
 // Core batched pipeline on device buffers.
 static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uint8_t* mask_pyr,
-                     const uint64_t* mask_bits, const int32_t* d_mask_index, mcs_keypoint* d_kps,
+                     const int32_t* d_mask_index, mcs_keypoint* d_kps,
                      int32_t* d_counts, uint8_t* d_desc, uint8_t* d_desc_masks,
                      const int32_t* d_cam_index, hipStream_t st) {
   const Plan& pl = h->plan;
@@ -130,7 +130,6 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
   fa.nframes = F;
   fill_level_ptrs(pl, fa.lp);
-  (void)mask_bits;
   const bool wide = pl.scale_factor > 1.5;
   // Schedule (one stream): the resize chain K1+K5 level by level, the level-0 blur, then FAST
   // of every level in one launch.  (FAST per level on a second stream beside the chain was
@@ -261,7 +260,6 @@ int mcs_extractor_create(const mcs_extractor_params* p, int32_t width, int32_t h
   ALLOC(h->d_sel, F * pl.sel_per_frame);
   ALLOC(h->d_sel_count, F * pl.nlevels);
   ALLOC(h->d_mask_single, pl.mask_frame_bytes);
-  ALLOC(h->d_bits_single, pl.cells.size() * kMaskBitRows);
   ALLOC(h->d_in, (size_t)width * height);
   ALLOC(h->d_kps, pl.sel_per_frame);
   ALLOC(h->d_desc, (size_t)pl.sel_per_frame * pl.p.desc_size);
@@ -289,7 +287,7 @@ void mcs_extractor_destroy(mcs_extractor* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_units, h->d_pyr, h->d_blur,
                   h->d_slots, h->d_cell_counts, h->d_cand, h->d_cnode, h->d_sel, h->d_sel_count,
-                  h->d_mask_pyr, h->d_mask_bits, h->d_mask_single, h->d_bits_single, h->d_in,
+                  h->d_mask_pyr, h->d_mask_single, h->d_in,
                   h->d_kps, h->d_desc, h->d_count, h->d_dmask, h->d_cams};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -350,16 +348,11 @@ int mcs_extractor_set_masks_device(mcs_extractor* h, const uint8_t* d_masks, int
   if (!h || n_masks < 0 || (n_masks > 0 && !d_masks)) return MCS_ERR_ARG;
   MCS_HIP_CHECK(hipSetDevice(h->device));
   if (h->d_mask_pyr) { MCS_HIP_CHECK(hipFree(h->d_mask_pyr)); h->d_mask_pyr = nullptr; }
-  if (h->d_mask_bits) { MCS_HIP_CHECK(hipFree(h->d_mask_bits)); h->d_mask_bits = nullptr; }
   h->n_masks = 0;
   if (n_masks == 0) return MCS_OK;
   int rc = dalloc(&h->d_mask_pyr, (size_t)n_masks * h->plan.mask_frame_bytes);
   if (rc) return rc;
-  rc = dalloc(&h->d_mask_bits, (size_t)n_masks * h->plan.cells.size() * kMaskBitRows);
-  if (rc) return rc;
   launch_mask_pyramids(h->plan, d_masks, n_masks, h->d_mask_pyr, (hipStream_t)stream);
-  launch_cell_maskbits(h->plan, h->d_cells, h->d_mask_pyr, n_masks, h->d_mask_bits,
-                       (hipStream_t)stream);
   MCS_HIP_CHECK(hipGetLastError());
   h->n_masks = n_masks;
   return MCS_OK;
@@ -394,8 +387,7 @@ int mcs_extract_batch_device_ex(mcs_extractor* h, const uint8_t* d_images, int32
   if (n_frames > h->max_frames) { set_error("n_frames > max_frames"); return MCS_ERR_CAPACITY; }
   MCS_HIP_CHECK(hipSetDevice(h->device));
   const uint8_t* mp = h->n_masks > 0 ? h->d_mask_pyr : nullptr;
-  const uint64_t* mf = h->n_masks > 0 ? h->d_mask_bits : nullptr;
-  return run_batch(h, d_images, n_frames, mp, mf, mp ? d_cam_index : nullptr, d_kps, d_counts,
+  return run_batch(h, d_images, n_frames, mp, mp ? d_cam_index : nullptr, d_kps, d_counts,
                    d_desc, d_desc_masks, h->n_cams > 1 ? d_cam_index : nullptr,
                    (hipStream_t)stream);
 }
@@ -419,19 +411,16 @@ int mcs_extract(mcs_extractor* h, const uint8_t* image, int32_t stride, const ui
   hipStream_t st = nullptr;
   MCS_HIP_CHECK(hipMemcpy2D(h->d_in, pl.W, image, stride, pl.W, pl.H, hipMemcpyHostToDevice));
   const uint8_t* mp = nullptr;
-  const uint64_t* mf = nullptr;
   if (mask) {
     // level 0 of the single-call mask pyramid doubles as the upload buffer
     MCS_HIP_CHECK(hipMemcpy2D(h->d_mask_single, pl.lv[0].bpitch, mask, mask_stride, pl.W, pl.H,
                               hipMemcpyHostToDevice));
     launch_mask_pyramids(pl, h->d_mask_single, 1, h->d_mask_single, st);
-    launch_cell_maskbits(pl, h->d_cells, h->d_mask_single, 1, h->d_bits_single, st);
     MCS_HIP_CHECK(hipGetLastError());
     mp = h->d_mask_single;
-    mf = h->d_bits_single;
   }
   const bool learn = pl.p.learn_masks != 0;
-  int rc = run_batch(h, h->d_in, 1, mp, mf, nullptr, h->d_kps, h->d_count, h->d_desc,
+  int rc = run_batch(h, h->d_in, 1, mp, nullptr, h->d_kps, h->d_count, h->d_desc,
                      learn ? h->d_dmask : nullptr, nullptr, st);
   if (rc) return rc;
   int32_t n = 0;

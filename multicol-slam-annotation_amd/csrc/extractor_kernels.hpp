@@ -62,41 +62,7 @@ void launch_pyr_blur(const PyrArgs& a, bool resize, bool wide, hipStream_t st);
 
 void launch_mask_pyramids(const Plan& pl, const uint8_t* d_masks, int n, uint8_t* dst,
                           hipStream_t st);
-// Per-camera FAST-window mask bitmaps: bits[m][cell][row] = 64-bit row of the cell's detection
-// window (bit x = mask level pixel (wx0 + x, wy0 + row) != 0; windows are <= 64 x 64)
-constexpr int kMaskBitRows = 64;
-void launch_cell_maskbits(const Plan& pl, const CellDesc* d_cells, const uint8_t* mask_pyr,
-                          int n_masks, uint64_t* bits, hipStream_t st);
-
-// ---- K2: FAST cells
-struct FastArgs {
-  const uint8_t* img0; int64_t img0_fstride;
-  const uint8_t* pyr; int64_t pyr_fstride;
-  const uint64_t* mask_bits;                     // [mask][cell][64] (nullable = no mask)
-  const int32_t* mask_index;
-  const CellDesc* cells; int ncells;
-  uint32_t* slots; int64_t slots_fstride;
-  int32_t* cell_counts;
-  int threshold;
-  uint32_t kk, rbits;     // byte-wise compare constants (v_lerp_u8), see launch_fast_cells
-  int nframes;
-  LevelPtrs lp;
-  // per-wave LDS layout (fast_lds_layout) and prefetch size
-  int tile_pitch, smap_off, surv_off, wave_lds;
-  int tile_dwords;        // max (wh + 6) * (ceil(ww / 4) + 2) over the plan's cells
-};
-// LDS layout of k_fast_cells for windows up to max_ww x max_wh
-inline void fast_lds_layout(int max_ww, int max_wh, FastArgs& a) {
-  auto al16 = [](int v) { return (v + 15) & ~15; };
-  a.tile_pitch = 4 * ((max_ww + 3) / 4) + 8;   // window - 4 .. quads + 7 (k_fast_cells staging)
-  a.smap_off = al16(a.tile_pitch * (max_wh + 6));
-  a.surv_off = a.smap_off + al16((max_ww + 2) * (max_wh + 2));
-  a.wave_lds = a.surv_off + al16(2 * max_ww * max_wh);
-  a.tile_dwords = (max_wh + 6) * ((max_ww + 3) / 4 + 2);
-}
-void launch_fast_cells(const FastArgs& a, hipStream_t st);
-
-// ---- K2 (row-streaming form): FAST over runs of cells, one wave per FastUnit
+// ---- K2: FAST over runs of cells (row-streaming), one wave per FastUnit
 struct FastRowArgs {
   const uint8_t* img0; int64_t img0_fstride;
   const uint8_t* pyr; int64_t pyr_fstride;
@@ -107,7 +73,7 @@ struct FastRowArgs {
   uint32_t* slots; int64_t slots_fstride;
   int32_t* cell_counts;
   int threshold;
-  uint32_t kk, rbits;
+  uint32_t kk, rbits;     // byte-wise compare constants (v_lerp_u8), see launch_fast_rows
   int nframes;
   LevelPtrs lp;
 };

@@ -17,8 +17,8 @@
 //         register window (rows y0-3 .. y0+kBand+2) and a 16-row LDS ring; with a 256 B row
 //         stride the ring address of pixel (y, x) + (dy, dx) is ((y << 8 | x) + (dy << 8) + dx)
 //         & 0xFFF
-//   A     compass pre-test per quad from the register window, 4 pixels per lane
-//         (k_fast_cells phase A), survivors -> list in raster order
+//   A     compass pre-test per quad from the register window, 4 pixels per lane, survivors
+//         -> list in raster order
 //   B     exact test + score of the survivors in full 64-lane batches from the ring: score + 1
 //         into an 8-row score ring, corners compacted in place (raster order)
 //   C     NMS of every corner whose lower neighbour row is scored (the band's last row waits
@@ -197,7 +197,10 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       }
     }
 
-    // ---- A: compass pre-test (k_fast_cells phase A) from the register window, survivors
+    // ---- A: compass pre-test from the register window, 4 pixels per lane: a 9-long arc of the
+    // 16-circle always holds two ADJACENT compass points (0/4/8/12), so a corner needs
+    // (D0|D8)&(D4|D12) or (B0|B8)&(B4|B12) (D = darker than v-t, B = brighter than v+t), tested
+    // byte-wise with v_lerp_u8 (launch_fast_rows); survivors
     // appended after the carried corners in raster order
     int ns = 0;
     const uint64_t lt = dev::lanemask_lt();
@@ -375,7 +378,10 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
 
 void launch_fast_rows(const FastRowArgs& a_in, hipStream_t st) {
   FastRowArgs a = a_in;
-  // byte-wise compare constants of the compass pre-test (k_fast.hip, launch_fast_cells)
+  // byte-wise compare constants of the compass pre-test: v_lerp_u8(v, ~p, r) =
+  // floor((v - p + 255 + r) / 2) per byte is >= K exactly when v - p > t (K = (t + 256 + r) / 2,
+  // r = t & 1), and a second lerp against ~(K-1) moves (>= K) into the byte's top bit; t = 255
+  // admits no corner: K = 256, which no byte reaches, is kk = 0
   const int t = a.threshold;
   const uint32_t r = (uint32_t)(t & 1), K = (uint32_t)(t + 256 + (int)r) / 2;
   a.rbits = r * 0x01010101u;

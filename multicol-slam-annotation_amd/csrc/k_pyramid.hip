@@ -317,37 +317,4 @@ void launch_mask_pyramids(const Plan& pl, const uint8_t* d_masks, int n, uint8_t
   }
 }
 
-// Per-camera bitmaps of every FAST window (runByPixelsMask keeps a keypoint only on a nonzero
-// mask pixel): one 64-bit word per window row, bit x = mask(wx0 + x, wy0 + row) != 0.  Built
-// once per registered mask set, read by k_fast_cells as one prefetched word pair per lane.
-__global__ __launch_bounds__(64) void k_cell_maskbits(const CellDesc* __restrict__ cells,
-                                                      int ncells, const uint8_t* __restrict__ mp,
-                                                      int64_t mfs, LevelPtrs lp,
-                                                      uint64_t* __restrict__ bits) {
-  const int c = blockIdx.x, m = blockIdx.y, y = threadIdx.x;
-  const CellDesc cd = cells[c];
-  const int ww = max(0, cd.wx1 - cd.wx0), wh = max(0, cd.wy1 - cd.wy0);
-  uint64_t b = 0;
-  if (y < wh) {
-    const uint8_t* row = mp + (int64_t)m * mfs + lp.mask_off[cd.level] +
-                         (int64_t)(cd.wy0 + y) * lp.bpitch[cd.level] + cd.wx0;
-    for (int x = 0; x < ww; x++) b |= (uint64_t)(row[x] != 0) << x;
-  }
-  bits[((int64_t)m * ncells + c) * kMaskBitRows + y] = b;
-}
-
-void launch_cell_maskbits(const Plan& pl, const CellDesc* d_cells, const uint8_t* mask_pyr,
-                          int n_masks, uint64_t* bits, hipStream_t st) {
-  LevelPtrs lp;
-  for (int l = 0; l < kMaxLevels; l++) {
-    const bool v = l < pl.nlevels;
-    lp.w[l] = v ? pl.lv[l].w : 0; lp.h[l] = v ? pl.lv[l].h : 0;
-    lp.pitch[l] = v ? pl.lv[l].pitch : 0; lp.bpitch[l] = v ? pl.lv[l].bpitch : 0;
-    lp.pyr_off[l] = v ? pl.lv[l].pyr_off : 0; lp.img_off[l] = v ? pl.lv[l].img_off : 0;
-    lp.mask_off[l] = v ? pl.lv[l].mask_off : 0;
-  }
-  hipLaunchKernelGGL(k_cell_maskbits, dim3((unsigned)pl.cells.size(), n_masks), dim3(kMaskBitRows),
-                     0, st, d_cells, (int)pl.cells.size(), mask_pyr, pl.mask_frame_bytes, lp, bits);
-}
-
 }  // namespace mcs
