@@ -130,7 +130,7 @@ int mcs_extractor_read_stage(mcs_extractor* h, int32_t stage, int32_t frame, int
 /* Live per-stage device timing (hipEvents recorded on the call's stream around each
  * stage of every batch call; no host synchronisation inside the call).  Stages:
  * 0 pyramid = resize + blur of levels 1..L-1 (k_pyr_rows<true> x L-1), 1 blur of level 0
- * (k_pyr_rows<false>), 2 FAST cells (k_fast_cells), 3 octree (k_octree),
+ * (k_pyr_rows<false>), 2 FAST (k_fast_rows), 3 octree (k_octree),
  * 4 orientation + descriptor (k_orient_desc).
  * read_timing synchronises, returns the summed milliseconds per stage over the recorded
  * calls and their number, and optionally resets.  At most 256 calls are kept. */
