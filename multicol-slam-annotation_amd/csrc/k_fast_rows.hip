@@ -33,14 +33,18 @@ namespace {
 #ifndef MCS_FAST_BAND
 #define MCS_FAST_BAND 4
 #endif
-constexpr int kBand = MCS_FAST_BAND;   // detection rows per band (4 or 8)
-static_assert(kBand == 4 || kBand == 8, "band height");
-constexpr int kScoreRows = kBand + 2 <= 8 ? 8 : 16;
+constexpr int kBand = MCS_FAST_BAND;   // detection rows per band (3, 4 or 8)
+static_assert(kBand >= 3 && kBand <= 8, "band height");
+// score rows alive at once: the NMS of a band reads rows y0 - 2 .. y1 and the band zeroes
+// y0 .. y0 + kBand, so kBand + 3 distinct rows share the ring
+constexpr int kScoreRows = kBand + 3 <= 8 ? 8 : 16;
 // LDS: the four waves' raw rings (16 x 256 B, 4 KB aligned), then their score rings (8 x 256 B,
 // 2 KB aligned), then their lists (carried corners, then the band's survivors, compacted in
 // place into its corners).  The alignment lets a ring address be (offset & mask) | base.
 constexpr int kRingBytes = 4096, kScoreBytes = kScoreRows * 256;
-constexpr int kListCap = 256 + kBand * 256;
+// a run's detection span is <= 246 px (kFastUnitSpan - 6): <= 246 carried corners + 246 kBand
+// survivors
+constexpr int kListCap = 248 + kBand * 248;
 constexpr int kScoreBase = 4 * kRingBytes, kListBase = kScoreBase + 4 * kScoreBytes;
 constexpr int kLdsBytes = kListBase + 4 * 2 * (kListCap + 2);   // + a dummy slot per list
 
@@ -175,14 +179,12 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) w[i] = rows[kBand + i];
-    // zero this band's score rows (kBand x 256 B: one 16-byte store per lane) and the row
-    // below them: on the last band that row lies below the window and must read as zero (its
-    // ring slot held row y0 - 4, which no NMS of this band reads)
+    // zero this band's score rows and the row below them: on the last band that row lies
+    // below the window and must read as zero (its ring slot held a row above y0 - 2, which no
+    // NMS of this band reads)
 #pragma unroll
-    for (int i = 0; i < kBand / 4; i++)
-      *reinterpret_cast<uint4*>(sc8 + (((y0 + 4 * i + (lane >> 4)) & (kScoreRows - 1)) << 8) + 16 * (lane & 15)) =
-          make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint32_t*>(sc8 + (((y0 + kBand) & (kScoreRows - 1)) << 8) + 4 * lane) = 0u;
+    for (int i = 0; i <= kBand; i++)
+      *reinterpret_cast<uint32_t*>(sc8 + (((y0 + i) & (kScoreRows - 1)) << 8) + 4 * lane) = 0u;
 
     // A band whose mask rows y0 - 1 .. y0 + kBand are all zero emits nothing, and nothing it
     // scores is read by an NMS that can emit (the neighbour bands' corners on rows y0 - 1 and
