@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   const uint8_t* const img = (level == 0) ? a.img0 + (int64_t)f * a.img0_fstride
                                           : a.pyr + (int64_t)f * a.pyr_fstride + a.lp.pyr_off[level];
   const uint8_t* const row0 = img + (int64_t)(u.wy0 - 3) * pitch + xa;
-  const int nraw = wh + 6;   // raw rows y_rel in [0, wh + 6); detection rows [3, wh + 3)
+  // raw rows y_rel in [0, wh + 6); detection rows [3, wh + 3)
 
   // top bit of byte k: pixel xa + 4 lane + k is a detection pixel of the run
   uint32_t detm = 0;
@@ -113,11 +113,13 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
 
   // raw row r (y_rel) of the run: one aligned dword per lane, the row's byte offset undone by
   // alignbyte with the next lane's dword (lane 63 is never consumed)
+  // No clamping: the last prefetch reaches at most 3 rows past the run's raw rows (row
+  // wy1 + 5 <= h - 20 of the level) and mask row wy0 - 1 >= 0, all inside the level.
   auto load_row = [&](int r) -> uint32_t {
-    return dev::align_down4(row0 + (int64_t)min(r, nraw - 1) * pitch)[lane];
+    return dev::align_down4(row0 + r * pitch)[lane];
   };
   auto fix_row = [&](int r, uint32_t own) -> uint32_t {
-    const uint32_t sh = (uint32_t)((uintptr_t)(row0 + (int64_t)min(r, nraw - 1) * pitch) & 3);
+    const uint32_t sh = (uint32_t)((uintptr_t)(row0 + r * pitch) & 3);
     const uint32_t nxt = __builtin_amdgcn_update_dpp(0u, own, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
     return __builtin_amdgcn_alignbyte(nxt, own, sh);
   };
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   // mask bytes of raw row r (all 0xFF without a mask)
   auto load_mrow = [&](int r) -> uint32_t {
     if (!mrow0) return 0xFFFFFFFFu;
-    return reinterpret_cast<const uint32_t*>(mrow0 + (int64_t)min(max(r, 0), nraw - 1) * mpitch)[lane];
+    return reinterpret_cast<const uint32_t*>(mrow0 + r * mpitch)[lane];
   };
 
   // the score ring starts zeroed: rows outside the detection window read as non-corners
