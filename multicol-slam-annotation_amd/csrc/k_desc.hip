@@ -22,6 +22,8 @@ __constant__ int c_pattern[2048] = {
 __constant__ uint32_t c_icw[2][33 * 9];
 // pattern as doubles (the rotation runs in double, :290-300)
 __constant__ double c_pattern_d[2048];
+// the same per test t as packed int8 (x0, y0, x1, y1): k_orient_desc stages it in LDS
+__constant__ uint32_t c_pattern_i8[512];
 
 int upload_desc_constants() {
   int umax[kHalfPatch + 1];
@@ -54,6 +56,11 @@ int upload_desc_constants() {
   double patd[2048];
   for (int i = 0; i < 2048; i++) patd[i] = (double)pat[i];
   MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern_d), patd, sizeof(patd)));
+  uint32_t pat8[512];
+  for (int t = 0; t < 512; t++)
+    pat8[t] = (uint32_t)(uint8_t)(int8_t)pat[4 * t] | (uint32_t)(uint8_t)(int8_t)pat[4 * t + 1] << 8 |
+              (uint32_t)(uint8_t)(int8_t)pat[4 * t + 2] << 16 | (uint32_t)(uint8_t)(int8_t)pat[4 * t + 3] << 24;
+  MCS_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern_i8), pat8, sizeof(pat8)));
   return MCS_OK;
 }
 
@@ -117,15 +124,17 @@ constexpr int kBlrAlign = 3;
 // IC moments of the raw patch (see c_icw); one half-wave (32 lanes) per keypoint: lane hl
 // holds patch dwords q = hl + 32k in registers (each dword is used by one lane only, so the
 // raw patch needs no LDS), sums reduced within the half (xor offsets < 32 never cross halves)
-__device__ __forceinline__ float ic_angle_regs(const uint32_t (&raw)[10], int hl) {
+__device__ __forceinline__ float ic_angle_regs(const uint32_t (&raw)[10], int hl,
+                                               const uint32_t* icw0 = c_icw[0],
+                                               const uint32_t* icw1 = c_icw[1]) {
   uint32_t a10 = 0, aS = 0, a01 = 0;
 #pragma unroll
   for (int k = 0; k < 10; k++) {
     const int q = hl + 32 * k;
     if (q < kRawH * kRawW) {
       const uint32_t px = raw[k];
-      const uint32_t d1 = __builtin_amdgcn_udot4(c_icw[0][q], px, 0u, false);
-      const uint32_t d0 = __builtin_amdgcn_udot4(c_icw[1][q], px, 0u, false);
+      const uint32_t d1 = __builtin_amdgcn_udot4(icw0[q], px, 0u, false);
+      const uint32_t d0 = __builtin_amdgcn_udot4(icw1[q], px, 0u, false);
       a10 += d1;
       aS += d0;
       a01 += (uint32_t)(q / kRawW) * d0;
@@ -159,12 +168,23 @@ __device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
 // descriptor come from one 64-bit ballot per 32 tests (low half / high half).
 __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_blr[8][kBlrH * kBlrRow];
+  // the IC weight tables and the packed pattern, staged once per workgroup: read per lane at
+  // lane-dependent indices, from constant memory they were L2 round trips inside the compute
+  // (one per test round) instead of LDS reads
+  __shared__ uint32_t s_icw[2][kRawH * kRawW];
+  __shared__ uint32_t s_pat[512];
   // wave index as a scalar: the pair, its level and counts are wave-uniform
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
   int f, item;
   const int pairs = (a.sel_per_frame + 1) / 2;
   if (!xcd_frame_map(blockIdx.x, a.nframes, (pairs + 3) / 4, &f, &item)) return;
+  for (int i = threadIdx.x; i < kRawH * kRawW; i += 256) {
+    s_icw[0][i] = c_icw[0][i];
+    s_icw[1][i] = c_icw[1][i];
+  }
+  for (int i = threadIdx.x; i < 512; i += 256) s_pat[i] = c_pattern_i8[i];
+  __syncthreads();
   // even j0: both keypoints on one level (every level's sel_off is even, build_plan)
   const int j0 = 2 * (item * 4 + wv);
   if (j0 >= a.sel_per_frame) return;
@@ -232,7 +252,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   }
   dev::wave_sync();
   // ---- IC_Angle: integer moments over the circular r=16 patch
-  const float angle = ic_angle_regs(raw, hl);
+  const float angle = ic_angle_regs(raw, hl, s_icw[0], s_icw[1]);
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
@@ -243,8 +263,9 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   uint32_t w = 0u;   // lane hl keeps test word hl of its half's descriptor
   for (int r = 0; r < nw; r++) {
     const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
-    const double px0 = c_pattern_d[4 * t], py0 = c_pattern_d[4 * t + 1];
-    const double px1 = c_pattern_d[4 * t + 2], py1 = c_pattern_d[4 * t + 3];
+    const uint32_t pw = s_pat[t];
+    const double px0 = (double)(int)(int8_t)(pw & 0xFF), py0 = (double)(int)(int8_t)((pw >> 8) & 0xFF);
+    const double px1 = (double)(int)(int8_t)((pw >> 16) & 0xFF), py1 = (double)(int)(int8_t)(pw >> 24);
     const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
     const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
     const uint64_t b = __ballot(bc[o0] < bc[o1]);
