@@ -210,15 +210,29 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
     for (int s = 0; s < 8; s++) bq[c][s] = expand16((w[s] >> (16 * h)) & 0xFFFF);
   }
   uint32_t k1[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, k2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  // train tile bits, one tile ahead: the next tile's loads are in flight while this one is
+  // expanded and multiplied (each thread 2 dwords of 64 trains x 8 dwords)
+  uint32_t nb[2];
+  auto fetch = [&](int t0n) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int e = tid + 256 * r;
+      const int tr = e >> 3, dw = e & 7;
+      nb[r] = t0n + tr < nt ? reinterpret_cast<const uint32_t*>(T + (int64_t)(t0n + tr) * 32)[dw] : 0u;
+    }
+  };
+  fetch(0);
   for (int t0 = 0; t0 < nt; t0 += kMfTileT) {
     const int ntile = min(kMfTileT, nt - t0);
+    const uint32_t cb[2] = {nb[0], nb[1]};
+    if (t0 + kMfTileT < nt) fetch(t0 + kMfTileT);
     __syncthreads();
     // ---- expand the tile: 64 trains x 8 dwords; each thread 2 dwords -> 2 x 32 bytes
 #pragma unroll
     for (int r = 0; r < 2; r++) {
       const int e = tid + 256 * r;          // 0..511
       const int tr = e >> 3, dw = e & 7;
-      const uint32_t bits = tr < ntile ? reinterpret_cast<const uint32_t*>(T + (int64_t)(t0 + tr) * 32)[dw] : 0u;
+      const uint32_t bits = cb[r];
       uint8_t* dst = s_t + tr * kMfPitch + dw * 32;
       const v4i lo = expand16(bits & 0xFFFF), hi = expand16(bits >> 16);
       *reinterpret_cast<v4i*>(dst) = lo;
