@@ -22,7 +22,10 @@ __device__ __forceinline__ int oct_quad(uint32_t pk, int midx, int midy) {
   return (x >= midx ? 1 : 0) + (y >= midy ? 2 : 0);
 }
 
-template <int MAXL>
+// CAP: candidates of a (frame, level) kept in LDS when they fit (every subdivision round reads
+// them again; from global memory each round was a dependent round trip); larger lists stay in
+// global memory.  Both cases go through one generic pointer.
+template <int MAXL, int CAP>
 __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   constexpr int kOctPer = MAXL / kOctThreads;  // nodes per thread in node scans
   int f, l;
@@ -40,9 +43,11 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   __shared__ int16_t npos[MAXL * 4];  // new position per (node, child); kept uses slot 0
   __shared__ uint8_t nflag[MAXL];     // expanding / in-E / processed flags
   __shared__ int s_var[8];
+  __shared__ uint32_t s_cand[CAP > 0 ? CAP : 1];
+  __shared__ int32_t s_cnode[CAP > 0 ? CAP : 1];
 
-  uint32_t* cand = a.cand + (int64_t)f * a.cand_fstride + L.cand_off;
-  int32_t* cnode = a.cnode + (int64_t)f * a.cand_fstride + L.cand_off;
+  uint32_t* const gcand = a.cand + (int64_t)f * a.cand_fstride + L.cand_off;
+  int32_t* const gcnode = a.cnode + (int64_t)f * a.cand_fstride + L.cand_off;
   const uint32_t* slots = a.slots + (int64_t)f * a.slots_fstride;
   const int32_t* counts = a.cell_counts + (int64_t)f * a.ncells + L.cell_begin;
   const int nc = L.cell_end - L.cell_begin;
@@ -59,14 +64,24 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
     n += tot;
   }
   __syncthreads();
-  {
-    const int wv = tid >> 6, lane = tid & 63;
-    for (int c = wv; c < nc; c += kOctThreads / 64) {
-      const int cnt = counts[c];
-      const uint32_t* src = slots + a.cells[L.cell_begin + c].slot_off;
-      const int dst = s_pref[c];
-      for (int k = lane; k < cnt; k += 64) cand[dst + k] = src[k];
+  const bool inl = n <= CAP;
+  uint32_t* const cand = inl ? s_cand : gcand;
+  int32_t* const cnode = inl ? s_cnode : gcnode;
+  // candidate i of the level: its cell is the last one whose prefix is <= i (empty cells share
+  // their successor's prefix), found by binary search in LDS; every candidate's two dependent
+  // loads are independent of the others (the per-cell walk chained them cell after cell).
+  // The global copy is kept for mcs_extractor_read_stage.
+  _Pragma("unroll 2") for (int i = tid; i < n; i += kOctThreads) {
+    int lo = 0, hi = nc;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_pref[mid] <= i) lo = mid + 1;
+      else hi = mid;
     }
+    const int c = lo - 1;
+    const uint32_t v = slots[a.cells[L.cell_begin + c].slot_off + (i - s_pref[c])];
+    cand[i] = v;
+    if (inl) gcand[i] = v;
   }
   __syncthreads();
 
@@ -383,9 +398,9 @@ void launch_octree(const OctArgs& a, int max_list, hipStream_t st) {
   for (int l = 0; l < a.nlevels; l++) max_cells = std::max(max_cells, a.lv[l].cell_end - a.lv[l].cell_begin);
   // s_pref holds 2*MAXL cell prefixes (the plan rejects > kMaxCellsPerLevel = 2048)
   if (max_list <= 512 && max_cells <= 1024)
-    hipLaunchKernelGGL(k_octree<512>, dim3(g), dim3(kOctThreads), 0, st, a);
+    hipLaunchKernelGGL((k_octree<512, 2048>), dim3(g), dim3(kOctThreads), 0, st, a);
   else
-    hipLaunchKernelGGL(k_octree<1024>, dim3(g), dim3(kOctThreads), 0, st, a);
+    hipLaunchKernelGGL((k_octree<1024, 0>), dim3(g), dim3(kOctThreads), 0, st, a);
 }
 
 }  // namespace mcs
