@@ -225,7 +225,7 @@ struct Dev {
   const int32_t* it_blk; const int32_t* it_chunk; const int32_t* it_slot;  // k_schur items
   const int32_t* fin_blk; const int32_t* fin_slot0; const int32_t* fin_nch;  // k_schur_fin
   double* schur_part;                                 // [slots][42]
-  const double* lam_dev;                              // [0] lambda, [1] lambda on rank 0 else 0
+  double lam, lam0;                                   // lambda; lambda on rank 0, 0 elsewhere
   const int32_t* pr_ptr; const int32_t* pr_e1; const int32_t* pr_e2;  // edge pairs per block
   int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
@@ -235,6 +235,10 @@ struct Dev {
   double* S; double* bs; double* xp;   // S: lower 64x64 tiles (ldlt.hpp), bs / xp: 64 T
   double* hdiag; double* bpf;          // [6 np] Hpp diagonal and b_p (all-reduced when sharded)
   double* red;                         // reduction scratch
+  // trial bookkeeping folded into k_point_trial (each was a 4-5 us copy / fill launch)
+  double* push_poses; double* push_points;  // backups (== poses_bk / points_bk)
+  int n_pose_dbl, n_point_dbl;              // 6 n_poses, 3 n_points
+  int* flag;                                // solve failure flag
 };
 
 // per active edge: error (+ robust chi2) and optionally Jacobians / weight / Hpl = w Jp^T Jl
@@ -417,7 +421,14 @@ __global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
 // also stores Dinv and db = Dinv b_l.
 __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
   const int q = blockIdx.x * 256 + threadIdx.x;
-  const double lam = d.lam_dev[0];
+  const double lam = d.lam;
+  // the trial's push (backup of every pose and point) and the solve-flag reset ride along
+  {
+    const int stride = gridDim.x * 256;
+    for (int i = q; i < d.n_pose_dbl; i += stride) d.push_poses[i] = d.poses[i];
+    for (int i = q; i < d.n_point_dbl; i += stride) d.push_points[i] = d.points[i];
+    if (q == 0) *d.flag = 0;
+  }
   if (q >= d.npe) return;
   const int e = d.pt_edges[q];
   const int l = d.point_h[d.e_point[e]];
@@ -488,7 +499,7 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
 }
 
 __global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
-  const double lam0 = d.lam_dev[1];
+  const double lam0 = d.lam0;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int it = blockIdx.x * 4 + w;
   if (it >= nitem) return;
@@ -545,7 +556,7 @@ __global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
 
 // blocks split into several chunks: sum the chunk slots in chunk order, then write
 __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nfin) {
-  const double lam0 = d.lam_dev[1];
+  const double lam0 = d.lam0;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + w;
   if (f >= nfin) return;
@@ -561,7 +572,7 @@ __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nfin) {
 // across shards, points are not).
 __global__ __launch_bounds__(256) void k_update(Dev d) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  const double lam = d.lam_dev[0];
+  const double lam = d.lam;
   if (k < d.nl) {
     double c[3] = {d.bl[3 * k], d.bl[3 * k + 1], d.bl[3 * k + 2]};
     for (int q = d.pt_ptr[k]; q < d.pt_ptr[k + 1]; q++) {
@@ -592,6 +603,13 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
     }
     d.red[k] = s;
   }
+}
+
+// the trial's pop (restore every pose and point from the backups) in one launch
+__global__ __launch_bounds__(256) void k_restore(Dev d) {
+  const int q = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  for (int i = q; i < d.n_pose_dbl; i += stride) d.poses[i] = d.push_poses[i];
+  for (int i = q; i < d.n_point_dbl; i += stride) d.points[i] = d.push_points[i];
 }
 
 }  // namespace ba
@@ -977,12 +995,16 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   lw.L = dz(ldlt::tile_doubles(T));
   lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
   lw.z = dz((size_t)ldlt::TB * T);
+  // scalars: [0] chi2 [1] point scale [2] pose scale [3] chi_now; the solve flag in [5] (one
+  // 48-byte readback per trial)
   double* d_scalar = dz(8);
   double* d_part = dz(kRedPartMax);
-  double* d_lam = dz(2);
-  d.lam_dev = d_lam;
-  int* d_flag = (int*)c->alloc(16);
-  if (he != hipSuccess || !d_flag) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
+  int* d_flag = reinterpret_cast<int*>(d_scalar + 5);
+  if (he != hipSuccess) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
+  d.push_poses = d_poses_bk; d.push_points = d_points_bk;
+  d.n_pose_dbl = 6 * p->n_poses; d.n_point_dbl = 3 * p->n_points;
+  d.flag = d_flag;
+  const unsigned g_state = gb(std::max(d.n_pose_dbl, d.n_point_dbl));
 
   // control state agreed by all ranks: the caller's stop flag is folded into every scalar
   // exchange, so no rank leaves the LM loop alone
@@ -1003,19 +1025,12 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     agreed_stop = v[1] > 0;
     return MCS_OK;
   };
-  auto copy_state = [&](double* dp, double* dl, const double* sp, const double* sl) -> int {
-    MCS_HIP_CHECK(hipMemcpyAsync(dp, sp, 48 * (size_t)p->n_poses, hipMemcpyDeviceToDevice, st));
-    MCS_HIP_CHECK(hipMemcpyAsync(dl, sl, 24 * (size_t)p->n_points, hipMemcpyDeviceToDevice, st));
-    return MCS_OK;
-  };
-  // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda from pinned[6..7]
+  // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda in d (by value)
   auto enqueue_trial = [&]() -> int {
     int rc2;
-    MCS_HIP_CHECK(hipMemcpyAsync(d_lam, c->pinned + 6, 16, hipMemcpyHostToDevice, st));
-    if ((rc2 = copy_state(d_poses_bk, d_points_bk, d_poses, d_points))) return rc2;  // push
     rec(2);
-    hipLaunchKernelGGL(k_point_trial, dim3(gb(d.npe)), dim3(256), 0, st, d);
-    MCS_HIP_CHECK(hipMemsetAsync(d_flag, 0, 4, st));
+    // also pushes the state (poses / points -> backups) and resets the solve flag
+    hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, d);
     if (s.np) {
       const int nitem = (int)s.it_blk.size(), nfin = (int)s.fin_blk.size();
       hipLaunchKernelGGL(k_schur, dim3((unsigned)((nitem + 3) / 4)), dim3(256), 0, st, d, nitem);
@@ -1035,22 +1050,10 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
     reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
-    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 24, hipMemcpyDeviceToHost, st));
-    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, d_flag, 4, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
     rec(6);
     return MCS_OK;
   };
-  // graph replay of the trial: one rank (no exchange callback inside), no stage timing, and
-  // the LDL^T kernel attributes already set (the first trial of a call runs eagerly)
-  static const bool graph_env = !(std::getenv("MCS_BA_NO_GRAPH") && std::getenv("MCS_BA_NO_GRAPH")[0] == '1');
-  const bool use_graph = graph_env && !sharded && !c->timing;
-  bool graph_ok = true;
-  int trial_no = 0;
-  hipGraphExec_t graph_exec = nullptr;
-  struct GraphGuard {
-    hipGraphExec_t* g;
-    ~GraphGuard() { if (*g) (void)hipGraphExecDestroy(*g); }
-  } graph_guard{&graph_exec};
   double chi0 = 0;
   if ((s.np + nl_glob) == 0 || nae_glob == 0) {
     if (rep) rep->chi2_initial = rep->chi2_final = 0;
@@ -1087,32 +1090,11 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       double rho = 0;
       int qmax = 0;
       do {
-        c->pinned[6] = lambda;
-        c->pinned[7] = sh.rank == 0 ? lambda : 0.0;
-        if (use_graph && !graph_exec && graph_ok && trial_no > 0) {
-          // the trial sequence is fixed within this call: capture it once, replay it per trial
-          // (lambda reaches the kernels through the captured pinned -> device copy)
-          hipGraph_t g = nullptr;
-          if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-            graph_ok = false;
-          } else {
-            const int erc = enqueue_trial();
-            const hipError_t ce = hipStreamEndCapture(st, &g);
-            if (erc != MCS_OK || ce != hipSuccess || !g ||
-                hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0) != hipSuccess) {
-              graph_ok = false;
-              graph_exec = nullptr;
-              (void)hipGetLastError();
-            }
-            if (g) (void)hipGraphDestroy(g);
-          }
-        }
-        if (use_graph && graph_exec) {
-          MCS_HIP_CHECK(hipGraphLaunch(graph_exec, st));
-        } else if ((rc = enqueue_trial())) {
-          return rc;
-        }
-        trial_no++;
+        // lambda reaches the kernels by value (Dev d), no upload; a captured graph of the trial
+        // (replayed per trial) measured no faster than these direct launches
+        d.lam = lambda;
+        d.lam0 = sh.rank == 0 ? lambda : 0.0;
+        if ((rc = enqueue_trial())) return rc;
         MCS_HIP_CHECK(hipStreamSynchronize(st));
         if (c->timing) {
           if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
@@ -1124,7 +1106,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         }
         double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
         const double scale_pose = c->pinned[2];
-        const int fl = c->pinned_i[0];   // identical on every rank (same reduced system)
+        int fl;   // identical on every rank (same reduced system)
+        std::memcpy(&fl, c->pinned + 5, sizeof(fl));
         if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
         agreed_stop = tr[2] > 0;
         double tempChi = tr[0];
@@ -1142,7 +1125,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         } else {
           lambda *= ni;
           ni *= 2;
-          if ((rc = copy_state(d_poses, d_points, d_poses_bk, d_points_bk))) return rc;  // pop
+          hipLaunchKernelGGL(k_restore, dim3(g_state), dim3(256), 0, st, d);  // pop
         }
         qmax++;
       } while (rho < 0 && qmax < o->max_trials && !agreed_stop);
