@@ -333,20 +333,36 @@ void reduce_dev(const double* v, int n, double* out, double* part, hipStream_t s
 }
 
 // per active point: Hll (3x3), b_l over its edges in edge order; diag -> red (for lambda init)
+// four lanes per point (edges q0 + sub, q0 + sub + 4, ...), the quad's partial sums combined
+// in a fixed order ((l0 + l1) + (l2 + l3)): deterministic, and 4x the threads of one lane per
+// point (config C: 3000 points would occupy 12 workgroups)
+__device__ __forceinline__ double quad_sum(double v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  return v;
+}
 __global__ __launch_bounds__(256) void k_points_build(Dev d) {
-  const int l = blockIdx.x * 256 + threadIdx.x;
-  if (l >= d.nl) return;
+  const int gt = blockIdx.x * 256 + threadIdx.x;
+  const int l = gt >> 2, sub = gt & 3;
+  const bool act = l < d.nl;
   double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-  for (int q = d.pt_ptr[l]; q < d.pt_ptr[l + 1]; q++) {
-    const int e = d.pt_edges[q];
-    const double* jl = d.jl + 6 * e;
-    const double w = d.w[e];
-    const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
-    for (int a = 0; a < 3; a++) {
-      for (int bb = 0; bb < 3; bb++) H[3 * a + bb] += w * (jl[a] * jl[bb] + jl[3 + a] * jl[3 + bb]);
-      b[a] += jl[a] * we0 + jl[3 + a] * we1;
+  if (act) {
+    for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
+      const int e = d.pt_edges[q];
+      const double* jl = d.jl + 6 * e;
+      const double w = d.w[e];
+      const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
+      for (int a = 0; a < 3; a++) {
+        for (int bb = 0; bb < 3; bb++) H[3 * a + bb] += w * (jl[a] * jl[bb] + jl[3 + a] * jl[3 + bb]);
+        b[a] += jl[a] * we0 + jl[3 + a] * we1;
+      }
     }
   }
+#pragma unroll
+  for (int i = 0; i < 9; i++) H[i] = quad_sum(H[i]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) b[i] = quad_sum(b[i]);
+  if (!act || sub != 0) return;
   for (int i = 0; i < 9; i++) d.Hll[9 * l + i] = H[i];
   for (int i = 0; i < 3; i++) d.bl[3 * l + i] = b[i];
   d.red[l] = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
@@ -571,11 +587,12 @@ __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nfin) {
 // red[k] (points, k < nl) and red[nl + i] (poses) summed separately (poses are replicated
 // across shards, points are not).
 __global__ __launch_bounds__(256) void k_update(Dev d) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int gt = blockIdx.x * 256 + threadIdx.x;
   const double lam = d.lam;
-  if (k < d.nl) {
-    double c[3] = {d.bl[3 * k], d.bl[3 * k + 1], d.bl[3 * k + 2]};
-    for (int q = d.pt_ptr[k]; q < d.pt_ptr[k + 1]; q++) {
+  if (gt < 4 * d.nl) {   // points: four lanes per point, as k_points_build
+    const int k = gt >> 2, sub = gt & 3;
+    double c[3] = {0.0, 0.0, 0.0};
+    for (int q = d.pt_ptr[k] + sub; q < d.pt_ptr[k + 1]; q += 4) {
       const int e = d.pt_edges[q];
       const int i1 = d.pose_h[d.e_pose[e]];
       if (i1 < 0) continue;
@@ -583,6 +600,9 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
       for (int b = 0; b < 3; b++)
         for (int a = 0; a < 6; a++) c[b] -= B[3 * a + b] * d.xp[6 * i1 + a];
     }
+#pragma unroll
+    for (int b = 0; b < 3; b++) c[b] = d.bl[3 * k + b] + quad_sum(c[b]);
+    if (sub != 0) return;
     const double* Di = d.Dinv + 9 * k;
     double s = 0;
     const int v = d.hpt_vtx[k];
@@ -592,8 +612,8 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
       s += xa * (lam * xa + d.bl[3 * k + a]);
     }
     d.red[k] = s;
-  } else if (k < d.nl + d.np) {
-    const int i = k - d.nl;
+  } else if (gt < 4 * d.nl + d.np) {
+    const int i = gt - 4 * d.nl;
     const int v = d.hpose_vtx[i];
     double s = 0;
     for (int a = 0; a < 6; a++) {
@@ -601,7 +621,7 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
       d.poses[6 * v + a] = d.poses_bk[6 * v + a] + xa;
       s += xa * (lam * xa + d.bpf[6 * i + a]);
     }
-    d.red[k] = s;
+    d.red[d.nl + i] = s;
   }
 }
 
@@ -1045,7 +1065,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       rec(3); rec(4);
     }
     rec(5);
-    hipLaunchKernelGGL(k_update, dim3(gb(s.nl + s.np)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, d);
     reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
     reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
@@ -1071,7 +1091,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       // the first iteration reads anything back (the max diagonal for lambda's init).
       rec(0);
       hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
-      hipLaunchKernelGGL(k_points_build, dim3(gb(s.nl)), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(k_points_build, dim3(gb(4 * s.nl)), dim3(256), 0, st, d);
       if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
       rec(1);
       c->n_iter++;
