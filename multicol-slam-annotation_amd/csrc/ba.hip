@@ -319,6 +319,25 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, i
   if (threadIdx.x == 0) *out = s[0];
 }
 
+// up to three independent k_reduce<false> sums in one launch (workgroup b sums array b, in
+// exactly k_reduce's order): the three closing sums of an LM trial
+struct Sum3 { const double* v[3]; int n[3]; double* out[3]; };
+__global__ __launch_bounds__(1024) void k_reduce3(Sum3 q) {
+  __shared__ double s[1024];
+  const int b = blockIdx.x;
+  const double* v = q.v[b];
+  const int n = q.n[b];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) acc = acc + v[i];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *q.out[b] = s[0];
+}
+
 // launch helper: part = kRedPartMax doubles of scratch (stream-ordered reuse is safe)
 template <bool MAX>
 void reduce_dev(const double* v, int n, double* out, double* part, hipStream_t st) {
@@ -1066,10 +1085,15 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     }
     rec(5);
     hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, d);
-    reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
-    reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+    if (d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768) {   // reduce_dev's one-kernel path
+      Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}, {d_scalar, d_scalar + 1, d_scalar + 2}};
+      hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q);
+    } else {
+      reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
+      reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
+      reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+    }
     MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
     rec(6);
     return MCS_OK;
