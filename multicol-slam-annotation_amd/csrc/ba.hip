@@ -245,7 +245,7 @@ struct Dev {
 __global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= d.nae) return;
-  const int e = d.aedge[k];
+  const int e = d.aedge ? d.aedge[k] : k;   // null: every edge
   const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
   const double* pose = d.poses + 6 * pi;
   const double* X = d.points + 3 * li;
@@ -319,23 +319,35 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, i
   if (threadIdx.x == 0) *out = s[0];
 }
 
-// up to three independent k_reduce<false> sums in one launch (workgroup b sums array b, in
-// exactly k_reduce's order): the three closing sums of an LM trial
-struct Sum3 { const double* v[3]; int n[3]; double* out[3]; };
-__global__ __launch_bounds__(1024) void k_reduce3(Sum3 q) {
-  __shared__ double s[1024];
-  const int b = blockIdx.x;
-  const double* v = q.v[b];
-  const int n = q.n[b];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += 1024) acc = acc + v[i];
-  s[threadIdx.x] = acc;
+// The closing sums of an LM trial (robust chi2, point and pose step norms), each in exactly
+// k_reduce<false>'s order (1024-strided partials, then the LDS tree), computed side by side
+// by one workgroup; the three sums and the solve flag go straight to host-coherent memory
+// and a sequence number is released after them, so the host sees the trial's outcome without
+// a readback copy or a stream synchronisation.
+struct Sum3 { const double* v[3]; int n[3]; };
+struct TrialSig { double v[3]; int32_t flag, pad; uint64_t seq; };
+__global__ __launch_bounds__(1024) void k_reduce3(Sum3 q, const int* flag, TrialSig* sig, uint64_t seq) {
+  __shared__ double s[3][1024];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 3; b++) {
+    double acc = 0.0;
+    for (int i = t; i < q.n[b]; i += 1024) acc = acc + q.v[b][i];
+    s[b][t] = acc;
+  }
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
-    if (threadIdx.x < o) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + o];
+    if (t < o) {
+#pragma unroll
+      for (int b = 0; b < 3; b++) s[b][t] = s[b][t] + s[b][t + o];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *q.out[b] = s[0];
+  if (t == 0) {
+    sig->v[0] = s[0][0]; sig->v[1] = s[1][0]; sig->v[2] = s[2][0];
+    sig->flag = *flag;
+    __hip_atomic_store(&sig->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // launch helper: part = kRedPartMax doubles of scratch (stream-ordered reuse is safe)
@@ -667,6 +679,8 @@ struct mcs_ba_ctx {
   size_t next = 0;
   double* pinned = nullptr;   // host-pinned readback scalars
   int32_t* pinned_i = nullptr;
+  TrialSig* sig = nullptr;    // host-coherent trial outcome (k_reduce3)
+  uint64_t sig_seq = 0;
   // host-pinned staging of a call's packed problem upload (grow-only)
   uint8_t* stage = nullptr;
   size_t stage_cap = 0;
@@ -713,6 +727,7 @@ struct HostStruct {
   std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
       ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, fin_blk,
       fin_slot0, fin_nch;
+  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
   int n_slots = 0;
   int np = 0, nl = 0;
 };
@@ -768,31 +783,59 @@ void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_
   for (int i = 0, b = 0; i < s.np; i++)
     for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
   s.pr_ptr.assign(nblk + 1, 0);
-  auto for_pairs = [&](auto&& f) {
-    for (int l = 0; l < s.nl; l++) {
-      const int q0 = s.pt_ptr[l], q1 = s.pt_ptr[l + 1];
-      for (int a = q0; a < q1; a++) {
-        const int e1 = s.pt_edges[a];
-        const int i1 = s.pose_h[p.edge_pose[e1]];
-        if (i1 < 0) continue;
-        for (int b = q0; b < q1; b++) {
-          const int e2 = s.pt_edges[b];
-          const int i2 = s.pose_h[p.edge_pose[e2]];
-          if (i2 < 0 || i2 > i1) continue;
-          f((size_t)i1 * (i1 + 1) / 2 + i2, e1, e2);
-        }
-      }
+  // Per point, its edges with an active pose, grouped by pose (stable, so edge order inside
+  // a group): the pairs of block (i1, i2), i2 <= i1, that a point contributes are then the
+  // product group(i1) x group(i2) in (e1, e2) order -- the order of the plain double loop over
+  // the point's edges, without visiting the pairs that fall above the diagonal.
+  std::vector<int32_t>& ge = s.tmp_e;   // grouped edges, point by point
+  std::vector<int32_t>& gr = s.tmp_g;   // groups: (pose, begin, end) triples
+  std::vector<int32_t>& gp = s.tmp_p;   // per point: first group (nl + 1 entries)
+  ge.clear(); gr.clear(); gp.assign(s.nl + 1, 0);
+  for (int l = 0; l < s.nl; l++) {
+    const size_t b0 = ge.size();
+    for (int a = s.pt_ptr[l]; a < s.pt_ptr[l + 1]; a++) {
+      const int e = s.pt_edges[a];
+      const int h = s.pose_h[p.edge_pose[e]];
+      if (h < 0) continue;
+      // insertion into (pose, edge order), stable
+      ge.push_back(e);
+      size_t q = ge.size() - 1;
+      while (q > b0 && s.pose_h[p.edge_pose[ge[q - 1]]] > h) { ge[q] = ge[q - 1]; q--; }
+      ge[q] = e;
     }
+    for (size_t q = b0; q < ge.size();) {
+      const int h = s.pose_h[p.edge_pose[ge[q]]];
+      size_t r = q + 1;
+      while (r < ge.size() && s.pose_h[p.edge_pose[ge[r]]] == h) r++;
+      gr.push_back(h); gr.push_back((int32_t)q); gr.push_back((int32_t)r);
+      q = r;
+    }
+    gp[l + 1] = (int32_t)(gr.size() / 3);
+  }
+  auto for_blocks = [&](auto&& f) {   // f(block, group of i1, group of i2), point by point
+    for (int l = 0; l < s.nl; l++)
+      for (int gi = gp[l]; gi < gp[l + 1]; gi++) {
+        const int h1 = gr[3 * gi];
+        for (int gj = gp[l]; gj <= gi; gj++)
+          f((size_t)h1 * (h1 + 1) / 2 + gr[3 * gj], gi, gj);
+      }
   };
-  for_pairs([&](size_t blk, int, int) { s.pr_ptr[blk + 1]++; });
+  for_blocks([&](size_t blk, int gi, int gj) {
+    s.pr_ptr[blk + 1] += (gr[3 * gi + 2] - gr[3 * gi + 1]) * (gr[3 * gj + 2] - gr[3 * gj + 1]);
+  });
   for (size_t b = 0; b < nblk; b++) s.pr_ptr[b + 1] += s.pr_ptr[b];
   s.pr_e1.assign(s.pr_ptr[nblk], 0);
   s.pr_e2.assign(s.pr_ptr[nblk], 0);
-  std::vector<int32_t> fill(s.pr_ptr.begin(), s.pr_ptr.end() - 1);
-  for_pairs([&](size_t blk, int e1, int e2) {
-    const int q = fill[blk]++;
-    s.pr_e1[q] = e1;
-    s.pr_e2[q] = e2;
+  std::vector<int32_t>& fill = s.tmp_f;
+  fill.assign(s.pr_ptr.begin(), s.pr_ptr.end() - 1);
+  for_blocks([&](size_t blk, int gi, int gj) {
+    int q = fill[blk];
+    for (int a = gr[3 * gi + 1]; a < gr[3 * gi + 2]; a++)
+      for (int b = gr[3 * gj + 1]; b < gr[3 * gj + 2]; b++, q++) {
+        s.pr_e1[q] = ge[a];
+        s.pr_e2[q] = ge[b];
+      }
+    fill[blk] = q;
   });
   // k_schur work items: chunks of kSchurChunk pairs (and, on diagonal blocks, pose edges)
   s.it_blk.clear(); s.it_chunk.clear(); s.it_slot.clear();
@@ -970,7 +1013,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     cnt[p->n_poses + 1] = nae_l;
     if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
   }
-  HostStruct s;
+  thread_local HostStruct hs;   // capacity reused across calls (no fresh pages per call)
+  HostStruct& s = hs;
   build_structure(*p, edge_level, points_fixed, cnt, s);
   const int nl_glob = (int)cnt[p->n_poses], nae_glob = (int)cnt[p->n_poses + 1];
   if (rep) {
@@ -1051,6 +1095,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
   volatile int32_t* stop = stop_flag ? stop_flag : &aux;
   int agreed_stop = 0;
   const size_t sc = X.sc;
+  const bool sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
 
   auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate (all ranks)
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
@@ -1086,16 +1131,43 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     rec(5);
     hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, d);
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    if (d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768) {   // reduce_dev's one-kernel path
-      Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}, {d_scalar, d_scalar + 1, d_scalar + 2}};
-      hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q);
+    if (sig_path) {
+      Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}};
+      hipLaunchKernelGGL(k_reduce3, dim3(1), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
     } else {
       reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
       reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
       reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+      MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
     }
-    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
     rec(6);
+    return MCS_OK;
+  };
+  // wait for the trial's outcome: spin on the released sequence number (sig_path), checking
+  // the stream now and then so a failed launch cannot spin forever; else synchronise the
+  // stream after the readback copy.  Fills pinned[0..2] and the solve flag.
+  auto wait_trial = [&](int* fl) -> int {
+    if (!sig_path) {
+      MCS_HIP_CHECK(hipStreamSynchronize(st));
+      std::memcpy(fl, c->pinned + 5, sizeof(*fl));
+      return MCS_OK;
+    }
+    const uint64_t want = c->sig_seq;
+    for (uint32_t k = 1;; k++) {
+      if (__atomic_load_n(&c->sig->seq, __ATOMIC_ACQUIRE) == want) break;
+      if ((k & 1023) == 0) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) {
+          if (__atomic_load_n(&c->sig->seq, __ATOMIC_ACQUIRE) == want) break;
+          set_error("BA: trial signal missing after the stream drained");
+          return MCS_ERR_HIP;
+        }
+        if (q != hipErrorNotReady) { set_hip_error(q, "BA trial", __FILE__, __LINE__); return MCS_ERR_HIP; }
+      }
+    }
+    c->pinned[0] = c->sig->v[0]; c->pinned[1] = c->sig->v[1]; c->pinned[2] = c->sig->v[2];
+    *fl = c->sig->flag;
+    if (c->timing) MCS_HIP_CHECK(hipStreamSynchronize(st));   // events complete
     return MCS_OK;
   };
   double chi0 = 0;
@@ -1139,7 +1211,8 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         d.lam = lambda;
         d.lam0 = sh.rank == 0 ? lambda : 0.0;
         if ((rc = enqueue_trial())) return rc;
-        MCS_HIP_CHECK(hipStreamSynchronize(st));
+        int fl;   // identical on every rank (same reduced system)
+        if ((rc = wait_trial(&fl))) return rc;
         if (c->timing) {
           if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
           c->acc_ms[1] += ms(2, 3);
@@ -1150,8 +1223,6 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
         }
         double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
         const double scale_pose = c->pinned[2];
-        int fl;   // identical on every rank (same reduced system)
-        std::memcpy(&fl, c->pinned + 5, sizeof(fl));
         if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
         agreed_stop = tr[2] > 0;
         double tempChi = tr[0];
@@ -1204,22 +1275,29 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     if (rep) rep->chi2_final = currentChi;
   }
   if (rep) rep->stop_flag = *stop;
-  MCS_HIP_CHECK(hipMemcpyAsync(poses, d_poses, 48 * (size_t)p->n_poses, hipMemcpyDeviceToHost, st));
-  MCS_HIP_CHECK(hipMemcpyAsync(points, d_points, 24 * (size_t)p->n_points, hipMemcpyDeviceToHost, st));
+  // results through the pinned staging buffer (free again: the stream has been drained since
+  // the upload), then one host copy each
   if (edge_chi2) {
     // chi2 of every edge (active or not) at the final estimate
-    std::vector<int32_t> all(NE);
-    for (int e = 0; e < NE; e++) all[e] = e;
-    int32_t* d_all = up(c, all, he);
-    if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
     Dev d2 = d;
-    d2.aedge = d_all;
+    d2.aedge = nullptr;
     d2.nae = NE;
     d2.rchi = dz(NE);
+    if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
     hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
-    MCS_HIP_CHECK(hipMemcpyAsync(edge_chi2, d.chi, 8 * (size_t)NE, hipMemcpyDeviceToHost, st));
   }
+  const size_t b_po = 48 * (size_t)p->n_poses, b_pt = 24 * (size_t)p->n_points;
+  const size_t b_ch = edge_chi2 ? 8 * (size_t)NE : 0;
+  if (b_po + b_pt + b_ch + 64 > c->stage_cap) MCS_HIP_CHECK(hipStreamSynchronize(st));   // regrow
+  uint8_t* hst = c->stage_get(b_po + b_pt + b_ch + 64);
+  if (!hst) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
+  if (b_po) MCS_HIP_CHECK(hipMemcpyAsync(hst, d_poses, b_po, hipMemcpyDeviceToHost, st));
+  if (b_pt) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po, d_points, b_pt, hipMemcpyDeviceToHost, st));
+  if (b_ch) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt, d.chi, b_ch, hipMemcpyDeviceToHost, st));
   MCS_HIP_CHECK(hipStreamSynchronize(st));
+  if (b_po) std::memcpy(poses, hst, b_po);
+  if (b_pt) std::memcpy(points, hst + b_po, b_pt);
+  if (b_ch) std::memcpy(edge_chi2, hst + b_po + b_pt, b_ch);
   MCS_HIP_CHECK(hipGetLastError());
   return MCS_OK;
 }
@@ -1250,6 +1328,8 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocDefault));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->sig, sizeof(TrialSig), hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset((void*)c->sig, 0, sizeof(TrialSig));
   *out = c;
   return MCS_OK;
 }
@@ -1261,6 +1341,7 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
   c->release();
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_i) (void)hipHostFree(c->pinned_i);
+  if (c->sig) (void)hipHostFree(c->sig);
   if (c->stage) (void)hipHostFree(c->stage);
   if (c->st) (void)hipStreamDestroy(c->st);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);

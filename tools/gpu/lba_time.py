@@ -9,12 +9,15 @@ pr = mba.make_problem(seed=1)
 s = mba.Solver(device=0)
 s.local_ba(pr)
 N = 20
-t0 = time.perf_counter()
-for _ in range(N):
+ts = []
+for _ in range(100):
+    t0 = time.perf_counter()
     r = s.local_ba(pr)
-wall = (time.perf_counter() - t0) / N * 1e3
+    ts.append((time.perf_counter() - t0) * 1e3)
+wall = float(np.median(ts))
 its = r["report1"].iterations + r["report2"].iterations
-print("wall ms/call %.3f  iterations/call %d  ms/iter %.4f" % (wall, its, wall / its))
+print("wall ms/call median %.3f  min %.3f  mean %.3f  iterations/call %d  ms/iter %.4f" % (
+    wall, min(ts), np.mean(ts), its, wall / its))
 s.enable_timing(True)
 for _ in range(N):
     r = s.local_ba(pr)
@@ -25,8 +28,10 @@ s.enable_timing(False)
 for mi in (0, 1, 2, 5, 10):
     o1 = mba.BAOptions(max_iterations=mi)
     s.optimize(pr, o1)
-    t0 = time.perf_counter()
-    for _ in range(N):
+    ts = []
+    for _ in range(50):
+        t0 = time.perf_counter()
         r = s.optimize(pr, o1)
-    print("optimize(max_iterations=%d) ms/call %.3f  iterations %d" % (
-        mi, (time.perf_counter() - t0) / N * 1e3, r["report"].iterations))
+        ts.append((time.perf_counter() - t0) * 1e3)
+    print("optimize(max_iterations=%d) ms/call median %.3f  min %.3f  iterations %d" % (
+        mi, float(np.median(ts)), min(ts), r["report"].iterations))
