@@ -319,34 +319,30 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ v, i
   if (threadIdx.x == 0) *out = s[0];
 }
 
-// The closing sums of an LM trial (robust chi2, point and pose step norms), each in exactly
-// k_reduce<false>'s order (1024-strided partials, then the LDS tree), computed side by side
-// by one workgroup; the three sums and the solve flag go straight to host-coherent memory
-// and a sequence number is released after them, so the host sees the trial's outcome without
-// a readback copy or a stream synchronisation.
+// The closing sums of an LM trial (robust chi2, point and pose step norms), one workgroup
+// each, in exactly k_reduce<false>'s order (1024-strided partials, then the LDS tree); every
+// sum goes straight to host-coherent memory with its own released sequence number (the solve
+// flag with the first), so the host sees the trial's outcome without a readback copy or a
+// stream synchronisation.
 struct Sum3 { const double* v[3]; int n[3]; };
-struct TrialSig { double v[3]; int32_t flag, pad; uint64_t seq; };
+struct TrialSig { double v[3]; int32_t flag, pad; uint64_t seq[3]; };
 __global__ __launch_bounds__(1024) void k_reduce3(Sum3 q, const int* flag, TrialSig* sig, uint64_t seq) {
-  __shared__ double s[3][1024];
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int b = 0; b < 3; b++) {
-    double acc = 0.0;
-    for (int i = t; i < q.n[b]; i += 1024) acc = acc + q.v[b][i];
-    s[b][t] = acc;
-  }
+  __shared__ double s[1024];
+  const int t = threadIdx.x, b = blockIdx.x;
+  const double* v = q.v[b];
+  const int n = q.n[b];
+  double acc = 0.0;
+  for (int i = t; i < n; i += 1024) acc = acc + v[i];
+  s[t] = acc;
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
-    if (t < o) {
-#pragma unroll
-      for (int b = 0; b < 3; b++) s[b][t] = s[b][t] + s[b][t + o];
-    }
+    if (t < o) s[t] = s[t] + s[t + o];
     __syncthreads();
   }
   if (t == 0) {
-    sig->v[0] = s[0][0]; sig->v[1] = s[1][0]; sig->v[2] = s[2][0];
-    sig->flag = *flag;
-    __hip_atomic_store(&sig->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    sig->v[b] = s[0];
+    if (b == 0) sig->flag = *flag;
+    __hip_atomic_store(&sig->seq[b], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1133,7 +1129,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
     if (sig_path) {
       Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}};
-      hipLaunchKernelGGL(k_reduce3, dim3(1), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
+      hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
     } else {
       reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
       reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
@@ -1153,12 +1149,17 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       return MCS_OK;
     }
     const uint64_t want = c->sig_seq;
+    auto arrived = [&]() {
+      return __atomic_load_n(&c->sig->seq[0], __ATOMIC_ACQUIRE) == want &&
+             __atomic_load_n(&c->sig->seq[1], __ATOMIC_ACQUIRE) == want &&
+             __atomic_load_n(&c->sig->seq[2], __ATOMIC_ACQUIRE) == want;
+    };
     for (uint32_t k = 1;; k++) {
-      if (__atomic_load_n(&c->sig->seq, __ATOMIC_ACQUIRE) == want) break;
+      if (arrived()) break;
       if ((k & 1023) == 0) {
         const hipError_t q = hipStreamQuery(st);
         if (q == hipSuccess) {
-          if (__atomic_load_n(&c->sig->seq, __ATOMIC_ACQUIRE) == want) break;
+          if (arrived()) break;
           set_error("BA: trial signal missing after the stream drained");
           return MCS_ERR_HIP;
         }
