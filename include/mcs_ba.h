@@ -231,6 +231,11 @@ int mcs_ba_read_timing(mcs_ba_ctx* c, double* ms, int32_t* n_iterations, int32_t
  * triangle read), b and x length n.  *zero_pivot = 1 when the LDL^T meets an exact zero. */
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
                          int32_t* zero_pivot);
+/* Same, choosing the kernels: path 0 = what the BA uses (n <= 64: the fused one-tile solve,
+ * else pad + panel steps + backward), path 1 = always pad + panel steps + backward.  Both
+ * give bitwise equal x (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled). */
+int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
+                            int32_t* zero_pivot, int32_t path);
 
 #ifdef __cplusplus
 }

@@ -1116,11 +1116,13 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
       hipLaunchKernelGGL(k_schur, dim3((unsigned)((nitem + 3) / 4)), dim3(256), 0, st, d, nitem);
       if (nfin)
         hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nfin + 3) / 4)), dim3(256), 0, st, d, nfin);
-      MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
+      // one tile (LocalBA): the padding is applied inside the fused solve, after the exchange
+      if (T > 1) MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
       rec(3);
       if ((rc2 = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc2;   // S tiles | bs
       rec(4);
-      MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
+      if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st));
+      else MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
     } else {
       rec(3); rec(4);
     }
@@ -1542,7 +1544,12 @@ int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double
 
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
                          int32_t* zero_pivot) {
-  if (!S || !b || !x || n < 1) return MCS_ERR_ARG;
+  return mcs_dense_ldlt_solve_ex(device, S, n, b, x, zero_pivot, 0);
+}
+
+int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
+                            int32_t* zero_pivot, int32_t path) {
+  if (!S || !b || !x || n < 1 || path < 0 || path > 1) return MCS_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     set_error("no HIP device visible (no CPU fallback)");
@@ -1572,9 +1579,13 @@ int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const doubl
     chk(hipMemcpyAsync(dA, hA.data(), NT * 8, hipMemcpyHostToDevice, st), "h2d");
     chk(hipMemcpyAsync(db, hb.data(), Np * 8, hipMemcpyHostToDevice, st), "h2d");
     chk(hipMemsetAsync(dflag, 0, 4, st), "memset");
-    chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
-    ldlt::Work w{dL, dI, dz};
-    chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
+    if (T == 1 && path == 0) {
+      chk(ldlt::solve_one_tile(dA, db, dx, n, 1.0, dflag, st), "ldlt");
+    } else {
+      chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
+      ldlt::Work w{dL, dI, dz};
+      chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
+    }
     std::vector<double> hx(Np);
     int32_t fl = 0;
     chk(hipMemcpyAsync(hx.data(), dx, Np * 8, hipMemcpyDeviceToHost, st), "d2h");

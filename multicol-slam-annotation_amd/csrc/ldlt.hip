@@ -445,7 +445,77 @@ __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int
   if (threadIdx.x == 0) b[r] = 0.0;
 }
 
+// The whole solve of a one-tile system (n <= 64: LocalBA-sized), one launch instead of
+// k_pad + k_panel + k_backward, with the same arithmetic: the padding rows are set as k_pad
+// writes them (diag_value on the diagonal, zero right-hand side), the tile is factored and
+// u = Linv b, z = u / D formed as k_panel's workgroup 0 does, and x = Linv^T z as
+// k_backward's one step (whose empty off-diagonal sum is +0: r = z exactly), in the same
+// partial layout and summation order.
+__global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, const double* __restrict__ b,
+                                                double* __restrict__ x, int n, double dv, int* flag) {
+  extern __shared__ double sm[];
+  double* sK = sm;               // A -> L (strict lower) + D (diagonal)
+  double* sI = sK + TB * LS;     // Linv
+  double* sv = sI + TB * LS;     // b, then z
+  double* su = sv + TB;          // u
+  double* part = su + TB;        // [16][TB]
+  __shared__ int fail;
+  const int t = threadIdx.x;
+  if (t == 0) fail = 0;
+  d2 vK[8];
+  fetch_tile(vK, A);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = 2 * (t + 256 * i), r = e >> 6, c = e & 63;
+    if (r >= n) {
+      vK[i].x = (c == r) ? dv : 0.0;
+      vK[i].y = (c + 1 == r) ? dv : 0.0;
+    }
+  }
+  if (t < TB) sv[t] = t < n ? b[t] : 0.0;
+  put_tile_lower(sK, vK);
+  __syncthreads();
+  factor_tile(sK, sI, &fail);
+  const double u = gemv_row(sI, sv);
+  if ((t & 3) == 0) su[t >> 2] = u;
+  __syncthreads();
+  if (t < TB) sv[t] = su[t] / sK[t * LS + t];
+  if (t == 0 && fail) *flag = 1;
+  __syncthreads();
+  const int c = t & 63;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int g = (t >> 6) + 4 * m;
+    double v = sI[g * LS + c] * sv[g] + sI[(g + 16) * LS + c] * sv[g + 16];
+    v += sI[(g + 32) * LS + c] * sv[g + 32] + sI[(g + 48) * LS + c] * sv[g + 48];
+    part[g * TB + c] = v;
+  }
+  __syncthreads();
+  if (t < TB) {
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc += part[q * TB + t];
+    x[t] = acc;
+  }
+}
+
 }  // namespace
+
+constexpr size_t kSolve1Lds = (2 * (size_t)TB * LS + 18 * TB) * sizeof(double);
+
+hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
+                          hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_solve1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kSolve1Lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  if (n < 1 || n > TB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_solve1, dim3(1), dim3(256), kSolve1Lds, st, A, b, x, n, diag_value, flag);
+  return hipGetLastError();
+}
 
 constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
 

@@ -39,6 +39,10 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
 
 // Padding rows/columns [n, 64T): diagonal = diag_value, rest 0; b[n..64T) = 0.
 hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st);
+// pad + solve of a one-tile system (n <= 64) in one launch, bitwise equal to pad + solve
+// (diag_value: the padding diagonal after any exchange, i.e. 1)
+hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
+                          hipStream_t st);
 
 }  // namespace ldlt
 }  // namespace mcs

@@ -127,6 +127,7 @@ SIGNATURES = {
     "mcs_ba_optimize_sharded": (ctypes.c_int, [_P] * 10),
     "mcs_global_ba": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_dense_ldlt_solve": (ctypes.c_int, [_I32, _P, _I32, _P, _P, _P]),
+    "mcs_dense_ldlt_solve_ex": (ctypes.c_int, [_I32, _P, _I32, _P, _P, _P, _I32]),
     "mcs_ba_enable_timing": (ctypes.c_int, [_P, _I32]),
     "mcs_ba_read_timing": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32]),
     "mcs_pose_optimization": (ctypes.c_int, [_P] * 8),

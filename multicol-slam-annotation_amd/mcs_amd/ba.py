@@ -714,15 +714,17 @@ Solver.global_ba = _solver_global_ba
 Solver.optimize_sharded = _solver_optimize_sharded
 
 
-def dense_ldlt_solve(S, b, device=0):
-    """Device LDL^T solve of the reduced camera system (test hook) -> (x, zero_pivot)."""
+def dense_ldlt_solve(S, b, device=0, tiled=False):
+    """Device LDL^T solve of the reduced camera system (test hook) -> (x, zero_pivot).
+    tiled=True forces the pad + panel + backward kernels even for n <= 64."""
     from . import lib, _check
     S = np.ascontiguousarray(S, np.float64)
     b = np.ascontiguousarray(b, np.float64)
     n = S.shape[0]
     x = np.zeros(n)
     zp = ctypes.c_int32()
-    _check(lib().mcs_dense_ldlt_solve(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp)))
+    _check(lib().mcs_dense_ldlt_solve_ex(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp),
+                                         1 if tiled else 0))
     return x, zp.value
 
 

@@ -152,6 +152,31 @@ def test_gpu_dense_ldlt_solve(gpu, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 7, 36, 60, 63, 64])
+def test_gpu_one_tile_solve_matches_tiled(gpu, n):
+    """The fused one-tile solve (LocalBA systems) is bitwise the pad + panel + backward path,
+    including a zero pivot and a right-hand side with signed zeros."""
+    from mcs_amd import ba
+    rng = np.random.default_rng(100 + n)
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    b[::5] = -0.0
+    x0, z0 = ba.dense_ldlt_solve(S, b)
+    x1, z1 = ba.dense_ldlt_solve(S, b, tiled=True)
+    assert z0 == z1 == 0
+    assert x0.tobytes() == x1.tobytes()
+    if n > 3:
+        S2 = S.copy()
+        S2[2, :] = 0.0
+        S2[:, 2] = 0.0
+        x0, z0 = ba.dense_ldlt_solve(S2, b)
+        x1, z1 = ba.dense_ldlt_solve(S2, b, tiled=True)
+        assert z0 == z1 == 1
+        assert np.array_equal(x0, x1, equal_nan=True)
+
+
+@pytest.mark.gpu
 def test_gpu_dense_ldlt_zero_pivot(gpu):
     from mcs_amd import ba
     S = np.eye(70)
