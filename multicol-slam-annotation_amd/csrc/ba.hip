@@ -525,7 +525,7 @@ __device__ __forceinline__ double readlane0_d(double v) {
 // k_schur_fin adds the slots in chunk order (config C: 55 blocks of thousands of pairs, so a
 // block per wave would leave the GPU idle).  Every order is fixed: bitwise reproducible.
 // lam0 = lambda on rank 0 and 0 elsewhere (the sharded sum then holds lambda once).
-constexpr int kSchurChunk = 256;
+constexpr int kSchurChunk = 128;   // pairs per wave (config C: 128 beat 32 / 64 / 256)
 
 __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double lam0, int lane,
                                             double v) {
