@@ -77,19 +77,22 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     from tests import oracle_bind as ob
     ob.lib()
     nkp = 0
+    kpss = [[None] * ncams for _ in range(n_multiframes)]
     descs = [[None] * ncams for _ in range(n_multiframes)]
+    top2 = [[None] * ncams for _ in range(n_multiframes - 1)]
     lock = threading.Lock()
 
     def work(c):
         nonlocal nkp
         for t in range(n_multiframes):
             k, d = ob.extract(imgs[t * ncams + c], masks[c], nfeatures=nfeatures)
+            kpss[t][c] = k
             descs[t][c] = d
             with lock:
                 nkp += len(k)
         for t in range(1, n_multiframes):
             q, tr = descs[t - 1][c], descs[t][c]
-            _ = _oracle_top2(ob, q, tr)
+            top2[t - 1][c] = ob.hamming_top2(q, tr)
 
     t0 = time.perf_counter()
     ths = [threading.Thread(target=work, args=(c,)) for c in range(ncams)]
@@ -99,7 +102,41 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
         th.join()
     dt = time.perf_counter() - t0
     sample = "%d multi-frames x %d cams (extract+match), oracle restatement" % (n_multiframes, ncams)
-    return nkp / dt / 1e3, sample, ncams
+    return nkp / dt / 1e3, sample, ncams, (kpss, descs, top2)
+
+
+def check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, ncams):
+    """Untimed post-run parity check of the timed batch: the camera-frames and match pairs the
+    CPU baseline leg computed (the first multi-frames of the batch) against the GPU's outputs of
+    the LAST timed step, bit-exact: keypoint fields, descriptors, (best idx, best dist, second
+    dist).  Returns a summary dict; raises if anything differs."""
+    import mcs_amd
+    kpss, descs, top2 = ref
+    cap = d_kps.shape[1] // 7
+    nmf = len(kpss)
+    frames = [t * ncams + c for t in range(nmf) for c in range(ncams)]
+    cnt = d_cnt.cpu().numpy()
+    kp = d_kps[:len(frames)].cpu().numpy().view(mcs_amd.KEYPOINT_DTYPE).reshape(len(frames), cap)
+    de = d_desc[:len(frames)].cpu().numpy()
+    for f in frames:
+        t, c = divmod(f, ncams)
+        n = len(kpss[t][c])
+        if cnt[f] != n or not np.array_equal(kp[f, :n], kpss[t][c]) or \
+                not np.array_equal(de[f, :n], descs[t][c]):
+            raise RuntimeError("bench parity: camera-frame %d differs from the oracle" % f)
+    npairs = (nmf - 1) * ncams
+    m = [x[:npairs].cpu().numpy() for x in d_m]
+    for t in range(nmf - 1):
+        for c in range(ncams):
+            p = t * ncams + c
+            n = len(kpss[t][c])
+            bi, bd, sd = top2[t][c]
+            if not (np.array_equal(m[0][p, :n], bi) and np.array_equal(m[1][p, :n], bd)
+                    and np.array_equal(m[3][p, :n], sd)):
+                raise RuntimeError("bench parity: match pair %d differs from the oracle" % p)
+    return {"camera_frames_bitexact": len(frames), "match_pairs_bitexact": npairs,
+            "keypoints_checked": int(sum(len(k) for row in kpss for k in row)),
+            "of_step": "last timed step"}
 
 
 def single_multiframe_latency(ex, d_img, d_midx, d_kps, d_cnt, d_desc, ncams, stream, reps):
@@ -140,18 +177,6 @@ def host_cpu_info():
         avail = os.cpu_count()
     return {"cpu_model": model, "host_threads_visible": avail,
             "oracle_build": "g++ -O3 -ffp-contract=off -fno-fast-math (portable x86-64, no -march)"}
-
-
-def _oracle_top2(ob, q, t):
-    import ctypes
-    n = len(q)
-    bi = np.zeros(n, np.int32)
-    bd = np.zeros(n, np.int32)
-    sd = np.zeros(n, np.int32)
-    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    ob.lib().oracle_hamming_top2(p(np.ascontiguousarray(q)), len(q), p(np.ascontiguousarray(t)),
-                                 len(t), q.shape[1], p(bi), p(bd), p(sd))
-    return bi, bd, sd
 
 
 def run_global_ba(args, rank, world, local_rank, dev):
@@ -463,9 +488,7 @@ def main():
     W, H, NC = 754, 480, 3
     M = args.multiframes
     U = min(args.unique, M)
-    uimgs, masks = synth.rig_sequence(U, W, H, NC, seed=1 + rank)
-    idx = np.arange(M) % U
-    imgs = uimgs.reshape(U, NC, H, W)[idx].reshape(M * NC, H, W)
+    uimgs, imgs, masks, midx, pairs = synth.config_b_batch(M, U, rank, W, H, NC)
     F = M * NC
 
     params = mcs_amd.ExtractorParams(nfeatures=args.nfeatures, fast_threshold=20)
@@ -474,12 +497,10 @@ def main():
     d_img = torch.from_numpy(imgs).to(dev)
     d_mask = torch.from_numpy(masks).to(dev)
     ex.set_masks_device(d_mask.data_ptr(), NC, stream.cuda_stream)
-    d_midx = torch.from_numpy(np.tile(np.arange(NC, dtype=np.int32), M)).to(dev)
+    d_midx = torch.from_numpy(midx).to(dev)
     d_kps = torch.zeros((F, cap * 7), dtype=torch.int32, device=dev)
     d_cnt = torch.zeros(F, dtype=torch.int32, device=dev)
     d_desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
-    pairs = np.array([[t * NC + c, (t + 1) * NC + c] for t in range(M - 1) for c in range(NC)],
-                     np.int32)
     d_pairs = torch.from_numpy(pairs).to(dev)
     NP = len(pairs)
     d_m = [torch.zeros((NP, cap), dtype=torch.int32, device=dev) for _ in range(4)]
@@ -583,12 +604,14 @@ def main():
     cfg_d = run_config_d(args, rank, world, local_rank, dev, stream)
 
     cpu = None
+    parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         S = min(args.cpu_sample, U)
-        v, sample, cores = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
+        v, sample, cores, ref = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
         cpu = {"value": round(v, 3), "unit": "kfeatures/s", "cores": cores, "kind": "port",
                "sample": sample}
         cpu.update(host_cpu_info())
+        parity = check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, NC)
 
     if rank == 0:
         out = {
@@ -612,6 +635,7 @@ def main():
                        "parallelism": "dp%d (independent multi-frame segments)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity_check": parity,
             "localba": localba,
             "cpu_baseline_localba": cpu_ba,
             "globalba": gba,

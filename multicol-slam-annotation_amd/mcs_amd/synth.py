@@ -203,6 +203,23 @@ def rig_sequence(n_multiframes, width=754, height=480, ncams=3, seed=0, yaw_step
     return imgs, masks
 
 
+def config_b_batch(n_multiframes=171, n_unique=12, rank=0, width=754, height=480, ncams=3):
+    """The headline workload's input (bench.py config B), built the same way for the bench and
+    for its parity test: `n_unique` rendered multi-frames of the moving Lafida rig, repeated to
+    `n_multiframes` (t-major, camera-minor camera-frames), the per-camera mirror masks, the
+    camera index of every frame, and the match pairs (camera c of multi-frame t against camera
+    c of t+1, SearchForTriangulationRaw's same-camera rule, src/cORBmatcher.cpp:1040-1041).
+    Returns (unique_imgs, imgs, masks, mask_index, pairs)."""
+    U = min(n_unique, n_multiframes)
+    uimgs, masks = rig_sequence(U, width, height, ncams, seed=1 + rank)
+    idx = np.arange(n_multiframes) % U
+    imgs = uimgs.reshape(U, ncams, height, width)[idx].reshape(n_multiframes * ncams, height, width)
+    midx = np.tile(np.arange(ncams, dtype=np.int32), n_multiframes)
+    pairs = np.array([[t * ncams + c, (t + 1) * ncams + c]
+                      for t in range(n_multiframes - 1) for c in range(ncams)], np.int32)
+    return uimgs, imgs, masks, midx, pairs
+
+
 def random_frame(width, height, seed):
     """Unstructured uniform-noise frame (edge-case tests: many weak corners)."""
     return np.random.default_rng(seed).integers(0, 256, (height, width), dtype=np.uint8)

@@ -179,6 +179,19 @@ def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, de
     return kps[:n.value].copy(), desc[:n.value].copy()
 
 
+def hamming_top2(q, t):
+    """Dense best / second-best Hamming of every query row against every train row
+    (ties: lowest train index) -> (best_idx, best_dist, second_dist)."""
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    n = len(q)
+    bi = np.zeros(n, np.int32)
+    bd = np.zeros(n, np.int32)
+    sd = np.zeros(n, np.int32)
+    lib().oracle_hamming_top2(_p(q), n, _p(t), len(t), q.shape[1], _p(bi), _p(bd), _p(sd))
+    return bi, bd, sd
+
+
 def extract_ex(img, cam, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20,
                desc_size=32, do_dbrief=1, learn_masks=0, mode=1):
     """dBRIEF / mdBRIEF oracle: -> (kps, desc, desc_masks).  cam: mcs_amd.CamModel."""
