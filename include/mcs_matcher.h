@@ -79,6 +79,21 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
                                             double epi_thresh, int32_t* matches12,
                                             int32_t* n_matches);
 
+/* The essential matrices SearchForTriangulationRaw precomputes per camera pair
+ * (src/cORBmatcher.cpp:985-998): E[i][j] = ComputeE(KF1.Get_MtMc_inv(i), KF2.Get_MtMc(j))
+ * (src/misc.cpp:72-86), the rig poses given as the Cayley 6-vectors the keyframes hold
+ * (cMultiCamSys_::Set_M_t_from_min, src/cam_system_omni.cpp:170-183): mt1, mt2 [6],
+ * mc [ncams][6].  Out: E [ncams][ncams][9] row-major, the `E` input of the two entries above.
+ * Host math in the reference's cv::Matx operation order. */
+int mcs_compute_e_rig(const double* mt1, const double* mt2, const double* mc, int32_t ncams,
+                      double* E);
+
+/* CheckDistEpipolarLine(ray1, ray2, E12, thresh) (src/misc.cpp:54-70): 1 = passes (squared
+ * epipolar distance < thresh), 0 = fails (or den == 0), < 0 = argument error.  The check the
+ * triangulation entries apply to every candidate. */
+int mcs_check_dist_epipolar_line(const double* ray1, const double* ray2, const double* E12,
+                                 double thresh);
+
 /* ---- Projection-guided (windowed) matching -------------------------------------------
  * cMultiFrame feature grid (src/cMultiFrame.cpp:154-184, PosInGrid :342-353; 64 x 48 cells
  * per camera, include/cMultiFrame.h FRAME_GRID_COLS / FRAME_GRID_ROWS) and

@@ -665,8 +665,24 @@ __global__ __launch_bounds__(256) void k_restore(Dev d) {
 using namespace mcs;
 using namespace mcs::ba;
 
+namespace mcs {
+namespace ba {
+// host-side structure of one optimize() call (build_structure); owned by the context so its
+// capacity is reused across that context's calls and released with it
+struct HostStruct {
+  std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
+      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, fin_blk,
+      fin_slot0, fin_nch;
+  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
+  int n_slots = 0;
+  int np = 0, nl = 0;
+};
+}  // namespace ba
+}  // namespace mcs
+
 struct mcs_ba_ctx {
   int device = 0;
+  HostStruct hs;
   hipStream_t st = nullptr;
   // Device buffers are cached across calls: the driver requests them in the same order
   // every call, so request k reuses slot k when it is large enough (grow-only).
@@ -719,14 +735,6 @@ struct mcs_ba_ctx {
 
 namespace {
 
-struct HostStruct {
-  std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
-      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, fin_blk,
-      fin_slot0, fin_nch;
-  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
-  int n_slots = 0;
-  int np = 0, nl = 0;
-};
 
 // SparseOptimizer::initializeOptimization(0) + buildIndexMapping + BlockSolver::buildStructure
 // (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295): active edges (level 0), active
@@ -1009,8 +1017,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     cnt[p->n_poses + 1] = nae_l;
     if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
   }
-  thread_local HostStruct hs;   // capacity reused across calls (no fresh pages per call)
-  HostStruct& s = hs;
+  HostStruct& s = c->hs;
   build_structure(*p, edge_level, points_fixed, cnt, s);
   const int nl_glob = (int)cnt[p->n_poses], nae_glob = (int)cnt[p->n_poses + 1];
   if (rep) {
@@ -1158,6 +1165,7 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     };
     for (uint32_t k = 1;; k++) {
       if (arrived()) break;
+      __builtin_ia32_pause();   // spin politely: other ranks' threads may share this core
       if ((k & 1023) == 0) {
         const hipError_t q = hipStreamQuery(st);
         if (q == hipSuccess) {

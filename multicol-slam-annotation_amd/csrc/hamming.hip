@@ -520,6 +520,78 @@ static bool check_dist_epipolar_line(const double* r1, const double* r2, const d
   return (nom * nom) / den < thresh;
 }
 
+// ---- ComputeE per camera pair (src/misc.cpp:72-86) as SearchForTriangulationRaw builds its
+// Es table (src/cORBmatcher.cpp:985-998): Es[i][j] = ComputeE(KF1.Get_MtMc_inv(i),
+// KF2.Get_MtMc(j)), with MtMc = cayley2hom(M_t) * cayley2hom(M_c) and MtMc_inv =
+// cConverter::invMat(MtMc) (cMultiCamSys_::Set_M_t_from_min, src/cam_system_omni.cpp:170-183).
+// Every product accumulates s = 0; s += a(i,k) b(k,j) in k order (cv::Matx), `t12 /= norm`
+// multiplies by 1./norm (cv::Vec::operator/=), norm = sqrt of the in-order sum of squares.
+// Tiny 3x3 / 4x4 host math: nothing here is worth a device launch.
+static void host_matmul(const double* a, const double* b, double* c, int m, int l, int n) {
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < n; j++) {
+      double s = 0;
+      for (int k = 0; k < l; k++) s += a[i * l + k] * b[k * n + j];
+      c[i * n + j] = s;
+    }
+}
+
+static void host_cayley2hom(const double* p, double* T) {  // include/misc.h:134-162, 213-226
+  const double c1 = p[0], c2 = p[1], c3 = p[2];
+  const double c1s = c1 * c1, c2s = c2 * c2, c3s = c3 * c3;
+  const double scale = 1.0 + c1s + c2s + c3s;
+  const double R[9] = {1 + c1s - c2s - c3s, 2 * (c1 * c2 - c3), 2 * (c1 * c3 + c2),
+                       2 * (c1 * c2 + c3), 1 - c1s + c2s - c3s, 2 * (c2 * c3 - c1),
+                       2 * (c1 * c3 - c2), 2 * (c2 * c3 + c1), 1 - c1s - c2s + c3s};
+  const double inv = 1 / scale;  // R = (1 / scale) * R
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) T[4 * i + j] = R[3 * i + j] * inv;
+    T[4 * i + 3] = p[3 + i];
+  }
+  T[12] = T[13] = T[14] = 0.0;
+  T[15] = 1.0;
+}
+
+static void host_inv_mat(const double* M, double* O) {  // src/cConverter.cpp:31-44
+  double Rt[9], t[3];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) Rt[3 * i + j] = M[4 * j + i];
+  for (int i = 0; i < 3; i++) {  // t = -R * t
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (Rt[3 * i + k] * -1.0) * M[4 * k + 3];
+    t[i] = s;
+  }
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) O[4 * i + j] = Rt[3 * i + j];
+    O[4 * i + 3] = t[i];
+  }
+  O[12] = O[13] = O[14] = 0.0;
+  O[15] = 1.0;
+}
+
+static void host_compute_e(const double* T1, const double* T2, double* E) {  // misc.cpp:72-86
+  double R1w[9], R2wt[9], nR1w[9], R12[9], A[9], t12[3], t1w[3], t2w[3];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) {
+      R1w[3 * i + j] = T1[4 * i + j];
+      nR1w[3 * i + j] = T1[4 * i + j] * -1.0;
+      R2wt[3 * i + j] = T2[4 * j + i];
+    }
+    t1w[i] = T1[4 * i + 3];
+    t2w[i] = T2[4 * i + 3];
+  }
+  host_matmul(R1w, R2wt, R12, 3, 3, 3);   // R12 = R1w * R2w.t()
+  host_matmul(nR1w, R2wt, A, 3, 3, 3);    // t12 = -R1w * R2w.t() * t2w + t1w
+  host_matmul(A, t2w, t12, 3, 3, 1);
+  for (int i = 0; i < 3; i++) t12[i] = t12[i] + t1w[i];
+  double ss = 0;
+  for (int i = 0; i < 3; i++) ss += t12[i] * t12[i];
+  const double ialpha = 1. / std::sqrt(ss);  // t12 /= cv::norm(t12)
+  for (int i = 0; i < 3; i++) t12[i] = t12[i] * ialpha;
+  const double S[9] = {0.0, -t12[2], t12[1], t12[2], 0.0, -t12[0], -t12[1], t12[0], 0.0};  // Skew
+  host_matmul(S, R12, E, 3, 3, 3);        // t12x * R12
+}
+
 static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
                                     const int32_t* cam1, const uint8_t* has_mp1,
                                     const double* rays1, int32_t n1, const uint8_t* desc2,
@@ -667,6 +739,31 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
   return search_for_triangulation(desc1, mask1, cam1, has_mp1, rays1, n1, desc2, mask2, cam2,
                                   has_mp2, rays2, n2, ncams, E, bytes, th_low, epi_thresh,
                                   matches12, n_matches);
+}
+
+int mcs_compute_e_rig(const double* mt1, const double* mt2, const double* mc, int32_t ncams,
+                      double* E) {
+  if (!mt1 || !mt2 || !mc || !E || ncams <= 0) { set_error("compute_e_rig: bad arguments"); return MCS_ERR_ARG; }
+  double T1[16], T2[16], Mc[16], M[16], inv1[16];
+  host_cayley2hom(mt1, T1);
+  host_cayley2hom(mt2, T2);
+  for (int i = 0; i < ncams; i++) {
+    host_cayley2hom(mc + 6 * i, Mc);
+    host_matmul(T1, Mc, M, 4, 4, 4);
+    host_inv_mat(M, inv1);
+    for (int j = 0; j < ncams; j++) {
+      host_cayley2hom(mc + 6 * j, Mc);
+      host_matmul(T2, Mc, M, 4, 4, 4);
+      host_compute_e(inv1, M, E + 9 * ((size_t)i * ncams + j));
+    }
+  }
+  return MCS_OK;
+}
+
+int mcs_check_dist_epipolar_line(const double* ray1, const double* ray2, const double* E12,
+                                 double thresh) {
+  if (!ray1 || !ray2 || !E12) { set_error("check_dist_epipolar_line: null argument"); return MCS_ERR_ARG; }
+  return check_dist_epipolar_line(ray1, ray2, E12, thresh) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -15,6 +15,9 @@
 //                      the right-hand side b_i -= L_ik u_k.
 // backward (one workgroup): x_k = Linv_kk^T z_k, z_j -= L_kj^T x_k for j < k.
 #include "ldlt.hpp"
+#include <mutex>
+#include <set>
+#include <utility>
 
 namespace mcs {
 namespace ldlt {
@@ -503,15 +506,25 @@ __global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, co
 
 constexpr size_t kSolve1Lds = (2 * (size_t)TB * LS + 18 * TB) * sizeof(double);
 
+// hipFuncSetAttribute applies to the current device: set each kernel's dynamic-LDS limit once
+// per (kernel, device), under a lock (a process may drive several GPUs from several threads)
+hipError_t set_lds_limit(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
+}
+
 hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
                           hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_solve1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kSolve1Lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = set_lds_limit((const void*)k_solve1, (int)kSolve1Lds);
+  if (e != hipSuccess) return e;
   if (n < 1 || n > TB) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_solve1, dim3(1), dim3(256), kSolve1Lds, st, A, b, x, n, diag_value, flag);
   return hipGetLastError();
@@ -520,16 +533,9 @@ hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, do
 constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
 
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kPanelLds);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)k_backward, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            96 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = set_lds_limit((const void*)k_panel, (int)kPanelLds);
+  if (e == hipSuccess) e = set_lds_limit((const void*)k_backward, 96 * 1024);
+  if (e != hipSuccess) return e;
   if ((size_t)T * TB * sizeof(double) > 96 * 1024) return hipErrorInvalidValue;
   for (int k = 0; k < T; k++) {
     const int m = T - 1 - k;

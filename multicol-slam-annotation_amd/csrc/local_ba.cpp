@@ -15,8 +15,13 @@ extern "C" int mcs_local_ba_select(const mcs_lba_map* m, int32_t cur_kf, const i
   if (!m || !g || cur_kf < 0 || cur_kf >= m->n_kf || n_covis < 0 || (n_covis > 0 && !covis) ||
       !m->kf_id || !m->kf_bad || !m->kf_mp_off || !m->pt_bad || !m->pt_obs_off ||
       !g->local_kf || !g->fixed_kf || !g->pose_fixed || !g->points || !g->point_extra_obs ||
-      (g->edge_cap > 0 && (!g->edge_obs || !g->edge_pose || !g->edge_point))) {
+      (g->edge_cap > 0 && (!g->edge_obs || !g->edge_pose || !g->edge_point)) ||
+      (m->kf_mp_off[m->n_kf] > 0 && !m->kf_mp)) {
     set_error("mcs_local_ba_select: null argument");
+    return MCS_ERR_ARG;
+  }
+  if (m->n_points > 0 && m->pt_obs_off[m->n_points] > 0 && !m->obs_kf) {
+    set_error("mcs_local_ba_select: null argument (obs_kf)");
     return MCS_ERR_ARG;
   }
   const int nkf = m->n_kf, npt = m->n_points;
@@ -27,9 +32,16 @@ extern "C" int mcs_local_ba_select(const mcs_lba_map* m, int32_t cur_kf, const i
   // ---- local keyframes: pKF, then every covisible (marked even when bad, added when not)
   g->local_kf[g->n_local++] = cur_kf;
   local_mark[cur_kf] = 1;
+  // GetVectorCovisibleKeyFrames holds each neighbour once and never pKF itself; a list that
+  // does not would make pose slots and local_kf disagree, so it is rejected
   for (int i = 0; i < n_covis; i++) {
     const int k = covis[i];
     if (k < 0 || k >= nkf) { set_error("mcs_local_ba_select: covisible index out of range"); return MCS_ERR_ARG; }
+    if (local_mark[k]) {
+      set_error(k == cur_kf ? "mcs_local_ba_select: covisible list holds the current keyframe"
+                            : "mcs_local_ba_select: duplicate covisible keyframe");
+      return MCS_ERR_ARG;
+    }
     local_mark[k] = 1;
     if (!m->kf_bad[k] && g->n_local < nkf) g->local_kf[g->n_local++] = k;
   }

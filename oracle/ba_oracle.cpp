@@ -563,6 +563,56 @@ int optimize(Graph& g, const mcs_ba_options& o, volatile int32_t* stop_in, mcs_b
 
 extern "C" {
 
+// ComputeE (src/misc.cpp:72-86) for every camera pair as SearchForTriangulationRaw's Es table
+// (src/cORBmatcher.cpp:985-998): E[i][j] = ComputeE(invMat(M_t1 M_c[i]), M_t2 M_c[j]).
+int oracle_compute_e_rig(const double* mt1, const double* mt2, const double* mc, int ncams,
+                         double* E) {
+  auto matmul = [](const double* a, const double* b, double* c, int m, int l, int n) {
+    for (int i = 0; i < m; i++)
+      for (int j = 0; j < n; j++) {
+        double s = 0;
+        for (int k = 0; k < l; k++) s += a[i * l + k] * b[k * n + j];
+        c[i * n + j] = s;
+      }
+  };
+  double T1[16], T2[16], Mc[16], M1[16], M2[16], I1[16];
+  cay2hom(mt1, T1);
+  cay2hom(mt2, T2);
+  for (int i = 0; i < ncams; i++)
+    for (int j = 0; j < ncams; j++) {
+      cay2hom(mc + 6 * i, Mc);
+      mat44(T1, Mc, M1);
+      inv_mat(M1, I1);
+      cay2hom(mc + 6 * j, Mc);
+      mat44(T2, Mc, M2);
+      double R1w[9], R2w[9], R2wt[9], nR1w[9], R12[9], A[9], t12[3], t1w[3], t2w[3];
+      for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) {
+          R1w[3 * r + c] = I1[4 * r + c];
+          R2w[3 * r + c] = M2[4 * r + c];
+        }
+        t1w[r] = I1[4 * r + 3];
+        t2w[r] = M2[4 * r + 3];
+      }
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+          R2wt[3 * r + c] = R2w[3 * c + r];
+          nR1w[3 * r + c] = -R1w[3 * r + c];
+        }
+      matmul(R1w, R2wt, R12, 3, 3, 3);
+      matmul(nR1w, R2wt, A, 3, 3, 3);
+      matmul(A, t2w, t12, 3, 3, 1);
+      for (int r = 0; r < 3; r++) t12[r] += t1w[r];
+      double ss = 0;
+      for (int r = 0; r < 3; r++) ss += t12[r] * t12[r];
+      const double ia = 1. / std::sqrt(ss);
+      for (int r = 0; r < 3; r++) t12[r] *= ia;
+      const double S[9] = {0.0, -t12[2], t12[1], t12[2], 0.0, -t12[0], -t12[1], t12[0], 0.0};
+      matmul(S, R12, E + 9 * ((size_t)i * ncams + j), 3, 3, 3);
+    }
+  return 0;
+}
+
 int oracle_ba_edge(const double* pose, const double* X, const double* mc, const double* cam,
                    const double* meas, double* err, double* jp, double* jl) {
   edge_error(pose, X, mc, cam, meas, err);

@@ -83,6 +83,22 @@ static bool check_dist_epipolar_line(const double* r1, const double* r2, const d
   return dsqr < thresh;
 }
 
+int oracle_check_dist_epipolar_line(const double* r1, const double* r2, const double* E,
+                                    double thresh, double* dsqr) {
+  // as check_dist_epipolar_line, also reporting dsqr (NaN when den == 0)
+  double r2tE[3], nom, Ex1[3], Et[9], Etx2[3];
+  matx_mul(r2, E, r2tE, 1, 3, 3);
+  matx_mul(r2tE, r1, &nom, 1, 3, 1);
+  matx_mul(E, r1, Ex1, 3, 3, 1);
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) Et[3 * r + c] = E[3 * c + r];
+  matx_mul(Et, r2, Etx2, 3, 3, 1);
+  const double den = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Ex1[2] * Ex1[2] + Etx2[0] * Etx2[0] +
+                     Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
+  if (dsqr) *dsqr = den == 0.0 ? NAN : (nom * nom) / den;
+  return check_dist_epipolar_line(r1, r2, E, thresh) ? 1 : 0;
+}
+
 // masks1 / masks2 nullable: the cORBmatcher was built with havingMasks (mdBRIEF), which also
 // selects the thresholds TH_LOW = floor(featDim) instead of 2 * featDim (:52-65).
 int oracle_search_for_triangulation_raw_ex(const uint8_t* desc1, const uint8_t* masks1, int n1,

@@ -41,6 +41,8 @@ _SIGS = {
     "oracle_hamming_top2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P]),
     "oracle_search_for_triangulation_raw": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
     "oracle_search_for_triangulation_raw_ex": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
+    "oracle_check_dist_epipolar_line": (_I, [_P, _P, _P, _D, _P]),
+    "oracle_compute_e_rig": (_I, [_P, _P, _P, _I, _P]),
     "oracle_frame_grid": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "oracle_window_candidates": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I]),
     # DBoW2 vocabulary oracle
@@ -190,6 +192,23 @@ def hamming_top2(q, t):
     sd = np.zeros(n, np.int32)
     lib().oracle_hamming_top2(_p(q), n, _p(t), len(t), q.shape[1], _p(bi), _p(bd), _p(sd))
     return bi, bd, sd
+
+
+def check_dist_epipolar_line(ray1, ray2, E, thresh):
+    """-> (passes, dsqr) of CheckDistEpipolarLine (dsqr = nan when den == 0)."""
+    d = np.zeros(1)
+    ok = lib().oracle_check_dist_epipolar_line(_p(np.ascontiguousarray(ray1, np.float64)),
+                                              _p(np.ascontiguousarray(ray2, np.float64)),
+                                              _p(np.ascontiguousarray(E, np.float64)), thresh, _p(d))
+    return bool(ok), float(d[0])
+
+
+def compute_e_rig(mt1, mt2, mc):
+    mc = np.ascontiguousarray(mc, np.float64)
+    E = np.zeros((len(mc), len(mc), 3, 3))
+    lib().oracle_compute_e_rig(_p(np.ascontiguousarray(mt1, np.float64)),
+                               _p(np.ascontiguousarray(mt2, np.float64)), _p(mc), len(mc), _p(E))
+    return E
 
 
 def extract_ex(img, cam, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20,

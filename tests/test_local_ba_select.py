@@ -108,6 +108,18 @@ def test_select_capacity_error(built, bigmap):
     assert rc == -2 and g.n_edges > 10   # MCS_ERR_CAPACITY, count still reported
 
 
+def test_select_rejects_self_or_duplicate_covisibles(built, bigmap):
+    """GetVectorCovisibleKeyFrames never lists pKF itself or a keyframe twice; such a list is
+    an argument error (pose slots would disagree with local_kf), not a silent truncation."""
+    from mcs_amd import ba, McsError
+    cv = list(ba.covisibles(bigmap, 23))
+    assert len(cv) >= 2
+    for bad in ([23] + cv, cv + [cv[0]]):
+        with pytest.raises(McsError):
+            ba.local_ba_select(bigmap, 23, bad)
+    ba.local_ba_select(bigmap, 23, cv)   # the genuine list still works
+
+
 def test_oracle_bookkeeping_two_observation_points(built):
     """A 2-observation point losing one observation turns bad: its other edge is skipped by
     the culling and it is not written back (oracle restatement on a crafted problem)."""
