@@ -226,6 +226,21 @@ int mcs_ba_enable_timing(mcs_ba_ctx* c, int32_t on);
 int mcs_ba_read_timing(mcs_ba_ctx* c, double* ms, int32_t* n_iterations, int32_t* n_trials,
                        int32_t* last_n, int32_t reset);
 
+/* Host wall time of the host-side phases of the calls on this context (always accumulated):
+ * 0 argument checks + active counts, 1 structure build (initializeOptimization +
+ * buildStructure), 2 packing + upload of the problem, 3 waiting for the device + result
+ * download, 4 LocalBA bookkeeping between the rounds (culling, re-masking).  ms[] accumulates
+ * until read with reset. */
+#define MCS_BA_NHOST 5
+int mcs_ba_read_host_timing(mcs_ba_ctx* c, double* ms, int32_t* n_calls, int32_t reset);
+
+/* Test hook: the structure of `p` (edges with edge_level != 0 inactive; NULL = all active)
+ * built by the product (Schur pair lists and k_schur items on the device) against the host
+ * restatement of BlockSolver::buildStructure's pairs (block pointers, every (e1, e2) pair in
+ * order, every work item).  Returns the number of differing entries (0 = identical) or a
+ * negative status. */
+int mcs_ba_check_structure(mcs_ba_ctx* c, const mcs_ba_problem* p, const uint8_t* edge_level);
+
 /* Test hook for the dense reduced-camera solve (LinearSolverEigen::solve,
  * ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126): S is n x n row-major (lower
  * triangle read), b and x length n.  *zero_pivot = 1 when the LDL^T meets an exact zero. */

@@ -18,6 +18,7 @@
 #include "common.hpp"
 #include "../../include/mcs_ba.h"
 #include "ldlt.hpp"
+#include "ba_structure.hpp"
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -26,6 +27,8 @@
 #include <limits>
 #include <new>
 #include <vector>
+#include <string.h>
+#include <rocprim/rocprim.hpp>
 
 namespace mcs {
 namespace ba {
@@ -206,7 +209,28 @@ __device__ __forceinline__ void huber(double e, double delta, double dsqr, doubl
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
+// Device-side Levenberg-Marquardt control (Optimizer::run_device): the accept / reject
+// decision, the lambda schedule, Raul's nBad stop and the terminate action of g2o run in
+// k_lm_end after every trial, so the host enqueues trial after trial without reading anything
+// back.  Kernels of a step that is no longer needed (done) return at once; the linearisation
+// of a step runs only when the previous trial ended an iteration (lin).
+constexpr int kLmTraceCap = 64;
+struct LmCtl {
+  double lambda, currentChi, iniChi, lastChi, tau, gain_threshold;
+  double chi0, lambda_final;
+  int ni, qmax, nBad, it, iter;
+  int done, lin, restore, stop_out, ext_stop;
+  int max_iterations, max_trials, terminate_max_iter, pad_;
+  double trace[kLmTraceCap];
+};
+// host-coherent progress word of run_device (written by k_lm_end after every step)
+struct LmSig { uint64_t seq; int32_t done, iter; int32_t ext_stop, pad_; };
+
 struct Dev {
+  LmCtl* ctl;   // device-driven LM (null: host-driven, lambda by value below)
+  // device-driven trial sums: per-workgroup partials of the robust chi2 (k_edges), of the
+  // points' and the poses' model decrease (k_update); null = the per-element arrays only
+  double* part_chi; double* part_pt; double* part_ps;
   // problem
   const double* mc; const double* cam;
   const int32_t* e_pose; const int32_t* e_point; const int32_t* e_cam;
@@ -220,13 +244,15 @@ struct Dev {
   const int32_t* hpose_vtx; const int32_t* hpt_vtx;   // vertex id per hessian index
   int np, nl;
   const int32_t* pt_ptr; const int32_t* pt_edges;     // CSR active points -> active edges
+  const int32_t* pt_h;                                // pose Hessian index per pt_edges entry
   const int32_t* ps_ptr; const int32_t* ps_edges;     // CSR active poses  -> active edges
   const int32_t* blk_i; const int32_t* blk_j;         // lower pose blocks (i >= j)
   const int32_t* it_blk; const int32_t* it_chunk; const int32_t* it_slot;  // k_schur items
-  const int32_t* fin_blk; const int32_t* fin_slot0; const int32_t* fin_nch;  // k_schur_fin
+  const int32_t* blk_nch; const int32_t* blk_slot0;  // chunks / first partial slot per block
   double* schur_part;                                 // [slots][42]
   double lam, lam0;                                   // lambda; lambda on rank 0, 0 elsewhere
-  const int32_t* pr_ptr; const int32_t* pr_e1; const int32_t* pr_e2;  // edge pairs per block
+  const int32_t* pr_ptr; const uint2* pr;             // edge pairs (e1, e2) per block
+  const int32_t* nitem;                               // k_schur items (device-built count)
   int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
   double* err; double* w; double* jp; double* jl; double* hpl; double* y; double* chi; double* rchi;
@@ -241,9 +267,49 @@ struct Dev {
   int* flag;                                // solve failure flag
 };
 
+// deterministic sum over a 256-thread workgroup: xor butterfly per wave, then the 4 wave sums
+// in wave order (every thread calls; the result is valid in every thread)
+__device__ __forceinline__ double block_sum256(double v) {
+  __shared__ double sm[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();   // sm may still be read by a previous call
+  if (lane == 0) sm[w] = v;
+  __syncthreads();
+  return ((sm[0] + sm[1]) + sm[2]) + sm[3];
+}
+
+__device__ __forceinline__ double lam_of(const Dev& d) { return d.ctl ? d.ctl->lambda : d.lam; }
+__device__ __forceinline__ double lam0_of(const Dev& d) { return d.ctl ? d.ctl->lambda : d.lam0; }
+// a kernel of a device-driven step that is not needed (the loop has ended)
+__device__ __forceinline__ bool lm_done(const Dev& d) { return d.ctl && d.ctl->done; }
+
+constexpr int kRedNT = 256;   // k_build workgroup (1024 measured slower: 18.3 vs 12.9 us at config C)
+
 // per active edge: error (+ robust chi2) and optionally Jacobians / weight / Hpl = w Jp^T Jl
+// (device-driven linearisation: only when the previous trial ended an iteration)
 __global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
   const int k = blockIdx.x * 256 + threadIdx.x;
+  if (lm_done(d) || (linearize && d.ctl && !d.ctl->lin)) return;
+  if (!linearize && d.part_chi) {   // trial chi2 of a device-driven step: + workgroup partial
+    double r0 = 0.0;
+    if (k < d.nae) {
+      const int e = d.aedge ? d.aedge[k] : k;
+      const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
+      double er[2];
+      edge_error(d.poses + 6 * pi, d.points + 3 * li, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
+      const double c2 = d.e_info[e] * (er[0] * er[0] + er[1] * er[1]);
+      double r1;
+      huber(c2, d.delta, d.dsqr, &r0, &r1);
+      d.err[2 * e] = er[0]; d.err[2 * e + 1] = er[1];
+      d.chi[e] = c2;
+      d.rchi[k] = r0;
+    }
+    const double sum = block_sum256(r0);
+    if (threadIdx.x == 0) d.part_chi[blockIdx.x] = sum;
+    return;
+  }
   if (k >= d.nae) return;
   const int e = d.aedge ? d.aedge[k] : k;   // null: every edge
   const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
@@ -346,6 +412,143 @@ __global__ __launch_bounds__(1024) void k_reduce3(Sum3 q, const int* flag, Trial
   }
 }
 
+// ---- device-driven Levenberg-Marquardt control (one thread) ------------------------------
+// x^3 rounded once (double-double product), the value std::pow(x, 3) returns: host and device
+// (and every rank) take the identical lambda step
+__host__ __device__ inline double cube_rn(double x) {
+  const double p = x * x;
+  const double pe = __builtin_fma(x, x, -p);       // x^2 = p + pe exactly
+  const double h = p * x;
+  const double he = __builtin_fma(p, x, -h);       // p x = h + he exactly
+  return h + (he + pe * x);
+}
+
+// The end of a device-driven step in one launch (one workgroup): the trial's three sums
+// (robust chi2, points' and poses' model decrease; summed exactly as k_reduce3's three
+// workgroups do, or taken from sc when reduce_dev already formed them), the LM control
+// (lm_control) and the pop of a rejected trial by every thread.
+__device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig);
+__global__ __launch_bounds__(1024) void k_lm_end(Dev d, Sum3 q, int have_sums, double* sc,
+                                                 const int* flag, LmSig* sig, uint64_t seq) {
+  __shared__ double s[1024];
+  __shared__ int rej;
+  LmCtl* c = d.ctl;
+  const int t = threadIdx.x;
+  if (!c->done) {
+    if (have_sums != 1) {   // 0: the per-element arrays; 2: workgroup partials (q says which)
+      for (int b = 0; b < 3; b++) {
+        const double* v = q.v[b];
+        double acc = 0.0;
+        for (int i = t; i < q.n[b]; i += 1024) acc = acc + v[i];
+        s[t] = acc;
+        __syncthreads();
+        for (int o = 512; o > 0; o >>= 1) {
+          if (t < o) s[t] = s[t] + s[t + o];
+          __syncthreads();
+        }
+        if (t == 0) sc[b] = s[0];
+        __syncthreads();
+      }
+    }
+    if (t == 0) {
+      lm_control(c, sc, *flag, sig);
+      rej = c->restore;
+    }
+    __syncthreads();
+    if (rej) {   // pop: every pose and point back to the backups of the trial's push
+      for (int i = t; i < d.n_pose_dbl; i += 1024) d.poses[i] = d.push_poses[i];
+      for (int i = t; i < d.n_point_dbl; i += 1024) d.points[i] = d.push_points[i];
+    }
+  }
+  if (t == 0) {   // relaxed: a stale `done` only costs the host one more (no-op) step
+    __hip_atomic_store(&sig->done, c->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sig->iter, c->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sig->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// chi2 of the starting point -> currentChi (the optimize() call's activeRobustChi2)
+__global__ void k_lm_start(LmCtl* c, const double* sc) {
+  if (threadIdx.x != 0) return;
+  c->chi0 = sc[0];
+  c->currentChi = sc[0];
+  c->iniChi = sc[0];
+}
+// lambda of iteration 0: tau * max diagonal (computeLambdaInit,
+// optimization_algorithm_levenberg.cpp:166-180)
+__global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
+  if (threadIdx.x != 0 || c->done) return;
+  c->lambda = c->tau * fmax(sc[1], sc[2]);
+  c->ni = 2;
+  c->nBad = 0;
+}
+// after a trial (k_lm_end, one thread): OptimizationAlgorithmLevenberg::solve's accept / reject
+// (optimization_algorithm_levenberg.cpp:99-163) and, when the iteration ends, the terminate
+// action (sparse_optimizer_terminate_action.cpp:43-72) -- the arithmetic of the host driver
+// statement for statement.  sc = {robust chi2, points' model decrease, poses' model
+// decrease}; flag = the solve failed (zero pivot).
+__device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig) {
+  {
+    const int stop = __hip_atomic_load(&sig->ext_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    c->ext_stop = stop;
+    double tempChi = sc[0];
+    if (flag) tempChi = 1.7976931348623157e308;
+    double rho = c->currentChi - tempChi;
+    double scale = sc[2] + sc[1];
+    scale += 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+      double alpha = 1. - cube_rn(2 * rho - 1);
+      alpha = fmin(alpha, 2. / 3.);
+      c->lambda *= fmax(1. / 3., alpha);
+      c->ni = 2;
+      c->currentChi = tempChi;
+      c->restore = 0;
+    } else {
+      c->lambda *= c->ni;
+      c->ni *= 2;
+      c->restore = 1;   // k_lm_end pops the state right after this decision
+    }
+    c->qmax++;
+    if (rho < 0 && c->qmax < c->max_trials && !stop) {
+      c->lin = 0;       // the next step retries the trial with the larger lambda
+    } else {
+      int result = 0;
+      if (c->qmax == c->max_trials || rho == 0) result = 1;
+      else {
+        if ((c->iniChi - c->currentChi) * 1e3 < c->iniChi) c->nBad++;
+        else c->nBad = 0;
+        if (c->nBad >= 3) result = 1;
+      }
+      c->it++;
+      const int i = c->iter;
+      const double cur = c->currentChi;
+      if (i < kLmTraceCap) c->trace[i] = cur;
+      int stopOpt = 0;
+      if (i == 0) c->lastChi = cur;
+      else {
+        if (i < c->terminate_max_iter) {
+          const double gain = (c->lastChi - cur) / cur;
+          c->lastChi = cur;
+          if (gain >= 0 && gain < c->gain_threshold) stopOpt = 1;
+        } else {
+          stopOpt = 1;
+        }
+      }
+      if (stopOpt) c->stop_out = 1;
+      c->lambda_final = c->lambda;
+      c->iter = i + 1;
+      if (c->iter >= c->max_iterations || stop || stopOpt || result != 0) {
+        c->done = 1;
+      } else {
+        c->lin = 1;
+        c->qmax = 0;
+        c->iniChi = c->currentChi;
+      }
+    }
+  }
+}
+
 // launch helper: part = kRedPartMax doubles of scratch (stream-ordered reuse is safe)
 template <bool MAX>
 void reduce_dev(const double* v, int n, double* out, double* part, hipStream_t st) {
@@ -368,8 +571,8 @@ __device__ __forceinline__ double quad_sum(double v) {
   v += __shfl_xor(v, 2);
   return v;
 }
-__global__ __launch_bounds__(256) void k_points_build(Dev d) {
-  const int gt = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void points_build_body(const Dev& d, int block) {
+  const int gt = block * kRedNT + threadIdx.x;
   const int l = gt >> 2, sub = gt & 3;
   const bool act = l < d.nl;
   double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
@@ -395,9 +598,10 @@ __global__ __launch_bounds__(256) void k_points_build(Dev d) {
   d.red[l] = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
 }
 
-// Deterministic block sum of NV per-thread partials: fixed xor-butterfly inside each wave,
-// then the 4 wave sums in wave order.  On return sm[v * 4] holds sum v (after the barrier).
-template <int NV>
+// Deterministic block sum of NV per-thread partials over a workgroup of NW waves: fixed
+// xor-butterfly inside each wave, then the NW wave sums in wave order.  On return
+// sm[v * NW] holds sum v (after the barrier).
+template <int NV, int NW>
 __device__ __forceinline__ void block_sum_vec(double (&acc)[NV], double* sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -407,26 +611,29 @@ __device__ __forceinline__ void block_sum_vec(double (&acc)[NV], double* sm) {
   }
   if (lane == 0) {
 #pragma unroll
-    for (int v = 0; v < NV; v++) sm[v * 4 + w] = acc[v];
+    for (int v = 0; v < NV; v++) sm[v * NW + w] = acc[v];
   }
   __syncthreads();
   if (threadIdx.x < NV) {
     const int v = threadIdx.x;
-    sm[v * 4] = ((sm[v * 4] + sm[v * 4 + 1]) + sm[v * 4 + 2]) + sm[v * 4 + 3];
+    double t = sm[v * NW];
+#pragma unroll
+    for (int k = 1; k < NW; k++) t += sm[v * NW + k];
+    sm[v * NW] = t;
   }
   __syncthreads();
 }
 
-constexpr int kRedNT = 256;
 constexpr int kUpper6[21][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, {1, 1},
                                 {1, 2}, {1, 3}, {1, 4}, {1, 5}, {2, 2}, {2, 3}, {2, 4},
                                 {2, 5}, {3, 3}, {3, 4}, {3, 5}, {4, 4}, {4, 5}, {5, 5}};
 
-// per active pose: Hpp (6x6, upper 21 mirrored), b_p; edges of the pose split over 256
-// threads (fixed stride), block tree sum.  Also the diagonal and b_p into the exchange area.
-__global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
-  __shared__ double sm[27 * 4];
-  const int i = blockIdx.x, t = threadIdx.x;
+// per active pose: Hpp (6x6, upper 21 mirrored), b_p; edges of the pose split over the
+// workgroup's threads (fixed stride), block tree sum.  Also the diagonal and b_p into the
+// exchange area.
+__device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
+  __shared__ double sm[27 * (kRedNT / 64)];
+  const int t = threadIdx.x;
   double acc[27];
 #pragma unroll
   for (int v = 0; v < 27; v++) acc[v] = 0.0;
@@ -446,25 +653,33 @@ __global__ __launch_bounds__(kRedNT) void k_poses_build(Dev d) {
 #pragma unroll
     for (int a = 0; a < 6; a++) acc[21 + a] += j0[a] * we0 + j1[a] * we1;
   }
-  block_sum_vec<27>(acc, sm);
+  constexpr int NW = kRedNT / 64;
+  block_sum_vec<27, NW>(acc, sm);
   if (t < 21) {
     const int a = kUpper6[t][0], bb = kUpper6[t][1];
-    const double h = sm[t * 4];
+    const double h = sm[t * NW];
     d.Hpp[36 * i + 6 * a + bb] = h;
     d.Hpp[36 * i + 6 * bb + a] = h;
     if (a == bb) d.hdiag[6 * i + a] = h;
   } else if (t < 27) {
-    d.bp[6 * i + t - 21] = sm[t * 4];
-    d.bpf[6 * i + t - 21] = sm[t * 4];
+    d.bp[6 * i + t - 21] = sm[t * NW];
+    d.bpf[6 * i + t - 21] = sm[t * NW];
   }
+}
+// both builds in one launch: workgroups [0, np) per pose, the rest four lanes per point
+__global__ __launch_bounds__(kRedNT) void k_build(Dev d) {
+  if (lm_done(d) || (d.ctl && !d.ctl->lin)) return;
+  if ((int)blockIdx.x < d.np) poses_build_body(d, blockIdx.x);
+  else points_build_body(d, blockIdx.x - d.np);
 }
 
 // One thread per (point, edge) entry of the point CSR: D = Hll + lambda I -> Dinv (cofactors,
 // recomputed per entry: identical bits), Y_e = Hpl_e Dinv; the first entry of each point
 // also stores Dinv and db = Dinv b_l.
 __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
+  if (lm_done(d)) return;
   const int q = blockIdx.x * 256 + threadIdx.x;
-  const double lam = d.lam;
+  const double lam = lam_of(d);
   // the trial's push (backup of every pose and point) and the solve-flag reset ride along
   {
     const int stride = gridDim.x * 256;
@@ -522,10 +737,10 @@ __device__ __forceinline__ double readlane0_d(double v) {
 // lanes that can hold data (levels whose partners are all past the chunk add zeros and are
 // skipped) leaves the 42 sums in lane 0.  A block with one chunk (config E: ~90 pairs per
 // block) writes S / bschur directly; otherwise the chunk's sums go to a partial slot and
-// k_schur_fin adds the slots in chunk order (config C: 55 blocks of thousands of pairs, so a
+// the wave that completes the block's last chunk adds the slots in chunk order (config C: 55
+// blocks of thousands of pairs, so a
 // block per wave would leave the GPU idle).  Every order is fixed: bitwise reproducible.
 // lam0 = lambda on rank 0 and 0 elsewhere (the sharded sum then holds lambda once).
-constexpr int kSchurChunk = 128;   // pairs per wave (config C: 128 beat 32 / 64 / 256)
 
 __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double lam0, int lane,
                                             double v) {
@@ -541,11 +756,12 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
   }
 }
 
-__global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
-  const double lam0 = d.lam0;
+__global__ __launch_bounds__(256) void k_schur(Dev d) {
+  if (lm_done(d)) return;
+  const double lam0 = lam0_of(d);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int it = blockIdx.x * 4 + w;
-  if (it >= nitem) return;
+  if (it >= *d.nitem) return;
   const int blk = d.it_blk[it], c = d.it_chunk[it], slot = d.it_slot[it];
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
   const int q0 = min(d.pr_ptr[blk] + c * kSchurChunk, d.pr_ptr[blk + 1]);
@@ -554,8 +770,9 @@ __global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
 #pragma unroll
   for (int v = 0; v < 42; v++) acc[v] = 0.0;
   for (int q = q0 + lane; q < q1; q += 64) {
-    const double* Y = d.y + 18 * d.pr_e1[q];
-    const double* B = d.hpl + 18 * d.pr_e2[q];
+    const uint2 pq = d.pr[q];
+    const double* Y = d.y + 18 * pq.x;
+    const double* B = d.hpl + 18 * pq.y;
     double y[18], bb[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) { y[k] = Y[k]; bb[k] = B[k]; }
@@ -597,26 +814,35 @@ __global__ __launch_bounds__(256) void k_schur(Dev d, int nitem) {
   else if (lane < 42) d.schur_part[(size_t)slot * 42 + lane] = mine;
 }
 
-// blocks split into several chunks: sum the chunk slots in chunk order, then write
-__global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nfin) {
-  const double lam0 = d.lam0;
+// blocks split into several chunks: sum the chunk slots in chunk order, then write (one wave
+// per block; blocks of one chunk were written by k_schur).  Measured against finishing in
+// k_schur by the wave whose chunk arrives last (agent release / atomic / acquire): equal at
+// config C, 2.6x slower k_schur at config E, whose 199 diagonal blocks split 16 ways.
+__global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nblk) {
+  if (lm_done(d)) return;
+  const double lam0 = lam0_of(d);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + w;
-  if (f >= nfin) return;
-  const int blk = d.fin_blk[f], s0 = d.fin_slot0[f], n = d.fin_nch[f];
+  const int b = blockIdx.x * 4 + w;
+  if (b >= nblk) return;
+  const int n = d.blk_nch[b];
+  if (n <= 1) return;
+  const int s0 = d.blk_slot0[b];
   double v = 0.0;
   if (lane < 42)
     for (int c = 0; c < n; c++) v += d.schur_part[(size_t)(s0 + c) * 42 + lane];
-  schur_write(d, d.blk_i[blk], d.blk_j[blk], lam0, lane, v);
+  schur_write(d, d.blk_i[b], d.blk_j[b], lam0, lane, v);
 }
+
 
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p); point = backup + x_l; model-decrease terms:
 // red[k] (points, k < nl) and red[nl + i] (poses) summed separately (poses are replicated
 // across shards, points are not).
 __global__ __launch_bounds__(256) void k_update(Dev d) {
+  if (lm_done(d)) return;
   const int gt = blockIdx.x * 256 + threadIdx.x;
-  const double lam = d.lam;
-  if (gt < 4 * d.nl) {   // points: four lanes per point, as k_points_build
+  const double lam = lam_of(d);
+  double spt = 0.0, sps = 0.0;   // this thread's point / pose model-decrease term
+  if (gt < 4 * d.nl) {   // points: four lanes per point, as the point build
     const int k = gt >> 2, sub = gt & 3;
     double c[3] = {0.0, 0.0, 0.0};
     for (int q = d.pt_ptr[k] + sub; q < d.pt_ptr[k + 1]; q += 4) {
@@ -629,16 +855,18 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
     }
 #pragma unroll
     for (int b = 0; b < 3; b++) c[b] = d.bl[3 * k + b] + quad_sum(c[b]);
-    if (sub != 0) return;
-    const double* Di = d.Dinv + 9 * k;
-    double s = 0;
-    const int v = d.hpt_vtx[k];
-    for (int a = 0; a < 3; a++) {
-      const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
-      d.points[3 * v + a] = d.points_bk[3 * v + a] + xa;
-      s += xa * (lam * xa + d.bl[3 * k + a]);
+    if (sub == 0) {
+      const double* Di = d.Dinv + 9 * k;
+      double s = 0;
+      const int v = d.hpt_vtx[k];
+      for (int a = 0; a < 3; a++) {
+        const double xa = Di[3 * a] * c[0] + Di[3 * a + 1] * c[1] + Di[3 * a + 2] * c[2];
+        d.points[3 * v + a] = d.points_bk[3 * v + a] + xa;
+        s += xa * (lam * xa + d.bl[3 * k + a]);
+      }
+      d.red[k] = s;
+      spt = s;
     }
-    d.red[k] = s;
   } else if (gt < 4 * d.nl + d.np) {
     const int i = gt - 4 * d.nl;
     const int v = d.hpose_vtx[i];
@@ -649,7 +877,176 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
       s += xa * (lam * xa + d.bpf[6 * i + a]);
     }
     d.red[d.nl + i] = s;
+    sps = s;
   }
+  if (d.part_pt) {   // device-driven step: workgroup partials of both sums
+    const double a = block_sum256(spt);
+    const double b = block_sum256(sps);
+    if (threadIdx.x == 0) { d.part_pt[blockIdx.x] = a; d.part_ps[blockIdx.x] = b; }
+  }
+}
+
+// ---- device build of the Schur pair lists and the k_schur work items ---------------------
+// BlockSolver::buildStructure's per-point product of pose groups (block_solver.hpp:143-295),
+// in the order build_pairs_host (ba_structure.hpp) produces on the host: per point, groups of
+// its edges by active pose in increasing pose order, for every group pair (P1 >= P2) the
+// edges of P1 x the edges of P2 in edge order; points in order; then a stable radix sort by
+// block id (rocPRIM) makes the lists block-major with that order kept inside every block.
+
+// A point's active-pose edges as (pose, edge) sorted by pose, stable (edge order inside a
+// pose), in a private array; more than kPairK of them take the slow path below.
+constexpr int kPairK = 48;
+__device__ __forceinline__ int point_groups(const Dev& d, int l, int* hs, int* es) {
+  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
+  int k = 0;
+  for (int q = q0; q < q1; q++) {
+    const int h = d.pt_h[q];
+    if (h < 0) continue;
+    if (k == kPairK) return -1;
+    int i = k++;
+    while (i > 0 && hs[i - 1] > h) { hs[i] = hs[i - 1]; es[i] = es[i - 1]; i--; }
+    hs[i] = h;
+    es[i] = d.pt_edges[q];
+  }
+  return k;
+}
+
+// pairs a point contributes: #{(a, b) : h(a) >= h(b) >= 0} over its active edges
+__global__ __launch_bounds__(256) void k_pair_count(Dev d, int32_t* cnt) {
+  const int l = blockIdx.x * 256 + threadIdx.x;
+  if (l > d.nl) return;
+  if (l == d.nl) { cnt[l] = 0; return; }   // the scan's total slot
+  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
+  int n = 0;
+  for (int a = q0; a < q1; a++) {
+    const int ha = d.pt_h[a];
+    if (ha < 0) continue;
+    for (int b = q0; b < q1; b++) {
+      const int hb = d.pt_h[b];
+      n += (hb >= 0 && hb <= ha) ? 1 : 0;
+    }
+  }
+  cnt[l] = n;
+}
+
+__global__ __launch_bounds__(256) void k_pair_emit(Dev d, const int32_t* off, uint32_t* keys,
+                                                   uint2* vals, int64_t pmax, uint32_t pad_key) {
+  const int64_t gt = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // padding past the last pair: a key above every block, sorted to the end
+  const int64_t total = off[d.nl];
+  for (int64_t q = total + gt; q < pmax; q += (int64_t)gridDim.x * 256) {
+    keys[q] = pad_key;
+    vals[q] = make_uint2(0u, 0u);
+  }
+  const int l = (int)gt;
+  if (l >= d.nl) return;
+  int64_t o = off[l];
+  int hs[kPairK], es[kPairK];
+  const int k = point_groups(d, l, hs, es);
+  if (k >= 0) {
+    for (int i0 = 0; i0 < k;) {          // group gi = [i0, i1) of pose P1
+      int i1 = i0 + 1;
+      while (i1 < k && hs[i1] == hs[i0]) i1++;
+      const int P1 = hs[i0];
+      for (int j0 = 0; j0 <= i0;) {      // group gj = [j0, j1) of pose P2 <= P1
+        int j1 = j0 + 1;
+        while (j1 < k && hs[j1] == hs[j0]) j1++;
+        const uint32_t blk = (uint32_t)((int64_t)P1 * (P1 + 1) / 2 + hs[j0]);
+        for (int a = i0; a < i1; a++)
+          for (int b = j0; b < j1; b++) {
+            keys[o] = blk;
+            vals[o] = make_uint2((uint32_t)es[a], (uint32_t)es[b]);
+            o++;
+          }
+        j0 = j1;
+      }
+      i0 = i1;
+    }
+    return;
+  }
+  // more than kPairK active edges: the same order from repeated minimum searches
+  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
+  int p1 = -1;
+  for (;;) {   // distinct active poses of the point, ascending
+    int P1 = 0x7FFFFFFF;
+    for (int a = q0; a < q1; a++) { const int h = d.pt_h[a]; if (h > p1 && h < P1) P1 = h; }
+    if (P1 == 0x7FFFFFFF) break;
+    int p2 = -1;
+    for (;;) {
+      int P2 = 0x7FFFFFFF;
+      for (int b = q0; b < q1; b++) { const int h = d.pt_h[b]; if (h > p2 && h <= P1 && h < P2) P2 = h; }
+      if (P2 == 0x7FFFFFFF) break;
+      const uint32_t blk = (uint32_t)((int64_t)P1 * (P1 + 1) / 2 + P2);
+      for (int a = q0; a < q1; a++) {
+        if (d.pt_h[a] != P1) continue;
+        const uint32_t ea = (uint32_t)d.pt_edges[a];
+        for (int b = q0; b < q1; b++) {
+          if (d.pt_h[b] != P2) continue;
+          keys[o] = blk;
+          vals[o] = make_uint2(ea, (uint32_t)d.pt_edges[b]);
+          o++;
+        }
+      }
+      p2 = P2;
+    }
+    p1 = P1;
+  }
+}
+
+// pr_ptr[b] = first sorted pair of block >= b (b = 0..nblk; the padding keys are nblk), and
+// the block's chunk count (pairs, or on a diagonal block its pose's edges, per kSchurChunk)
+__global__ __launch_bounds__(256) void k_block_ptr(Dev d, const uint32_t* keys, int64_t pmax,
+                                                   int nblk, int32_t* pr_ptr, int32_t* nch,
+                                                   int32_t* nslot) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b > nblk) return;
+  auto lb = [&](uint32_t k) {
+    int64_t lo = 0, hi = pmax;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (keys[m] < k) lo = m + 1; else hi = m;
+    }
+    return lo;
+  };
+  const int64_t p0 = lb((uint32_t)b);
+  pr_ptr[b] = (int32_t)p0;
+  if (b == nblk) { nch[b] = 0; nslot[b] = 0; return; }
+  const int np_ = (int)(lb((uint32_t)b + 1) - p0);
+  const int bi = d.blk_i[b], bj = d.blk_j[b];
+  const int ne = (bi == bj) ? d.ps_ptr[bi + 1] - d.ps_ptr[bi] : 0;
+  const int n = max(1, (max(np_, ne) + kSchurChunk - 1) / kSchurChunk);
+  nch[b] = n;
+  nslot[b] = n > 1 ? n : 0;
+}
+
+__global__ __launch_bounds__(256) void k_block_items(int nblk, const int32_t* nch,
+                                                     const int32_t* it_off, const int32_t* slot_off,
+                                                     int32_t* it_blk, int32_t* it_chunk,
+                                                     int32_t* it_slot, int32_t* it_nch,
+                                                     int32_t* nitem) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b == nblk) *nitem = it_off[nblk];
+  if (b >= nblk) return;
+  const int n = nch[b], i0 = it_off[b];
+  for (int c = 0; c < n; c++) {
+    it_blk[i0 + c] = b;
+    it_chunk[i0 + c] = c;
+    it_slot[i0 + c] = n > 1 ? slot_off[b] + c : -1;
+    it_nch[i0 + c] = n;
+  }
+}
+
+// edges that left the active set (LocalBA culling, Optimizer::remask): zero every per-edge term
+// a build kernel reads, so their contributions to Hll / b_l / Hpp / b_p / Schur are exact zeros
+__global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges, int n) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const int e = edges[k];
+  d.w[e] = 0.0;
+  d.err[2 * e] = 0.0; d.err[2 * e + 1] = 0.0;
+  for (int i = 0; i < 12; i++) d.jp[12 * e + i] = 0.0;
+  for (int i = 0; i < 6; i++) d.jl[6 * e + i] = 0.0;
+  for (int i = 0; i < 18; i++) { d.hpl[18 * e + i] = 0.0; d.y[18 * e + i] = 0.0; }
 }
 
 // the trial's pop (restore every pose and point from the backups) in one launch
@@ -665,20 +1062,6 @@ __global__ __launch_bounds__(256) void k_restore(Dev d) {
 using namespace mcs;
 using namespace mcs::ba;
 
-namespace mcs {
-namespace ba {
-// host-side structure of one optimize() call (build_structure); owned by the context so its
-// capacity is reused across that context's calls and released with it
-struct HostStruct {
-  std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
-      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, fin_blk,
-      fin_slot0, fin_nch;
-  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
-  int n_slots = 0;
-  int np = 0, nl = 0;
-};
-}  // namespace ba
-}  // namespace mcs
 
 struct mcs_ba_ctx {
   int device = 0;
@@ -693,6 +1076,9 @@ struct mcs_ba_ctx {
   int32_t* pinned_i = nullptr;
   TrialSig* sig = nullptr;    // host-coherent trial outcome (k_reduce3)
   uint64_t sig_seq = 0;
+  LmSig* lsig = nullptr;      // host-coherent progress of the device-driven LM (k_lm_end)
+  uint64_t lsig_seq = 0;
+  void* pinned_ctl = nullptr; // host-pinned readback of the final LmCtl
   // host-pinned staging of a call's packed problem upload (grow-only)
   uint8_t* stage = nullptr;
   size_t stage_cap = 0;
@@ -711,6 +1097,8 @@ struct mcs_ba_ctx {
   bool timing = false;
   hipEvent_t ev[8] = {};
   double acc_ms[MCS_BA_NSTAGES] = {};
+  double host_ms[MCS_BA_NHOST] = {};   // host phases (mcs_ba_read_host_timing)
+  int32_t host_calls = 0;
   int32_t n_iter = 0, n_trial = 0, last_n = 0;
   void* alloc(size_t bytes) {
     bytes += 64;
@@ -735,134 +1123,6 @@ struct mcs_ba_ctx {
 
 namespace {
 
-
-// SparseOptimizer::initializeOptimization(0) + buildIndexMapping + BlockSolver::buildStructure
-// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295): active edges (level 0), active
-// non-fixed poses in vertex order (pose_cnt: number of active edges per pose over ALL shards),
-// active points in vertex order, CSR lists and the per-block edge pairs of the Schur
-// complement, all by counting sorts in edge order (deterministic).
-void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
-                     const std::vector<double>& pose_cnt, HostStruct& s) {
-  s.aedge.clear();
-  s.aedge.reserve(p.n_edges);
-  for (int e = 0; e < p.n_edges; e++)   // level 0 and not allVerticesFixed (:206-267)
-    if ((!level || level[e] == 0) && !(points_fixed && p.pose_fixed[p.edge_pose[e]])) s.aedge.push_back(e);
-  std::vector<char> lh(p.n_points, 0);
-  if (!points_fixed)
-    for (int e : s.aedge) lh[p.edge_point[e]] = 1;
-  s.pose_h.assign(p.n_poses, -1);
-  s.point_h.assign(p.n_points, -1);
-  s.hpose_vtx.clear(); s.hpt_vtx.clear();
-  s.np = s.nl = 0;
-  for (int i = 0; i < p.n_poses; i++)
-    if (pose_cnt[i] > 0 && !p.pose_fixed[i]) { s.pose_h[i] = s.np++; s.hpose_vtx.push_back(i); }
-  for (int i = 0; i < p.n_points; i++)
-    if (lh[i]) { s.point_h[i] = s.nl++; s.hpt_vtx.push_back(i); }
-  // CSR point -> edges, pose -> edges (counting sort, stable in edge order)
-  s.pt_ptr.assign(s.nl + 1, 0);
-  s.ps_ptr.assign(s.np + 1, 0);
-  for (int e : s.aedge) {
-    const int l = s.point_h[p.edge_point[e]];
-    if (l >= 0) s.pt_ptr[l + 1]++;
-    const int h = s.pose_h[p.edge_pose[e]];
-    if (h >= 0) s.ps_ptr[h + 1]++;
-  }
-  for (int l = 0; l < s.nl; l++) s.pt_ptr[l + 1] += s.pt_ptr[l];
-  for (int h = 0; h < s.np; h++) s.ps_ptr[h + 1] += s.ps_ptr[h];
-  s.pt_edges.assign(s.pt_ptr[s.nl], 0);
-  s.ps_edges.assign(s.ps_ptr[s.np], 0);
-  {
-    std::vector<int32_t> fp(s.pt_ptr.begin(), s.pt_ptr.end() - 1), fs(s.ps_ptr.begin(), s.ps_ptr.end() - 1);
-    for (int e : s.aedge) {
-      const int l = s.point_h[p.edge_point[e]];
-      if (l >= 0) s.pt_edges[fp[l]++] = e;
-      const int h = s.pose_h[p.edge_pose[e]];
-      if (h >= 0) s.ps_edges[fs[h]++] = e;
-    }
-  }
-  // lower pose blocks (i >= j), block id i(i+1)/2 + j, and their edge pairs in
-  // (point, e1, e2) order
-  const size_t nblk = (size_t)s.np * (s.np + 1) / 2;
-  s.blk_i.resize(nblk); s.blk_j.resize(nblk);
-  for (int i = 0, b = 0; i < s.np; i++)
-    for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
-  s.pr_ptr.assign(nblk + 1, 0);
-  // Per point, its edges with an active pose, grouped by pose (stable, so edge order inside
-  // a group): the pairs of block (i1, i2), i2 <= i1, that a point contributes are then the
-  // product group(i1) x group(i2) in (e1, e2) order -- the order of the plain double loop over
-  // the point's edges, without visiting the pairs that fall above the diagonal.
-  std::vector<int32_t>& ge = s.tmp_e;   // grouped edges, point by point
-  std::vector<int32_t>& gr = s.tmp_g;   // groups: (pose, begin, end) triples
-  std::vector<int32_t>& gp = s.tmp_p;   // per point: first group (nl + 1 entries)
-  ge.clear(); gr.clear(); gp.assign(s.nl + 1, 0);
-  for (int l = 0; l < s.nl; l++) {
-    const size_t b0 = ge.size();
-    for (int a = s.pt_ptr[l]; a < s.pt_ptr[l + 1]; a++) {
-      const int e = s.pt_edges[a];
-      const int h = s.pose_h[p.edge_pose[e]];
-      if (h < 0) continue;
-      // insertion into (pose, edge order), stable
-      ge.push_back(e);
-      size_t q = ge.size() - 1;
-      while (q > b0 && s.pose_h[p.edge_pose[ge[q - 1]]] > h) { ge[q] = ge[q - 1]; q--; }
-      ge[q] = e;
-    }
-    for (size_t q = b0; q < ge.size();) {
-      const int h = s.pose_h[p.edge_pose[ge[q]]];
-      size_t r = q + 1;
-      while (r < ge.size() && s.pose_h[p.edge_pose[ge[r]]] == h) r++;
-      gr.push_back(h); gr.push_back((int32_t)q); gr.push_back((int32_t)r);
-      q = r;
-    }
-    gp[l + 1] = (int32_t)(gr.size() / 3);
-  }
-  auto for_blocks = [&](auto&& f) {   // f(block, group of i1, group of i2), point by point
-    for (int l = 0; l < s.nl; l++)
-      for (int gi = gp[l]; gi < gp[l + 1]; gi++) {
-        const int h1 = gr[3 * gi];
-        for (int gj = gp[l]; gj <= gi; gj++)
-          f((size_t)h1 * (h1 + 1) / 2 + gr[3 * gj], gi, gj);
-      }
-  };
-  for_blocks([&](size_t blk, int gi, int gj) {
-    s.pr_ptr[blk + 1] += (gr[3 * gi + 2] - gr[3 * gi + 1]) * (gr[3 * gj + 2] - gr[3 * gj + 1]);
-  });
-  for (size_t b = 0; b < nblk; b++) s.pr_ptr[b + 1] += s.pr_ptr[b];
-  s.pr_e1.assign(s.pr_ptr[nblk], 0);
-  s.pr_e2.assign(s.pr_ptr[nblk], 0);
-  std::vector<int32_t>& fill = s.tmp_f;
-  fill.assign(s.pr_ptr.begin(), s.pr_ptr.end() - 1);
-  for_blocks([&](size_t blk, int gi, int gj) {
-    int q = fill[blk];
-    for (int a = gr[3 * gi + 1]; a < gr[3 * gi + 2]; a++)
-      for (int b = gr[3 * gj + 1]; b < gr[3 * gj + 2]; b++, q++) {
-        s.pr_e1[q] = ge[a];
-        s.pr_e2[q] = ge[b];
-      }
-    fill[blk] = q;
-  });
-  // k_schur work items: chunks of kSchurChunk pairs (and, on diagonal blocks, pose edges)
-  s.it_blk.clear(); s.it_chunk.clear(); s.it_slot.clear();
-  s.fin_blk.clear(); s.fin_slot0.clear(); s.fin_nch.clear();
-  s.n_slots = 0;
-  for (size_t b = 0; b < nblk; b++) {
-    const int np_ = s.pr_ptr[b + 1] - s.pr_ptr[b];
-    int ne = 0;
-    if (s.blk_i[b] == s.blk_j[b]) ne = s.ps_ptr[s.blk_i[b] + 1] - s.ps_ptr[s.blk_i[b]];
-    const int nch = std::max(1, (std::max(np_, ne) + kSchurChunk - 1) / kSchurChunk);
-    if (nch > 1) {
-      s.fin_blk.push_back((int32_t)b);
-      s.fin_slot0.push_back(s.n_slots);
-      s.fin_nch.push_back(nch);
-    }
-    for (int c = 0; c < nch; c++) {
-      s.it_blk.push_back((int32_t)b);
-      s.it_chunk.push_back(c);
-      s.it_slot.push_back(nch > 1 ? s.n_slots + c : -1);
-    }
-    if (nch > 1) s.n_slots += nch;
-  }
-}
 
 template <typename T>
 T* up(mcs_ba_ctx* c, const std::vector<T>& v, hipError_t& e) {
@@ -941,42 +1201,54 @@ struct Shard {
   void* user = nullptr;
 };
 
-int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
-                  double* points, const uint8_t* edge_level, double* edge_chi2,
-                  volatile int32_t* stop_flag, mcs_ba_report* rep, const mcs_ba_shard* shard_in,
-                  bool points_fixed) {
-  if (!c || !p || !o || !poses || !points) return MCS_ERR_ARG;
-  if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
-  for (int e = 0; e < p->n_edges; e++) {
-    if (p->edge_pose[e] < 0 || p->edge_pose[e] >= p->n_poses || p->edge_point[e] < 0 ||
-        p->edge_point[e] >= p->n_points || p->edge_cam[e] < 0 || p->edge_cam[e] >= p->n_cams) {
-      set_error("edge vertex index out of range");
-      return MCS_ERR_ARG;
-    }
+// One optimize() call split in two so that LocalBA's second round can reuse the first
+// round's device state: setup() = initializeOptimization + buildStructure + the problem
+// upload; remask() = the same graph with more edges at level 1 (the culled ones: their
+// per-edge terms are zeroed once and the active-edge list shrinks, nothing else moves);
+// run() = SparseOptimizer::optimize (LM iterations) + the result download.
+// host phase clock: add the time since the previous mark to c->host_ms[k]
+struct HostClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(double* acc, int k) {
+    const auto n = std::chrono::steady_clock::now();
+    acc[k] += std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
   }
-  MCS_HIP_CHECK(hipSetDevice(c->device));
+};
+
+struct Optimizer {
+  mcs_ba_ctx* c;
+  const mcs_ba_problem* p;
+  bool points_fixed;
   Shard sh;
-  if (shard_in && shard_in->world > 1) {
-    if (!shard_in->xchg || !shard_in->allreduce || shard_in->rank < 0 || shard_in->rank >= shard_in->world ||
-        shard_in->xchg_cap < xchg_doubles(p->n_poses)) {
-      set_error("invalid mcs_ba_shard (exchange buffer too small or no allreduce callback)");
-      return MCS_ERR_ARG;
-    }
-    sh.rank = shard_in->rank; sh.world = shard_in->world; sh.xchg = shard_in->xchg;
-    sh.fn = shard_in->allreduce; sh.user = shard_in->user;
-  }
-  const bool sharded = sh.world > 1;
-  hipStream_t st = c->st;
-  auto rec = [&](int k) { if (c->timing) (void)hipEventRecord(c->ev[k], st); };
-  auto ms = [&](int a, int b) { float f = 0.f; (void)hipEventElapsedTime(&f, c->ev[a], c->ev[b]); return (double)f; };
-  c->free_all();
+  bool sharded = false;
+  hipStream_t st = nullptr;
+  HostStruct& s;
+  Dev d;
+  int n = 0, T = 1, NE = 0;
+  int64_t pmax = 0;      // upper bound of the Schur pairs (device-built lists)
+  int items_max = 1;     // upper bound of the k_schur work items
+  int32_t* it_nch_dev = nullptr;   // chunks of each item's block (checked by the test hook)
+  int nblk = 0;
+  XLayout X{1, 0};
+  int nl_glob = 0, nae_glob = 0;
+  double *d_poses = nullptr, *d_points = nullptr, *d_scalar = nullptr, *d_part = nullptr;
+  int* d_flag = nullptr;
+  ldlt::Work lw;
+  unsigned g_state = 1;
+  bool sig_path = false;
   hipError_t he = hipSuccess;
-  if (!sharded) {
-    sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
-    if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+
+  Optimizer(mcs_ba_ctx* c_, const mcs_ba_problem* p_, bool pf) : c(c_), p(p_), points_fixed(pf), s(c_->hs) {
+    std::memset(&d, 0, sizeof(d));
+  }
+  double* dz(size_t cnt_) {
+    double* q = (double*)c->alloc(std::max<size_t>(1, cnt_) * 8);
+    if (!q) he = hipErrorOutOfMemory;
+    return q;
   }
   // collective over xchg[off, off+cnt) (stream drained first); no-op on one rank
-  auto allreduce = [&](int op, size_t off, size_t cnt) -> int {
+  int allreduce(int op, size_t off, size_t cnt) {
     if (!sharded || cnt == 0) return MCS_OK;
     MCS_HIP_CHECK(hipStreamSynchronize(st));
     const auto t0 = std::chrono::steady_clock::now();
@@ -987,9 +1259,9 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     if (c->timing)
       c->acc_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MCS_OK;
-  };
+  }
   // all-reduce host scalars through the tail of the exchange buffer
-  auto allreduce_host = [&](double* v, int cnt, int op, size_t off) -> int {
+  int allreduce_host(double* v, int cnt, int op, size_t off) {
     if (!sharded) return MCS_OK;
     MCS_HIP_CHECK(hipMemcpyAsync(sh.xchg + off, v, 8 * (size_t)cnt, hipMemcpyHostToDevice, st));
     int rc = allreduce(op, off, cnt);
@@ -997,320 +1269,616 @@ int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* 
     MCS_HIP_CHECK(hipMemcpyAsync(v, sh.xchg + off, 8 * (size_t)cnt, hipMemcpyDeviceToHost, st));
     MCS_HIP_CHECK(hipStreamSynchronize(st));
     return MCS_OK;
-  };
+  }
 
-  // ---- structure: global pose activity (+ active point / edge counts)
-  int rc;
-  std::vector<double> cnt((size_t)p->n_poses + 2, 0.0);
-  {
-    int nae_l = 0;
-    std::vector<char> pt_seen(points_fixed ? 0 : p->n_points, 0);
-    int nl_l = 0;
+  int setup(const double* poses, const double* points, const uint8_t* edge_level,
+            const mcs_ba_shard* shard_in) {
+    if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
+    HostClock hc;
+    c->host_calls++;
     for (int e = 0; e < p->n_edges; e++) {
-      if (edge_level && edge_level[e]) continue;
-      if (points_fixed && p->pose_fixed[p->edge_pose[e]]) continue;   // all vertices fixed
-      cnt[p->edge_pose[e]] += 1.0;
-      nae_l++;
-      if (!points_fixed && !pt_seen[p->edge_point[e]]) { pt_seen[p->edge_point[e]] = 1; nl_l++; }
-    }
-    cnt[p->n_poses] = nl_l;
-    cnt[p->n_poses + 1] = nae_l;
-    if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
-  }
-  HostStruct& s = c->hs;
-  build_structure(*p, edge_level, points_fixed, cnt, s);
-  const int nl_glob = (int)cnt[p->n_poses], nae_glob = (int)cnt[p->n_poses + 1];
-  if (rep) {
-    rep->n_active_edges = nae_glob;
-    rep->n_active_poses = s.np;
-    rep->n_active_points = nl_glob;
-    rep->iterations = 0;
-  }
-  const int n = 6 * s.np;
-  const int T = ldlt::tiles_for(std::max(1, n));
-  if ((size_t)T * ldlt::TB * 8 > 96 * 1024) {
-    set_error("more than 2048 active poses: exceeds the backward-solve LDS budget");
-    return MCS_ERR_UNSUPPORTED;
-  }
-  const XLayout X(T, s.np);
-  Dev d;
-  std::memset(&d, 0, sizeof(d));
-  const int NE = p->n_edges;
-  double *d_poses = nullptr, *d_points = nullptr, *d_poses_bk = nullptr, *d_points_bk = nullptr;
-  {
-    Packer pk;
-    pk.add(&d.mc, p->mc, 6 * (size_t)p->n_cams);
-    pk.add(&d.cam, p->cam, 17 * (size_t)p->n_cams);
-    pk.add(&d.e_pose, p->edge_pose, (size_t)NE);
-    pk.add(&d.e_point, p->edge_point, (size_t)NE);
-    pk.add(&d.e_cam, p->edge_cam, (size_t)NE);
-    pk.add(&d.e_meas, p->edge_meas, 2 * (size_t)NE);
-    pk.add(&d.e_info, p->edge_info, (size_t)NE);
-    pk.add(&d_poses, (const double*)poses, 6 * (size_t)p->n_poses);
-    pk.add(&d_points, (const double*)points, 3 * (size_t)p->n_points);
-    pk.add(&d_poses_bk, (const double*)poses, 6 * (size_t)p->n_poses);
-    pk.add(&d_points_bk, (const double*)points, 3 * (size_t)p->n_points);
-    pk.add(&d.aedge, s.aedge);
-    pk.add(&d.pose_h, s.pose_h); pk.add(&d.point_h, s.point_h);
-    pk.add(&d.hpose_vtx, s.hpose_vtx); pk.add(&d.hpt_vtx, s.hpt_vtx);
-    pk.add(&d.pt_ptr, s.pt_ptr); pk.add(&d.pt_edges, s.pt_edges);
-    pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
-    pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
-    pk.add(&d.it_blk, s.it_blk); pk.add(&d.it_chunk, s.it_chunk); pk.add(&d.it_slot, s.it_slot);
-    pk.add(&d.fin_blk, s.fin_blk); pk.add(&d.fin_slot0, s.fin_slot0); pk.add(&d.fin_nch, s.fin_nch);
-    pk.add(&d.pr_ptr, s.pr_ptr); pk.add(&d.pr_e1, s.pr_e1); pk.add(&d.pr_e2, s.pr_e2);
-    he = pk.flush(c);
-  }
-  d.delta = p->huber_delta;
-  d.dsqr = p->huber_delta * p->huber_delta;
-  d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
-  d.nae = (int)s.aedge.size();
-  d.np = s.np; d.nl = s.nl;
-  d.npe = (int)s.pt_edges.size();
-  auto dz = [&](size_t cnt_) { double* q = (double*)c->alloc(std::max<size_t>(1, cnt_) * 8); if (!q) he = hipErrorOutOfMemory; return q; };
-  d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
-  d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
-  d.Hpp = dz(36 * (size_t)s.np); d.bp = dz(6 * (size_t)s.np);
-  d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
-  d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
-  d.S = sh.xchg + X.S; d.bs = sh.xchg + X.bs; d.hdiag = sh.xchg + X.hdiag; d.bpf = sh.xchg + X.bpf;
-  d.xp = dz((size_t)ldlt::TB * T);
-  d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
-  d.schur_part = dz((size_t)s.n_slots * 42);
-  ldlt::Work lw;
-  lw.L = dz(ldlt::tile_doubles(T));
-  lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
-  lw.z = dz((size_t)ldlt::TB * T);
-  // scalars: [0] chi2 [1] point scale [2] pose scale [3] chi_now; the solve flag in [5] (one
-  // 48-byte readback per trial)
-  double* d_scalar = dz(8);
-  double* d_part = dz(kRedPartMax);
-  int* d_flag = reinterpret_cast<int*>(d_scalar + 5);
-  if (he != hipSuccess) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
-  d.push_poses = d_poses_bk; d.push_points = d_points_bk;
-  d.n_pose_dbl = 6 * p->n_poses; d.n_point_dbl = 3 * p->n_points;
-  d.flag = d_flag;
-  const unsigned g_state = gb(std::max(d.n_pose_dbl, d.n_point_dbl));
-
-  // control state agreed by all ranks: the caller's stop flag is folded into every scalar
-  // exchange, so no rank leaves the LM loop alone
-  volatile int32_t aux = 0;
-  volatile int32_t* stop = stop_flag ? stop_flag : &aux;
-  int agreed_stop = 0;
-  const size_t sc = X.sc;
-  const bool sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
-
-  auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate (all ranks)
-    hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
-    MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
-    MCS_HIP_CHECK(hipStreamSynchronize(st));
-    double v[2] = {c->pinned[3], (double)(*stop != 0)};
-    int r = allreduce_host(v, 2, MCS_REDUCE_SUM, sc);
-    if (r) return r;
-    *out = v[0];
-    agreed_stop = v[1] > 0;
-    return MCS_OK;
-  };
-  // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda in d (by value)
-  auto enqueue_trial = [&]() -> int {
-    int rc2;
-    rec(2);
-    // also pushes the state (poses / points -> backups) and resets the solve flag
-    hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, d);
-    if (s.np) {
-      const int nitem = (int)s.it_blk.size(), nfin = (int)s.fin_blk.size();
-      hipLaunchKernelGGL(k_schur, dim3((unsigned)((nitem + 3) / 4)), dim3(256), 0, st, d, nitem);
-      if (nfin)
-        hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nfin + 3) / 4)), dim3(256), 0, st, d, nfin);
-      // one tile (LocalBA): the padding is applied inside the fused solve, after the exchange
-      if (T > 1) MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
-      rec(3);
-      if ((rc2 = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc2;   // S tiles | bs
-      rec(4);
-      if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st));
-      else MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
-    } else {
-      rec(3); rec(4);
-    }
-    rec(5);
-    hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, d);
-    hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
-    if (sig_path) {
-      Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}};
-      hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
-    } else {
-      reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
-      reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
-      reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
-      MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
-    }
-    rec(6);
-    return MCS_OK;
-  };
-  // wait for the trial's outcome: spin on the released sequence number (sig_path), checking
-  // the stream now and then so a failed launch cannot spin forever; else synchronise the
-  // stream after the readback copy.  Fills pinned[0..2] and the solve flag.
-  auto wait_trial = [&](int* fl) -> int {
-    if (!sig_path) {
-      MCS_HIP_CHECK(hipStreamSynchronize(st));
-      std::memcpy(fl, c->pinned + 5, sizeof(*fl));
-      return MCS_OK;
-    }
-    const uint64_t want = c->sig_seq;
-    auto arrived = [&]() {
-      return __atomic_load_n(&c->sig->seq[0], __ATOMIC_ACQUIRE) == want &&
-             __atomic_load_n(&c->sig->seq[1], __ATOMIC_ACQUIRE) == want &&
-             __atomic_load_n(&c->sig->seq[2], __ATOMIC_ACQUIRE) == want;
-    };
-    for (uint32_t k = 1;; k++) {
-      if (arrived()) break;
-      __builtin_ia32_pause();   // spin politely: other ranks' threads may share this core
-      if ((k & 1023) == 0) {
-        const hipError_t q = hipStreamQuery(st);
-        if (q == hipSuccess) {
-          if (arrived()) break;
-          set_error("BA: trial signal missing after the stream drained");
-          return MCS_ERR_HIP;
-        }
-        if (q != hipErrorNotReady) { set_hip_error(q, "BA trial", __FILE__, __LINE__); return MCS_ERR_HIP; }
+      if (p->edge_pose[e] < 0 || p->edge_pose[e] >= p->n_poses || p->edge_point[e] < 0 ||
+          p->edge_point[e] >= p->n_points || p->edge_cam[e] < 0 || p->edge_cam[e] >= p->n_cams) {
+        set_error("edge vertex index out of range");
+        return MCS_ERR_ARG;
       }
     }
-    c->pinned[0] = c->sig->v[0]; c->pinned[1] = c->sig->v[1]; c->pinned[2] = c->sig->v[2];
-    *fl = c->sig->flag;
-    if (c->timing) MCS_HIP_CHECK(hipStreamSynchronize(st));   // events complete
+    MCS_HIP_CHECK(hipSetDevice(c->device));
+    if (shard_in && shard_in->world > 1) {
+      if (!shard_in->xchg || !shard_in->allreduce || shard_in->rank < 0 || shard_in->rank >= shard_in->world ||
+          shard_in->xchg_cap < xchg_doubles(p->n_poses)) {
+        set_error("invalid mcs_ba_shard (exchange buffer too small or no allreduce callback)");
+        return MCS_ERR_ARG;
+      }
+      sh.rank = shard_in->rank; sh.world = shard_in->world; sh.xchg = shard_in->xchg;
+      sh.fn = shard_in->allreduce; sh.user = shard_in->user;
+    }
+    sharded = sh.world > 1;
+    st = c->st;
+    c->free_all();
+    if (!sharded) {
+      sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
+      if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+    }
+    // ---- structure: global pose activity (+ active point / edge counts)
+    int rc;
+    std::vector<double> cnt((size_t)p->n_poses + 2, 0.0);
+    {
+      int nae_l = 0;
+      std::vector<char> pt_seen(points_fixed ? 0 : p->n_points, 0);
+      int nl_l = 0;
+      for (int e = 0; e < p->n_edges; e++) {
+        if (edge_level && edge_level[e]) continue;
+        if (points_fixed && p->pose_fixed[p->edge_pose[e]]) continue;   // all vertices fixed
+        cnt[p->edge_pose[e]] += 1.0;
+        nae_l++;
+        if (!points_fixed && !pt_seen[p->edge_point[e]]) { pt_seen[p->edge_point[e]] = 1; nl_l++; }
+      }
+      cnt[p->n_poses] = nl_l;
+      cnt[p->n_poses + 1] = nae_l;
+      if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
+    }
+    hc.mark(c->host_ms, 0);
+    build_structure(*p, edge_level, points_fixed, cnt, s);
+    hc.mark(c->host_ms, 1);
+    nl_glob = (int)cnt[p->n_poses];
+    nae_glob = (int)cnt[p->n_poses + 1];
+    n = 6 * s.np;
+    T = ldlt::tiles_for(std::max(1, n));
+    if ((size_t)T * ldlt::TB * 8 > 96 * 1024) {
+      set_error("more than 2048 active poses: exceeds the backward-solve LDS budget");
+      return MCS_ERR_UNSUPPORTED;
+    }
+    X = XLayout(T, s.np);
+    NE = p->n_edges;
+    double *d_poses_bk = nullptr, *d_points_bk = nullptr;
+    {
+      Packer pk;
+      pk.add(&d.mc, p->mc, 6 * (size_t)p->n_cams);
+      pk.add(&d.cam, p->cam, 17 * (size_t)p->n_cams);
+      pk.add(&d.e_pose, p->edge_pose, (size_t)NE);
+      pk.add(&d.e_point, p->edge_point, (size_t)NE);
+      pk.add(&d.e_cam, p->edge_cam, (size_t)NE);
+      pk.add(&d.e_meas, p->edge_meas, 2 * (size_t)NE);
+      pk.add(&d.e_info, p->edge_info, (size_t)NE);
+      pk.add(&d_poses, poses, 6 * (size_t)p->n_poses);
+      pk.add(&d_points, points, 3 * (size_t)p->n_points);
+      pk.add(&d_poses_bk, poses, 6 * (size_t)p->n_poses);
+      pk.add(&d_points_bk, points, 3 * (size_t)p->n_points);
+      pk.add(&d.aedge, s.aedge);
+      pk.add(&d.pose_h, s.pose_h); pk.add(&d.point_h, s.point_h);
+      pk.add(&d.hpose_vtx, s.hpose_vtx); pk.add(&d.hpt_vtx, s.hpt_vtx);
+      pk.add(&d.pt_ptr, s.pt_ptr); pk.add(&d.pt_edges, s.pt_edges); pk.add(&d.pt_h, s.pt_h);
+      pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
+      pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
+      he = pk.flush(c);
+    }
+    d.delta = p->huber_delta;
+    d.dsqr = p->huber_delta * p->huber_delta;
+    d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
+    d.nae = (int)s.aedge.size();
+    d.np = s.np; d.nl = s.nl;
+    d.npe = (int)s.pt_edges.size();
+    d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
+    d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
+    d.Hpp = dz(36 * (size_t)s.np); d.bp = dz(6 * (size_t)s.np);
+    d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
+    d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
+    d.S = sh.xchg + X.S; d.bs = sh.xchg + X.bs; d.hdiag = sh.xchg + X.hdiag; d.bpf = sh.xchg + X.bpf;
+    d.xp = dz((size_t)ldlt::TB * T);
+    d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
+    // bounds of the device-built pair lists / items: a point with k active edges gives at most
+    // k (k + 1) / 2 pairs; a block at most 1 + pairs / CH + pose edges / CH chunks
+    nblk = s.np * (s.np + 1) / 2;
+    pmax = 0;
+    for (int l = 0; l < s.nl; l++) {
+      const int64_t k = s.pt_ptr[l + 1] - s.pt_ptr[l];
+      pmax += k * (k + 1) / 2;
+    }
+    if (pmax > INT32_MAX) { set_error("BA: more than 2^31 Schur pairs"); return MCS_ERR_UNSUPPORTED; }
+    items_max = (int)std::min<int64_t>(INT32_MAX, 2 * (int64_t)nblk + pmax / kSchurChunk +
+                                                       s.ps_ptr[s.np] / kSchurChunk + 1);
+    d.schur_part = dz((size_t)items_max * 42);
+
+    lw.L = dz(ldlt::tile_doubles(T));
+    lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
+    lw.z = dz((size_t)ldlt::TB * T);
+    // scalars: [0] chi2 [1] point scale [2] pose scale [3] chi_now; the solve flag in [5] (one
+    // 48-byte readback per trial)
+    d_scalar = dz(8);
+    d_part = dz(kRedPartMax);
+    d_flag = reinterpret_cast<int*>(d_scalar + 5);
+    if (he != hipSuccess) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
+    d.push_poses = d_poses_bk; d.push_points = d_points_bk;
+    d.n_pose_dbl = 6 * p->n_poses; d.n_point_dbl = 3 * p->n_points;
+    d.flag = d_flag;
+    g_state = gb(std::max(d.n_pose_dbl, d.n_point_dbl));
+    sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
+    const int rp = enqueue_pairs();
+    hc.mark(c->host_ms, 2);
+    return rp;
+  }
+
+  // The Schur pair lists and k_schur items, built on the device (the kernels above), stream
+  // ordered after the upload: nothing is read back.
+  int enqueue_pairs() {
+    int32_t* cnt = (int32_t*)c->alloc(4 * (size_t)(s.nl + 1));
+    int32_t* off = (int32_t*)c->alloc(4 * (size_t)(s.nl + 1));
+    uint32_t* k_in = (uint32_t*)c->alloc(4 * (size_t)std::max<int64_t>(1, pmax));
+    uint32_t* k_out = (uint32_t*)c->alloc(4 * (size_t)std::max<int64_t>(1, pmax));
+    uint2* v_in = (uint2*)c->alloc(8 * (size_t)std::max<int64_t>(1, pmax));
+    uint2* v_out = (uint2*)c->alloc(8 * (size_t)std::max<int64_t>(1, pmax));
+    int32_t* pr_ptr = (int32_t*)c->alloc(4 * (size_t)(nblk + 1));
+    int32_t* nch = (int32_t*)c->alloc(4 * (size_t)(nblk + 1));
+    int32_t* nslot = (int32_t*)c->alloc(4 * (size_t)(nblk + 1));
+    int32_t* it_off = (int32_t*)c->alloc(4 * (size_t)(nblk + 1));
+    int32_t* slot_off = (int32_t*)c->alloc(4 * (size_t)(nblk + 1));
+    int32_t* it_blk = (int32_t*)c->alloc(4 * (size_t)items_max);
+    int32_t* it_chunk = (int32_t*)c->alloc(4 * (size_t)items_max);
+    int32_t* it_slot = (int32_t*)c->alloc(4 * (size_t)items_max);
+    int32_t* it_nch = (int32_t*)c->alloc(4 * (size_t)items_max);
+    int32_t* nitem = (int32_t*)c->alloc(4);
+    if (!cnt || !off || !k_in || !k_out || !v_in || !v_out || !pr_ptr || !nch || !nslot || !it_off ||
+        !slot_off || !it_blk || !it_chunk || !it_slot || !it_nch || !nitem) {
+      set_error("BA: out of device memory (pair lists)");
+      return MCS_ERR_HIP;
+    }
+    const unsigned bits = nblk > 0 ? 32u - (unsigned)__builtin_clz((unsigned)nblk) : 1u;
+    size_t b_scan1 = 0, b_scan2 = 0, b_sort = 0;
+    auto plus = rocprim::plus<int32_t>();
+    MCS_HIP_CHECK(rocprim::exclusive_scan(nullptr, b_scan1, cnt, off, 0, (size_t)s.nl + 1, plus, st));
+    MCS_HIP_CHECK(rocprim::exclusive_scan(nullptr, b_scan2, nch, it_off, 0, (size_t)nblk + 1, plus, st));
+    if (pmax > 0)
+      MCS_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, b_sort, k_in, k_out, v_in, v_out, (size_t)pmax, 0u, bits, st));
+    const size_t tb = std::max(std::max(b_scan1, b_scan2), b_sort) + 256;
+    void* tmp = c->alloc(tb);
+    if (!tmp) { set_error("BA: out of device memory (scan storage)"); return MCS_ERR_HIP; }
+    size_t b = tb;
+    hipLaunchKernelGGL(k_pair_count, dim3(gb(s.nl + 1)), dim3(256), 0, st, d, cnt);
+    MCS_HIP_CHECK(rocprim::exclusive_scan(tmp, b, cnt, off, 0, (size_t)s.nl + 1, plus, st));
+    if (pmax > 0) {
+      const unsigned g = std::max(gb(s.nl), std::min(gb((int)std::min<int64_t>(pmax, INT32_MAX)), 4096u));
+      hipLaunchKernelGGL(k_pair_emit, dim3(g), dim3(256), 0, st, d, (const int32_t*)off, k_in, v_in, pmax,
+                         (uint32_t)nblk);
+      b = tb;
+      MCS_HIP_CHECK(rocprim::radix_sort_pairs(tmp, b, k_in, k_out, v_in, v_out, (size_t)pmax, 0u, bits, st));
+    }
+    hipLaunchKernelGGL(k_block_ptr, dim3(gb(nblk + 1)), dim3(256), 0, st, d, (const uint32_t*)k_out, pmax,
+                       nblk, pr_ptr, nch, nslot);
+    b = tb;
+    MCS_HIP_CHECK(rocprim::exclusive_scan(tmp, b, nch, it_off, 0, (size_t)nblk + 1, plus, st));
+    b = tb;
+    MCS_HIP_CHECK(rocprim::exclusive_scan(tmp, b, nslot, slot_off, 0, (size_t)nblk + 1, plus, st));
+    hipLaunchKernelGGL(k_block_items, dim3(gb(nblk + 1)), dim3(256), 0, st, nblk, (const int32_t*)nch,
+                       (const int32_t*)it_off, (const int32_t*)slot_off, it_blk, it_chunk, it_slot, it_nch,
+                       nitem);
+    MCS_HIP_CHECK(hipGetLastError());
+    d.pr_ptr = pr_ptr; d.pr = v_out;
+    d.it_blk = it_blk; d.it_chunk = it_chunk; d.it_slot = it_slot;
+    d.blk_nch = nch; d.blk_slot0 = slot_off;
+    it_nch_dev = it_nch;
+    d.nitem = nitem;
     return MCS_OK;
-  };
-  double chi0 = 0;
-  if ((s.np + nl_glob) == 0 || nae_glob == 0) {
-    if (rep) rep->chi2_initial = rep->chi2_final = 0;
-  } else {
-    if ((rc = chi_now(&chi0))) return rc;
-    if (rep) rep->chi2_initial = chi0;
-    double lambda = 0, lastChi = 0;
-    int ni = 2, nBad = 0, it = 0;
-    bool ok = true;
-    double currentChi = chi0;
-    for (int i = 0; i < o->max_iterations && !agreed_stop && ok; i++) {
-      // ---- OptimizationAlgorithmLevenberg::solve(i)
-      // The robust chi2 of the linearisation point equals the chi2 the previous iteration
-      // ended with (same kernel, same state: accepted trial or restored backup), so only
-      // the first iteration reads anything back (the max diagonal for lambda's init).
-      rec(0);
-      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
-      hipLaunchKernelGGL(k_points_build, dim3(gb(4 * s.nl)), dim3(256), 0, st, d);
-      if (s.np) hipLaunchKernelGGL(k_poses_build, dim3(s.np), dim3(kRedNT), 0, st, d);
-      rec(1);
-      c->n_iter++;
-      bool lin_pending = c->timing;
-      if ((rc = allreduce(MCS_REDUCE_SUM, X.hdiag, 12 * (size_t)s.np))) return rc;   // hdiag | bpf
-      if (i == 0) {
+  }
+
+  // More edges at level 1 (a subset of the active ones; unsharded only).  g2o re-runs
+  // initializeOptimization: the culled edges leave the graph, and a vertex left without active
+  // edges leaves the system.  Here the culled edges' per-edge terms (weight, Jacobians, Hpl,
+  // error) are zeroed once and the active-edge list shrinks; every sum they took part in then
+  // adds exact zeros, and a point left without edges keeps Hll = 0 (its update is Dinv * 0 = 0,
+  // its Schur and model-decrease terms are 0).  Returns 1 (nothing changed on the device) when
+  // an active pose would leave the system: the caller then rebuilds from scratch.
+  int remask(const uint8_t* edge_level) {
+    if (sharded) return 1;
+    HostClock hc;
+    std::vector<int32_t> keep;
+    std::vector<int32_t> culled;
+    keep.reserve(s.aedge.size());
+    std::vector<int32_t> pose_left(s.np, 0);
+    std::vector<char> pt_left(s.nl, 0);
+    for (int e : s.aedge) {
+      if (edge_level && edge_level[e]) { culled.push_back(e); continue; }
+      keep.push_back(e);
+      const int h = s.pose_h[p->edge_pose[e]];
+      if (h >= 0) pose_left[h]++;
+      const int l = s.point_h[p->edge_point[e]];
+      if (l >= 0) pt_left[l] = 1;
+    }
+    for (int h = 0; h < s.np; h++)
+      if (pose_left[h] == 0) return 1;
+    int nl_left = 0;
+    for (int l = 0; l < s.nl; l++) nl_left += pt_left[l];
+    if (!culled.empty()) {
+      const size_t nb = (keep.size() + culled.size()) * 4 + 512;
+      uint8_t* h = c->stage_get(nb);   // the stream is idle: run() ended with a synchronise
+      if (!h) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
+      int32_t* dk = (int32_t*)c->alloc(std::max<size_t>(1, keep.size()) * 4);
+      int32_t* dc = (int32_t*)c->alloc(culled.size() * 4);
+      if (!dk || !dc) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+      const size_t off_c = ((keep.size() * 4 + 255) & ~(size_t)255);
+      std::memcpy(h, keep.data(), keep.size() * 4);
+      std::memcpy(h + off_c, culled.data(), culled.size() * 4);
+      if (!keep.empty()) MCS_HIP_CHECK(hipMemcpyAsync(dk, h, keep.size() * 4, hipMemcpyHostToDevice, st));
+      MCS_HIP_CHECK(hipMemcpyAsync(dc, h + off_c, culled.size() * 4, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_zero_edges, dim3(gb((int)culled.size())), dim3(256), 0, st, d, (const int32_t*)dc,
+                         (int)culled.size());
+      d.aedge = dk;
+      d.nae = (int)keep.size();
+    }
+    s.aedge.swap(keep);
+    nae_glob = d.nae;
+    nl_glob = nl_left;
+    sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
+    hc.mark(c->host_ms, 4);
+    return MCS_OK;
+  }
+
+  int run(const mcs_ba_options* o, double* poses, double* points, double* edge_chi2,
+          volatile int32_t* stop_flag, mcs_ba_report* rep) {
+    // one GPU and no per-stage timing: the LM control runs on the device (no per-trial
+    // host round trip); sharded runs agree on every decision through the host exchange
+    if (!sharded && !c->timing) return run_device(o, poses, points, edge_chi2, stop_flag, rep);
+    auto rec = [&](int k) { if (c->timing) (void)hipEventRecord(c->ev[k], st); };
+    auto ms = [&](int a, int b) { float f = 0.f; (void)hipEventElapsedTime(&f, c->ev[a], c->ev[b]); return (double)f; };
+    int rc;
+    if (rep) {
+      rep->n_active_edges = nae_glob;
+      rep->n_active_poses = s.np;
+      rep->n_active_points = nl_glob;
+      rep->iterations = 0;
+    }
+    // control state agreed by all ranks: the caller's stop flag is folded into every scalar
+    // exchange, so no rank leaves the LM loop alone
+    volatile int32_t aux = 0;
+    volatile int32_t* stop = stop_flag ? stop_flag : &aux;
+    int agreed_stop = 0;
+    const size_t sc = X.sc;
+
+    auto chi_now = [&](double* out) -> int {   // robust chi2 of the current estimate (all ranks)
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
+      reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+      MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar, 8, hipMemcpyDeviceToHost, st));
+      MCS_HIP_CHECK(hipStreamSynchronize(st));
+      double v[2] = {c->pinned[3], (double)(*stop != 0)};
+      int r = allreduce_host(v, 2, MCS_REDUCE_SUM, sc);
+      if (r) return r;
+      *out = v[0];
+      agreed_stop = v[1] > 0;
+      return MCS_OK;
+    };
+    // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda in d (by value)
+    auto enqueue_trial = [&]() -> int {
+      int rc2;
+      rec(2);
+      // also pushes the state (poses / points -> backups) and resets the solve flag
+      hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, d);
+      if (s.np) {
+        hipLaunchKernelGGL(k_schur, dim3((unsigned)((items_max + 3) / 4)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, d, nblk);
+        // one tile (LocalBA): the padding is applied inside the fused solve, after the exchange
+        if (T > 1) MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
+        rec(3);
+        if ((rc2 = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc2;   // S tiles | bs
+        rec(4);
+        if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st));
+        else MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
+      } else {
+        rec(3); rec(4);
+      }
+      rec(5);
+      hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 0);
+      if (sig_path) {
+        Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}};
+        hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
+      } else {
+        reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
+        reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
+        reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, d_scalar, 48, hipMemcpyDeviceToHost, st));
+      }
+      rec(6);
+      return MCS_OK;
+    };
+    // wait for the trial's outcome: spin on the released sequence number (sig_path), checking
+    // the stream now and then so a failed launch cannot spin forever; else synchronise the
+    // stream after the readback copy.  Fills pinned[0..2] and the solve flag.
+    auto wait_trial = [&](int* fl) -> int {
+      if (!sig_path) {
+        MCS_HIP_CHECK(hipStreamSynchronize(st));
+        std::memcpy(fl, c->pinned + 5, sizeof(*fl));
+        return MCS_OK;
+      }
+      const uint64_t want = c->sig_seq;
+      auto arrived = [&]() {
+        return __atomic_load_n(&c->sig->seq[0], __ATOMIC_ACQUIRE) == want &&
+               __atomic_load_n(&c->sig->seq[1], __ATOMIC_ACQUIRE) == want &&
+               __atomic_load_n(&c->sig->seq[2], __ATOMIC_ACQUIRE) == want;
+      };
+      for (uint32_t k = 1;; k++) {
+        if (arrived()) break;
+        __builtin_ia32_pause();   // spin politely: other ranks' threads may share this core
+        if ((k & 1023) == 0) {
+          const hipError_t q = hipStreamQuery(st);
+          if (q == hipSuccess) {
+            if (arrived()) break;
+            set_error("BA: trial signal missing after the stream drained");
+            return MCS_ERR_HIP;
+          }
+          if (q != hipErrorNotReady) { set_hip_error(q, "BA trial", __FILE__, __LINE__); return MCS_ERR_HIP; }
+        }
+      }
+      c->pinned[0] = c->sig->v[0]; c->pinned[1] = c->sig->v[1]; c->pinned[2] = c->sig->v[2];
+      *fl = c->sig->flag;
+      if (c->timing) MCS_HIP_CHECK(hipStreamSynchronize(st));   // events complete
+      return MCS_OK;
+    };
+    double chi0 = 0;
+    if ((s.np + nl_glob) == 0 || nae_glob == 0) {
+      if (rep) rep->chi2_initial = rep->chi2_final = 0;
+    } else {
+      if ((rc = chi_now(&chi0))) return rc;
+      if (rep) rep->chi2_initial = chi0;
+      double lambda = 0, lastChi = 0;
+      int ni = 2, nBad = 0, it = 0;
+      bool ok = true;
+      double currentChi = chi0;
+      for (int i = 0; i < o->max_iterations && !agreed_stop && ok; i++) {
+        // ---- OptimizationAlgorithmLevenberg::solve(i)
+        // The robust chi2 of the linearisation point equals the chi2 the previous iteration
+        // ended with (same kernel, same state: accepted trial or restored backup), so only
+        // the first iteration reads anything back (the max diagonal for lambda's init).
+        rec(0);
+        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
+        hipLaunchKernelGGL(k_build, dim3((unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT)), dim3(kRedNT), 0, st, d);
+        rec(1);
+        c->n_iter++;
+        bool lin_pending = c->timing;
+        if ((rc = allreduce(MCS_REDUCE_SUM, X.hdiag, 12 * (size_t)s.np))) return rc;   // hdiag | bpf
+        if (i == 0) {
+          reduce_dev<true>(d.red, s.nl, d_scalar + 1, d_part, st);
+          reduce_dev<true>(d.hdiag, 6 * s.np, d_scalar + 2, d_part, st);
+          MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 16, hipMemcpyDeviceToHost, st));
+          MCS_HIP_CHECK(hipStreamSynchronize(st));
+          double mx = std::max(c->pinned[1], c->pinned[2]);
+          if ((rc = allreduce_host(&mx, 1, MCS_REDUCE_MAX, sc))) return rc;
+          lambda = o->tau * mx; ni = 2; nBad = 0;
+        }
+        const double iniChi = currentChi;
+        double rho = 0;
+        int qmax = 0;
+        do {
+          // lambda reaches the kernels by value (Dev d), no upload; a captured graph of the trial
+          // (replayed per trial) measured no faster than these direct launches
+          d.lam = lambda;
+          d.lam0 = sh.rank == 0 ? lambda : 0.0;
+          if ((rc = enqueue_trial())) return rc;
+          int fl;   // identical on every rank (same reduced system)
+          if ((rc = wait_trial(&fl))) return rc;
+          if (c->timing) {
+            if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
+            c->acc_ms[1] += ms(2, 3);
+            c->acc_ms[3] += ms(4, 5);
+            c->acc_ms[4] += ms(5, 6);
+            c->n_trial++;
+            c->last_n = n;
+          }
+          double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
+          const double scale_pose = c->pinned[2];
+          if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
+          agreed_stop = tr[2] > 0;
+          double tempChi = tr[0];
+          if (fl) tempChi = std::numeric_limits<double>::max();
+          rho = currentChi - tempChi;
+          double scale = scale_pose + tr[1];
+          scale += 1e-3;
+          rho /= scale;
+          if (rho > 0 && std::isfinite(tempChi)) {
+            double alpha = 1. - cube_rn(2 * rho - 1);
+            alpha = std::min(alpha, 2. / 3.);
+            lambda *= std::max(1. / 3., alpha);
+            ni = 2;
+            currentChi = tempChi;
+          } else {
+            lambda *= ni;
+            ni *= 2;
+            hipLaunchKernelGGL(k_restore, dim3(g_state), dim3(256), 0, st, d);  // pop
+          }
+          qmax++;
+        } while (rho < 0 && qmax < o->max_trials && !agreed_stop);
+        int result = 0;
+        if (qmax == o->max_trials || rho == 0) result = 1;
+        else {
+          if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+          else nBad = 0;
+          if (nBad >= 3) result = 1;
+        }
+        ok = (result == 0);
+        ++it;
+        // ---- SparseOptimizerTerminateAction (post-iteration): activeRobustChi2 of the
+        // current state == currentChi (see above); identical on every rank
+        const double cur = currentChi;
+        if (rep && rep->trace_chi2 && i < rep->trace_cap) rep->trace_chi2[i] = cur;
+        if (i == 0) lastChi = cur;
+        else {
+          bool stopOpt = false;
+          if (i < o->terminate_max_iter) {
+            const double gain = (lastChi - cur) / cur;
+            lastChi = cur;
+            if (gain >= 0 && gain < o->gain_threshold) stopOpt = true;
+          } else {
+            stopOpt = true;
+          }
+          if (stopOpt) { *stop = 1; agreed_stop = 1; }
+        }
+        if (rep) rep->lambda_final = lambda;
+      }
+      if (rep) rep->iterations = it;
+      if (rep) rep->chi2_final = currentChi;
+    }
+    if (rep) rep->stop_flag = *stop;
+    return download(poses, points, edge_chi2);
+  }
+
+  // results through the pinned staging buffer (free again: the stream has been drained since
+  // the upload), then one host copy each; edge_chi2 (nullable): chi2 of every edge
+  int download(double* poses, double* points, double* edge_chi2) {
+    HostClock hc;
+    if (edge_chi2) {
+      // chi2 of every edge (active or not) at the final estimate; a private view: d keeps its
+      // active list for a later remask() + run()
+      Dev d2 = d;
+      d2.ctl = nullptr;
+      d2.aedge = nullptr;
+      d2.nae = NE;
+      d2.err = dz(2 * (size_t)NE);
+      d2.rchi = dz(NE);
+      if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
+      hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
+    }
+    const size_t b_po = 48 * (size_t)p->n_poses, b_pt = 24 * (size_t)p->n_points;
+    const size_t b_ch = edge_chi2 ? 8 * (size_t)NE : 0;
+    if (b_po + b_pt + b_ch + 64 > c->stage_cap) MCS_HIP_CHECK(hipStreamSynchronize(st));   // regrow
+    uint8_t* hst = c->stage_get(b_po + b_pt + b_ch + 64);
+    if (!hst) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
+    if (b_po) MCS_HIP_CHECK(hipMemcpyAsync(hst, d_poses, b_po, hipMemcpyDeviceToHost, st));
+    if (b_pt) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po, d_points, b_pt, hipMemcpyDeviceToHost, st));
+    if (b_ch) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt, d.chi, b_ch, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    if (b_po) std::memcpy(poses, hst, b_po);
+    if (b_pt) std::memcpy(points, hst + b_po, b_pt);
+    if (b_ch) std::memcpy(edge_chi2, hst + b_po + b_pt, b_ch);
+    hc.mark(c->host_ms, 3);
+    MCS_HIP_CHECK(hipGetLastError());
+    return MCS_OK;
+  }
+
+  // Device-driven SparseOptimizer::optimize: the host enqueues LM steps (restore if the last
+  // trial was rejected, linearisation if it ended an iteration, one trial, k_lm_end) up to two
+  // ahead of the device and watches the progress word only to stop enqueuing; the decisions
+  // are k_lm_end's.  Kernels of steps past the end return at once.
+  int run_device(const mcs_ba_options* o, double* poses, double* points, double* edge_chi2,
+                 volatile int32_t* stop_flag, mcs_ba_report* rep) {
+    if (rep) {
+      rep->n_active_edges = nae_glob;
+      rep->n_active_poses = s.np;
+      rep->n_active_points = nl_glob;
+      rep->iterations = 0;
+    }
+    volatile int32_t aux = 0;
+    volatile int32_t* stop = stop_flag ? stop_flag : &aux;
+    LmCtl* dctl = (LmCtl*)c->alloc(sizeof(LmCtl));
+    if (!dctl) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+    LmCtl h0;
+    std::memset(&h0, 0, sizeof(h0));
+    h0.tau = o->tau; h0.gain_threshold = o->gain_threshold;
+    h0.max_iterations = o->max_iterations; h0.max_trials = o->max_trials;
+    h0.terminate_max_iter = o->terminate_max_iter;
+    h0.lin = 1; h0.ni = 2;
+    const bool empty = (s.np + nl_glob) == 0 || nae_glob == 0;
+    h0.done = (empty || o->max_iterations <= 0 || *stop != 0) ? 1 : 0;
+    c->lsig->ext_stop = *stop != 0;
+    MCS_HIP_CHECK(hipMemcpyAsync(dctl, &h0, sizeof(h0), hipMemcpyHostToDevice, st));
+    Dev dd = d;
+    dd.ctl = dctl;
+    const int* skip = &dctl->done;
+    const unsigned g_upd = gb(4 * s.nl + s.np), g_edg = gb(d.nae);
+    dd.part_chi = dz(g_edg);
+    dd.part_pt = dz(g_upd);
+    dd.part_ps = dz(g_upd);
+    if (he != hipSuccess) { set_hip_error(he, "BA partials", __FILE__, __LINE__); return MCS_ERR_HIP; }
+    if (!empty) {   // chi2 of the starting point (activeRobustChi2 before the first iteration)
+      Dev d0 = d;
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d0, 0);
+      reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
+      hipLaunchKernelGGL(k_lm_start, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
+    }
+    auto enqueue_step = [&](int step) -> int {
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
+      hipLaunchKernelGGL(k_build, dim3((unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT)), dim3(kRedNT), 0, st, dd);
+      if (step == 0) {   // iteration 0 is always step 0: lambda from the max diagonal
         reduce_dev<true>(d.red, s.nl, d_scalar + 1, d_part, st);
         reduce_dev<true>(d.hdiag, 6 * s.np, d_scalar + 2, d_part, st);
-        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 1, d_scalar + 1, 16, hipMemcpyDeviceToHost, st));
-        MCS_HIP_CHECK(hipStreamSynchronize(st));
-        double mx = std::max(c->pinned[1], c->pinned[2]);
-        if ((rc = allreduce_host(&mx, 1, MCS_REDUCE_MAX, sc))) return rc;
-        lambda = o->tau * mx; ni = 2; nBad = 0;
+        hipLaunchKernelGGL(k_lm_lambda0, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
       }
-      const double iniChi = currentChi;
-      double rho = 0;
-      int qmax = 0;
-      do {
-        // lambda reaches the kernels by value (Dev d), no upload; a captured graph of the trial
-        // (replayed per trial) measured no faster than these direct launches
-        d.lam = lambda;
-        d.lam0 = sh.rank == 0 ? lambda : 0.0;
-        if ((rc = enqueue_trial())) return rc;
-        int fl;   // identical on every rank (same reduced system)
-        if ((rc = wait_trial(&fl))) return rc;
-        if (c->timing) {
-          if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
-          c->acc_ms[1] += ms(2, 3);
-          c->acc_ms[3] += ms(4, 5);
-          c->acc_ms[4] += ms(5, 6);
-          c->n_trial++;
-          c->last_n = n;
+      hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, dd);
+      if (s.np) {
+        hipLaunchKernelGGL(k_schur, dim3((unsigned)((items_max + 3) / 4)), dim3(256), 0, st, dd);
+        hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, dd, nblk);
+        if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st, skip));
+        else {
+          MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, 1.0, st, skip));
+          MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st, skip));
         }
-        double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
-        const double scale_pose = c->pinned[2];
-        if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
-        agreed_stop = tr[2] > 0;
-        double tempChi = tr[0];
-        if (fl) tempChi = std::numeric_limits<double>::max();
-        rho = currentChi - tempChi;
-        double scale = scale_pose + tr[1];
-        scale += 1e-3;
-        rho /= scale;
-        if (rho > 0 && std::isfinite(tempChi)) {
-          double alpha = 1. - std::pow((2 * rho - 1), 3);
-          alpha = std::min(alpha, 2. / 3.);
-          lambda *= std::max(1. / 3., alpha);
-          ni = 2;
-          currentChi = tempChi;
-        } else {
-          lambda *= ni;
-          ni *= 2;
-          hipLaunchKernelGGL(k_restore, dim3(g_state), dim3(256), 0, st, d);  // pop
-        }
-        qmax++;
-      } while (rho < 0 && qmax < o->max_trials && !agreed_stop);
-      int result = 0;
-      if (qmax == o->max_trials || rho == 0) result = 1;
-      else {
-        if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-        else nBad = 0;
-        if (nBad >= 3) result = 1;
       }
-      ok = (result == 0);
-      ++it;
-      // ---- SparseOptimizerTerminateAction (post-iteration): activeRobustChi2 of the
-      // current state == currentChi (see above); identical on every rank
-      const double cur = currentChi;
-      if (rep && rep->trace_chi2 && i < rep->trace_cap) rep->trace_chi2[i] = cur;
-      if (i == 0) lastChi = cur;
-      else {
-        bool stopOpt = false;
-        if (i < o->terminate_max_iter) {
-          const double gain = (lastChi - cur) / cur;
-          lastChi = cur;
-          if (gain >= 0 && gain < o->gain_threshold) stopOpt = true;
-        } else {
-          stopOpt = true;
+      hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, dd);
+      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 0);
+      // the trial's three sums from the workgroup partials of k_edges / k_update (a fixed
+      // order: partials in workgroup order, each a fixed in-workgroup tree)
+      Sum3 q{{dd.part_chi, dd.part_pt, dd.part_ps}, {(int)g_edg, (int)g_upd, (int)g_upd}};
+      hipLaunchKernelGGL(k_lm_end, dim3(1), dim3(1024), 0, st, dd, q, 2, d_scalar,
+                         (const int*)d_flag, c->lsig, ++c->lsig_seq);
+      return hipGetLastError() == hipSuccess ? MCS_OK : MCS_ERR_HIP;
+    };
+    // progress word of the step whose k_lm_end published sequence `want`
+    auto wait_seq = [&](uint64_t want) -> int {
+      for (uint32_t k = 1;; k++) {
+        if (__atomic_load_n(&c->lsig->seq, __ATOMIC_ACQUIRE) >= want) return MCS_OK;
+        __builtin_ia32_pause();
+        if ((k & 1023) == 0) {
+          c->lsig->ext_stop = *stop != 0;   // the caller's abort flag reaches k_lm_end
+          const hipError_t q = hipStreamQuery(st);
+          if (q == hipSuccess) {
+            if (__atomic_load_n(&c->lsig->seq, __ATOMIC_ACQUIRE) >= want) return MCS_OK;
+            set_error("BA: LM progress word missing after the stream drained");
+            return MCS_ERR_HIP;
+          }
+          if (q != hipErrorNotReady) { set_hip_error(q, "BA LM step", __FILE__, __LINE__); return MCS_ERR_HIP; }
         }
-        if (stopOpt) { *stop = 1; agreed_stop = 1; }
       }
-      if (rep) rep->lambda_final = lambda;
+    };
+    int rc;
+    if (!h0.done) {
+      const uint64_t base = c->lsig_seq;
+      const int max_steps = o->max_iterations * std::max(1, o->max_trials);
+      for (int step = 0; step < max_steps; step++) {
+        if (step >= 2) {   // keep two steps in flight: wait for the one before the last
+          if ((rc = wait_seq(base + (uint64_t)step - 1))) return rc;
+          c->lsig->ext_stop = *stop != 0;
+          if (c->lsig->done) break;
+        }
+        if ((rc = enqueue_step(step))) { set_error("BA: LM step launch failed"); return rc; }
+      }
     }
-    if (rep) rep->iterations = it;
-    if (rep) rep->chi2_final = currentChi;
+    LmCtl* hc = (LmCtl*)c->pinned_ctl;
+    MCS_HIP_CHECK(hipMemcpyAsync(hc, dctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
+    // per-edge chi2 of every edge at the final estimate, poses, points: the common tail
+    const int rtail = download(poses, points, edge_chi2);
+    if (rtail) return rtail;
+    if (hc->stop_out) *stop = 1;   // the terminate action raised the flag (host-visible)
+    if (rep) {
+      rep->chi2_initial = empty ? 0.0 : hc->chi0;
+      rep->chi2_final = empty ? 0.0 : hc->currentChi;
+      rep->iterations = hc->it;
+      rep->lambda_final = hc->lambda_final;
+      if (rep->trace_chi2)
+        for (int i = 0; i < std::min(hc->iter, std::min(rep->trace_cap, kLmTraceCap)); i++)
+          rep->trace_chi2[i] = hc->trace[i];
+      rep->stop_flag = *stop;
+    }
+    return MCS_OK;
   }
-  if (rep) rep->stop_flag = *stop;
-  // results through the pinned staging buffer (free again: the stream has been drained since
-  // the upload), then one host copy each
-  if (edge_chi2) {
-    // chi2 of every edge (active or not) at the final estimate
-    Dev d2 = d;
-    d2.aedge = nullptr;
-    d2.nae = NE;
-    d2.rchi = dz(NE);
-    if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
-    hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
-  }
-  const size_t b_po = 48 * (size_t)p->n_poses, b_pt = 24 * (size_t)p->n_points;
-  const size_t b_ch = edge_chi2 ? 8 * (size_t)NE : 0;
-  if (b_po + b_pt + b_ch + 64 > c->stage_cap) MCS_HIP_CHECK(hipStreamSynchronize(st));   // regrow
-  uint8_t* hst = c->stage_get(b_po + b_pt + b_ch + 64);
-  if (!hst) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
-  if (b_po) MCS_HIP_CHECK(hipMemcpyAsync(hst, d_poses, b_po, hipMemcpyDeviceToHost, st));
-  if (b_pt) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po, d_points, b_pt, hipMemcpyDeviceToHost, st));
-  if (b_ch) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt, d.chi, b_ch, hipMemcpyDeviceToHost, st));
-  MCS_HIP_CHECK(hipStreamSynchronize(st));
-  if (b_po) std::memcpy(poses, hst, b_po);
-  if (b_pt) std::memcpy(points, hst + b_po, b_pt);
-  if (b_ch) std::memcpy(edge_chi2, hst + b_po + b_pt, b_ch);
-  MCS_HIP_CHECK(hipGetLastError());
-  return MCS_OK;
+};
+
+int optimize_impl(mcs_ba_ctx* c, const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
+                  double* points, const uint8_t* edge_level, double* edge_chi2,
+                  volatile int32_t* stop_flag, mcs_ba_report* rep, const mcs_ba_shard* shard_in,
+                  bool points_fixed) {
+  if (!c || !p || !o || !poses || !points) return MCS_ERR_ARG;
+  Optimizer opt(c, p, points_fixed);
+  int rc = opt.setup(poses, points, edge_level, shard_in);
+  if (rc) return rc;
+  return opt.run(o, poses, points, edge_chi2, stop_flag, rep);
 }
 
 }  // namespace
@@ -1341,6 +1909,9 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocDefault));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->sig, sizeof(TrialSig), hipHostMallocCoherent | hipHostMallocMapped));
   std::memset((void*)c->sig, 0, sizeof(TrialSig));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->lsig, sizeof(LmSig), hipHostMallocCoherent | hipHostMallocMapped));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_ctl, sizeof(LmCtl), hipHostMallocDefault));
+  std::memset((void*)c->lsig, 0, sizeof(LmSig));
   *out = c;
   return MCS_OK;
 }
@@ -1353,6 +1924,8 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pinned_i) (void)hipHostFree(c->pinned_i);
   if (c->sig) (void)hipHostFree(c->sig);
+  if (c->lsig) (void)hipHostFree(c->lsig);
+  if (c->pinned_ctl) (void)hipHostFree(c->pinned_ctl);
   if (c->stage) (void)hipHostFree(c->stage);
   if (c->st) (void)hipStreamDestroy(c->st);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -1378,6 +1951,50 @@ int mcs_ba_read_timing(mcs_ba_ctx* c, double* ms, int32_t* n_iterations, int32_t
   if (reset) {
     for (double& v : c->acc_ms) v = 0.0;
     c->n_iter = c->n_trial = 0;
+  }
+  return MCS_OK;
+}
+
+int mcs_ba_check_structure(mcs_ba_ctx* c, const mcs_ba_problem* p, const uint8_t* edge_level) {
+  if (!c || !p) return MCS_ERR_ARG;
+  Optimizer opt(c, p, false);
+  int rc = opt.setup(p->poses, p->points, edge_level, nullptr);
+  if (rc) return rc;
+  HostStruct h = c->hs;
+  build_pairs_host(*p, h);
+  const int nb = opt.nblk;
+  std::vector<int32_t> pr_ptr(nb + 1), items;
+  int32_t nitem = 0;
+  MCS_HIP_CHECK(hipMemcpyAsync(pr_ptr.data(), opt.d.pr_ptr, 4 * (size_t)(nb + 1), hipMemcpyDeviceToHost, c->st));
+  MCS_HIP_CHECK(hipMemcpyAsync(&nitem, opt.d.nitem, 4, hipMemcpyDeviceToHost, c->st));
+  MCS_HIP_CHECK(hipStreamSynchronize(c->st));
+  int64_t bad = 0;
+  for (int b = 0; b <= nb; b++) bad += pr_ptr[b] != h.pr_ptr[b];
+  if (bad) return (int)std::min<int64_t>(bad, INT32_MAX);
+  const int np_ = pr_ptr[nb];
+  std::vector<uint2> pr(std::max(1, np_));
+  if (np_) MCS_HIP_CHECK(hipMemcpy(pr.data(), opt.d.pr, 8 * (size_t)np_, hipMemcpyDeviceToHost));
+  for (int q = 0; q < np_; q++) bad += ((int)pr[q].x != h.pr_e1[q]) + ((int)pr[q].y != h.pr_e2[q]);
+  bad += nitem != (int32_t)h.it_blk.size();
+  if (!bad && nitem > 0) {
+    std::vector<int32_t> v(nitem);
+    const int32_t* src[4] = {opt.d.it_blk, opt.d.it_chunk, opt.d.it_slot, opt.it_nch_dev};
+    const std::vector<int32_t>* ref[4] = {&h.it_blk, &h.it_chunk, &h.it_slot, &h.it_nch};
+    for (int k = 0; k < 4; k++) {
+      MCS_HIP_CHECK(hipMemcpy(v.data(), src[k], 4 * (size_t)nitem, hipMemcpyDeviceToHost));
+      for (int i = 0; i < nitem; i++) bad += v[i] != (*ref[k])[i];
+    }
+  }
+  return (int)std::min<int64_t>(bad, INT32_MAX);
+}
+
+int mcs_ba_read_host_timing(mcs_ba_ctx* c, double* ms, int32_t* n_calls, int32_t reset) {
+  if (!c) return MCS_ERR_ARG;
+  for (int k = 0; k < MCS_BA_NHOST; k++) if (ms) ms[k] = c->host_ms[k];
+  if (n_calls) *n_calls = c->host_calls;
+  if (reset) {
+    for (double& v : c->host_ms) v = 0.0;
+    c->host_calls = 0;
   }
   return MCS_OK;
 }
@@ -1447,14 +2064,26 @@ int mcs_local_ba_ex(mcs_ba_ctx* c, const mcs_ba_problem* p, const int32_t* point
     }
   };
   o.max_iterations = 10;
-  int rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r1);
+  // round 1 builds the structure and uploads the problem; round 2 (the same graph with the
+  // culled edges at level 1) reuses both (Optimizer::remask) unless a pose left the system
+  Optimizer opt(c, p, false);
+  int rc = opt.setup(poses, points, level.data(), nullptr);
+  if (rc) return rc;
+  rc = opt.run(&o, poses, points, chi.data(), sf, r1);
   if (rc) return rc;
   // optimize() returns -1 == OptimizationAlgorithm::Fail only for an empty active graph
   if (r1->n_active_poses + r1->n_active_points == 0) return MCS_OK;   // :784-788
   if (stop_flag && *stop_flag) return MCS_OK;               // bDoMore = false (:790-794)
-  cull(true);
+  {
+    HostClock hc;
+    cull(true);
+    hc.mark(c->host_ms, 4);
+  }
   o.max_iterations = 15;                                    // :819-820
-  rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r2);
+  rc = opt.remask(level.data());
+  if (rc < 0) return rc;
+  if (rc == 0) rc = opt.run(&o, poses, points, chi.data(), sf, r2);
+  else rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r2);
   if (rc) return rc;
   if (r2->n_active_poses + r2->n_active_points == 0) return MCS_OK;   // :822-826
   cull(false);

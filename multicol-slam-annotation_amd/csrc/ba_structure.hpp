@@ -1,0 +1,164 @@
+// Host side of one bundle-adjustment call: g2o's initializeOptimization(0) +
+// buildIndexMapping + BlockSolver<6,3>::buildStructure over the flat problem of
+// include/mcs_ba.h (the active set, the Hessian index of every vertex, CSR edge lists and the
+// edge pairs of every lower block of the Schur complement, cut into k_schur work items).
+// Host-only C++ (also compiled by tools/bench/structure_bench.cpp on the CPU).
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/mcs_ba.h"
+
+namespace mcs {
+namespace ba {
+
+constexpr int kSchurChunk = 128;   // pairs per k_schur wave (config C: 128 beat 32 / 64 / 256)
+
+// host-side structure of one optimize() call (build_structure); owned by the context so its
+// capacity is reused across that context's calls and released with it
+struct HostStruct {
+  std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
+      ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, it_nch;
+  std::vector<int32_t> pt_h;   // Hessian index of the pose of every pt_edges entry (-1: fixed)
+  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
+  int n_slots = 0;
+  int np = 0, nl = 0;
+};
+
+// SparseOptimizer::initializeOptimization(0) + buildIndexMapping + BlockSolver::buildStructure
+// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295): active edges (level 0), active
+// non-fixed poses in vertex order (pose_cnt: number of active edges per pose over ALL shards),
+// active points in vertex order, CSR lists point -> edges and pose -> edges and the lower pose
+// blocks of the Schur complement, by counting sorts in edge order (deterministic).  The block
+// pairs themselves: build_pairs_host / the device build.
+inline void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
+                            const std::vector<double>& pose_cnt, HostStruct& s) {
+  s.aedge.clear();
+  s.aedge.reserve(p.n_edges);
+  for (int e = 0; e < p.n_edges; e++)   // level 0 and not allVerticesFixed (:206-267)
+    if ((!level || level[e] == 0) && !(points_fixed && p.pose_fixed[p.edge_pose[e]])) s.aedge.push_back(e);
+  std::vector<char> lh(p.n_points, 0);
+  if (!points_fixed)
+    for (int e : s.aedge) lh[p.edge_point[e]] = 1;
+  s.pose_h.assign(p.n_poses, -1);
+  s.point_h.assign(p.n_points, -1);
+  s.hpose_vtx.clear(); s.hpt_vtx.clear();
+  s.np = s.nl = 0;
+  for (int i = 0; i < p.n_poses; i++)
+    if (pose_cnt[i] > 0 && !p.pose_fixed[i]) { s.pose_h[i] = s.np++; s.hpose_vtx.push_back(i); }
+  for (int i = 0; i < p.n_points; i++)
+    if (lh[i]) { s.point_h[i] = s.nl++; s.hpt_vtx.push_back(i); }
+  // CSR point -> edges, pose -> edges (counting sort, stable in edge order)
+  s.pt_ptr.assign(s.nl + 1, 0);
+  s.ps_ptr.assign(s.np + 1, 0);
+  for (int e : s.aedge) {
+    const int l = s.point_h[p.edge_point[e]];
+    if (l >= 0) s.pt_ptr[l + 1]++;
+    const int h = s.pose_h[p.edge_pose[e]];
+    if (h >= 0) s.ps_ptr[h + 1]++;
+  }
+  for (int l = 0; l < s.nl; l++) s.pt_ptr[l + 1] += s.pt_ptr[l];
+  for (int h = 0; h < s.np; h++) s.ps_ptr[h + 1] += s.ps_ptr[h];
+  s.pt_edges.assign(s.pt_ptr[s.nl], 0);
+  s.ps_edges.assign(s.ps_ptr[s.np], 0);
+  {
+    std::vector<int32_t> fp(s.pt_ptr.begin(), s.pt_ptr.end() - 1), fs(s.ps_ptr.begin(), s.ps_ptr.end() - 1);
+    for (int e : s.aedge) {
+      const int l = s.point_h[p.edge_point[e]];
+      if (l >= 0) s.pt_edges[fp[l]++] = e;
+      const int h = s.pose_h[p.edge_pose[e]];
+      if (h >= 0) s.ps_edges[fs[h]++] = e;
+    }
+  }
+  s.pt_h.resize(s.pt_edges.size());
+  for (size_t q = 0; q < s.pt_edges.size(); q++) s.pt_h[q] = s.pose_h[p.edge_pose[s.pt_edges[q]]];
+  // lower pose blocks (i >= j), block id i(i+1)/2 + j, and their edge pairs in
+  // (point, e1, e2) order
+  const size_t nblk = (size_t)s.np * (s.np + 1) / 2;
+  s.blk_i.resize(nblk); s.blk_j.resize(nblk);
+  for (int i = 0, b = 0; i < s.np; i++)
+    for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
+}
+
+// The edge pairs of every lower block in (point, e1, e2) order and the k_schur work items, on
+// the host.  The product builds both on the device (ba.hip, enqueue_pairs); this restatement
+// is the checker of that build (mcs_ba_check_structure) and the CPU timing reference
+// (tools/bench/structure_bench.cpp).
+inline void build_pairs_host(const mcs_ba_problem& p, HostStruct& s) {
+  const size_t nblk = (size_t)s.np * (s.np + 1) / 2;
+  s.pr_ptr.assign(nblk + 1, 0);
+  // Per point, its edges with an active pose, grouped by pose (stable, so edge order inside
+  // a group): the pairs of block (i1, i2), i2 <= i1, that a point contributes are then the
+  // product group(i1) x group(i2) in (e1, e2) order -- the order of the plain double loop over
+  // the point's edges, without visiting the pairs that fall above the diagonal.
+  std::vector<int32_t>& ge = s.tmp_e;   // grouped edges, point by point
+  std::vector<int32_t>& gr = s.tmp_g;   // groups: (pose, begin, end) triples
+  std::vector<int32_t>& gp = s.tmp_p;   // per point: first group (nl + 1 entries)
+  ge.clear(); gr.clear(); gp.assign(s.nl + 1, 0);
+  for (int l = 0; l < s.nl; l++) {
+    const size_t b0 = ge.size();
+    for (int a = s.pt_ptr[l]; a < s.pt_ptr[l + 1]; a++) {
+      const int e = s.pt_edges[a];
+      const int h = s.pose_h[p.edge_pose[e]];
+      if (h < 0) continue;
+      // insertion into (pose, edge order), stable
+      ge.push_back(e);
+      size_t q = ge.size() - 1;
+      while (q > b0 && s.pose_h[p.edge_pose[ge[q - 1]]] > h) { ge[q] = ge[q - 1]; q--; }
+      ge[q] = e;
+    }
+    for (size_t q = b0; q < ge.size();) {
+      const int h = s.pose_h[p.edge_pose[ge[q]]];
+      size_t r = q + 1;
+      while (r < ge.size() && s.pose_h[p.edge_pose[ge[r]]] == h) r++;
+      gr.push_back(h); gr.push_back((int32_t)q); gr.push_back((int32_t)r);
+      q = r;
+    }
+    gp[l + 1] = (int32_t)(gr.size() / 3);
+  }
+  auto for_blocks = [&](auto&& f) {   // f(block, group of i1, group of i2), point by point
+    for (int l = 0; l < s.nl; l++)
+      for (int gi = gp[l]; gi < gp[l + 1]; gi++) {
+        const int h1 = gr[3 * gi];
+        for (int gj = gp[l]; gj <= gi; gj++)
+          f((size_t)h1 * (h1 + 1) / 2 + gr[3 * gj], gi, gj);
+      }
+  };
+  for_blocks([&](size_t blk, int gi, int gj) {
+    s.pr_ptr[blk + 1] += (gr[3 * gi + 2] - gr[3 * gi + 1]) * (gr[3 * gj + 2] - gr[3 * gj + 1]);
+  });
+  for (size_t b = 0; b < nblk; b++) s.pr_ptr[b + 1] += s.pr_ptr[b];
+  s.pr_e1.assign(s.pr_ptr[nblk], 0);
+  s.pr_e2.assign(s.pr_ptr[nblk], 0);
+  std::vector<int32_t>& fill = s.tmp_f;
+  fill.assign(s.pr_ptr.begin(), s.pr_ptr.end() - 1);
+  for_blocks([&](size_t blk, int gi, int gj) {
+    int q = fill[blk];
+    for (int a = gr[3 * gi + 1]; a < gr[3 * gi + 2]; a++)
+      for (int b = gr[3 * gj + 1]; b < gr[3 * gj + 2]; b++, q++) {
+        s.pr_e1[q] = ge[a];
+        s.pr_e2[q] = ge[b];
+      }
+    fill[blk] = q;
+  });
+  // k_schur work items: chunks of kSchurChunk pairs (and, on diagonal blocks, pose edges)
+  s.it_blk.clear(); s.it_chunk.clear(); s.it_slot.clear(); s.it_nch.clear();
+  s.n_slots = 0;
+  for (size_t b = 0; b < nblk; b++) {
+    const int np_ = s.pr_ptr[b + 1] - s.pr_ptr[b];
+    int ne = 0;
+    if (s.blk_i[b] == s.blk_j[b]) ne = s.ps_ptr[s.blk_i[b] + 1] - s.ps_ptr[s.blk_i[b]];
+    const int nch = std::max(1, (std::max(np_, ne) + kSchurChunk - 1) / kSchurChunk);
+    for (int c = 0; c < nch; c++) {
+      s.it_blk.push_back((int32_t)b);
+      s.it_chunk.push_back(c);
+      s.it_slot.push_back(nch > 1 ? s.n_slots + c : -1);
+      s.it_nch.push_back(nch);
+    }
+    if (nch > 1) s.n_slots += nch;
+  }
+}
+
+}  // namespace ba
+}  // namespace mcs

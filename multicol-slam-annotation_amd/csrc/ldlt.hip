@@ -286,7 +286,9 @@ __device__ __forceinline__ double gemv_row(const double* M, const double* v) {
 
 __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* __restrict__ b,
                                                double* __restrict__ L, double* __restrict__ Linv,
-                                               double* __restrict__ z, int k, int* flag) {
+                                               double* __restrict__ z, int k, int* flag,
+                                               const int* skip) {
+  if (skip && *skip) return;
   extern __shared__ double sm[];
   double* sK = sm;               // A_kk -> L_kk (strict lower) + D (diagonal)
   double* sI = sK + TB * LS;     // Linv_kk
@@ -397,7 +399,9 @@ constexpr int kBwdNT = 1024;
 __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ L,
                                                      const double* __restrict__ Linv,
                                                      const double* __restrict__ z,
-                                                     double* __restrict__ x, int T) {
+                                                     double* __restrict__ x, int T,
+                                                     const int* skip) {
+  if (skip && *skip) return;
   extern __shared__ double sx[];   // 64 T: solved blocks of x
   __shared__ double part[16][TB];
   __shared__ double rk[TB];
@@ -438,7 +442,9 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
   }
 }
 
-__global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int T, double dv) {
+__global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int T, double dv,
+                      const int* skip) {
+  if (skip && *skip) return;
   const int Np = T * TB;
   const int r = n + blockIdx.x;   // one workgroup per padding row
   if (r >= Np) return;
@@ -455,7 +461,9 @@ __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int
 // k_backward's one step (whose empty off-diagonal sum is +0: r = z exactly), in the same
 // partial layout and summation order.
 __global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, const double* __restrict__ b,
-                                                double* __restrict__ x, int n, double dv, int* flag) {
+                                                double* __restrict__ x, int n, double dv, int* flag,
+                                                const int* skip) {
+  if (skip && *skip) return;
   extern __shared__ double sm[];
   double* sK = sm;               // A -> L (strict lower) + D (diagonal)
   double* sI = sK + TB * LS;     // Linv
@@ -522,17 +530,18 @@ hipError_t set_lds_limit(const void* fn, int bytes) {
 }
 
 hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
-                          hipStream_t st) {
+                          hipStream_t st, const int* skip) {
   hipError_t e = set_lds_limit((const void*)k_solve1, (int)kSolve1Lds);
   if (e != hipSuccess) return e;
   if (n < 1 || n > TB) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_solve1, dim3(1), dim3(256), kSolve1Lds, st, A, b, x, n, diag_value, flag);
+  hipLaunchKernelGGL(k_solve1, dim3(1), dim3(256), kSolve1Lds, st, A, b, x, n, diag_value, flag, skip);
   return hipGetLastError();
 }
 
 constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
 
-hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st) {
+hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st,
+                 const int* skip) {
   hipError_t e = set_lds_limit((const void*)k_panel, (int)kPanelLds);
   if (e == hipSuccess) e = set_lds_limit((const void*)k_backward, 96 * 1024);
   if (e != hipSuccess) return e;
@@ -540,17 +549,17 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
   for (int k = 0; k < T; k++) {
     const int m = T - 1 - k;
     const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, flag);
+    hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, flag, skip);
   }
   hipLaunchKernelGGL(k_backward, dim3(1), dim3(kBwdNT), (size_t)T * TB * sizeof(double), st,
-                     (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T);
+                     (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T, skip);
   return hipGetLastError();
 }
 
-hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st) {
+hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st, const int* skip) {
   const int np = T * TB - n;
   if (np <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pad, dim3(np), dim3(256), 0, st, A, b, n, T, diag_value);
+  hipLaunchKernelGGL(k_pad, dim3(np), dim3(256), 0, st, A, b, n, T, diag_value, skip);
   return hipGetLastError();
 }
 

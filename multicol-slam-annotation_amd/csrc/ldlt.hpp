@@ -35,14 +35,18 @@ struct Work {
 
 // A: tiles (destroyed), b: 64 T (destroyed), x: 64 T (out).  *flag (device) = 1 on an
 // exact zero pivot, else left untouched (callers clear it).  All launches on st.
-hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st);
+// skip (nullable, device): every kernel returns at once when *skip != 0 (a device-driven
+// optimisation loop that has ended, ba.hip).
+hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st,
+                 const int* skip = nullptr);
 
 // Padding rows/columns [n, 64T): diagonal = diag_value, rest 0; b[n..64T) = 0.
-hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st);
+hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_t st,
+               const int* skip = nullptr);
 // pad + solve of a one-tile system (n <= 64) in one launch, bitwise equal to pad + solve
 // (diag_value: the padding diagonal after any exchange, i.e. 1)
 hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
-                          hipStream_t st);
+                          hipStream_t st, const int* skip = nullptr);
 
 }  // namespace ldlt
 }  // namespace mcs

@@ -746,5 +746,18 @@ def _solver_read_timing(self, reset=True):
     return dict(zip(BA_STAGES, ms.tolist())), it.value, tr.value, n.value
 
 
+BA_HOST_PHASES = ("checks", "structure", "upload", "download", "lba_bookkeeping")
+
+
+def _solver_read_host_timing(self, reset=True):
+    """-> (dict host phase -> accumulated ms, optimize calls) (mcs_ba_read_host_timing)."""
+    from . import _check
+    ms = np.zeros(len(BA_HOST_PHASES))
+    n = ctypes.c_int32()
+    _check(self._lib.mcs_ba_read_host_timing(self._h, _p(ms), ctypes.byref(n), 1 if reset else 0))
+    return dict(zip(BA_HOST_PHASES, ms.tolist())), n.value
+
+
+Solver.read_host_timing = _solver_read_host_timing
 Solver.enable_timing = _solver_enable_timing
 Solver.read_timing = _solver_read_timing

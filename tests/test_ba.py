@@ -161,3 +161,30 @@ def test_gpu_stop_flag_semantics(gpu, small_problem):
     r = S.optimize(pr, stop_flag=0)
     o = ob.ba_optimize(pr, stop_flag=0)
     assert r["stop_flag"] == o["stop_flag"] and r["report"].iterations == o["report"].iterations
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["configC", "culled", "duplicate_groups", "small"])
+def test_gpu_device_schur_structure_matches_host(gpu, case, problem, small_problem):
+    """The Schur pair lists and k_schur work items the product builds on the device are
+    entry-for-entry those of the host restatement of BlockSolver::buildStructure
+    (block_solver.hpp:143-295 via ba_structure.hpp build_pairs_host): block pointers, every
+    (e1, e2) pair in (point, e1, e2) order inside its block, every work item."""
+    import ctypes
+    from mcs_amd import ba, lib
+    pr = dict(small_problem if case == "small" else problem)
+    level = None
+    if case == "culled":   # LocalBA round 2: some edges at level 1
+        rng = np.random.default_rng(3)
+        level = (rng.random(len(pr["edge_pose"])) < 0.1).astype(np.uint8)
+    if case == "duplicate_groups":   # a point observed twice by one pose (multi-edge groups)
+        k = 40
+        for key in ("edge_pose", "edge_point", "edge_cam"):
+            pr[key] = np.concatenate([pr[key], pr[key][:k]])
+        pr["edge_meas"] = np.concatenate([pr["edge_meas"], pr["edge_meas"][:k] + 0.5])
+        pr["edge_info"] = np.concatenate([pr["edge_info"], pr["edge_info"][:k]])
+    s = ba.as_struct(pr)
+    solver = ba.Solver()
+    lv = None if level is None else level.ctypes.data_as(ctypes.c_void_p)
+    bad = lib().mcs_ba_check_structure(solver._h, ctypes.byref(s), lv)
+    assert bad == 0, bad

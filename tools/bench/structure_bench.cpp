@@ -1,0 +1,44 @@
+// CPU timing of the BA host structure build (ba_structure.hpp) on a dumped problem:
+//   python tools/bench/dump_problem.py /tmp/cfgc && g++ -O3 -std=c++17 \
+//     tools/bench/structure_bench.cpp -o /tmp/sb && /tmp/sb /tmp/cfgc
+#include <chrono>
+#include <cstdio>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "../../multicol-slam-annotation_amd/csrc/ba_structure.hpp"
+
+template <typename T>
+std::vector<T> load(const std::string& f) {
+  std::ifstream in(f, std::ios::binary | std::ios::ate);
+  const size_t n = (size_t)in.tellg() / sizeof(T);
+  in.seekg(0);
+  std::vector<T> v(n);
+  in.read(reinterpret_cast<char*>(v.data()), n * sizeof(T));
+  return v;
+}
+
+int main(int argc, char** argv) {
+  const std::string d = argc > 1 ? argv[1] : "/tmp/cfgc";
+  auto ep = load<int32_t>(d + "/edge_pose.bin"), el = load<int32_t>(d + "/edge_point.bin");
+  auto pf = load<uint8_t>(d + "/pose_fixed.bin");
+  auto np = load<int32_t>(d + "/sizes.bin");
+  mcs_ba_problem p{};
+  p.n_poses = np[0]; p.n_points = np[1]; p.n_edges = (int)ep.size(); p.n_cams = 3;
+  p.edge_pose = ep.data(); p.edge_point = el.data(); p.pose_fixed = pf.data();
+  mcs::ba::HostStruct s;
+  double best = 1e9;
+  for (int r = 0; r < 50; r++) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<double> cnt(p.n_poses + 2, 0.0);
+    for (int e = 0; e < p.n_edges; e++) cnt[p.edge_pose[e]] += 1.0;
+    mcs::ba::build_structure(p, nullptr, false, cnt, s);
+    mcs::ba::build_pairs_host(p, s);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    best = std::min(best, ms);
+  }
+  std::printf("edges %d points %d poses %d: np %d nl %d pairs %zu items %zu  build %.3f ms (best of 50)\n",
+              p.n_edges, p.n_points, p.n_poses, s.np, s.nl, s.pr_e1.size(), s.it_blk.size(), best);
+  return 0;
+}
