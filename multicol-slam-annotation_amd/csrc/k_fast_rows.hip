@@ -62,6 +62,19 @@ __device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
 __device__ __forceinline__ int fr_max3(int a, int b, int c) { return max(max(a, b), c); }
 }  // namespace
 
+// Tuning probe (tools/gpu/fast_probe.py, variant builds with -DMCS_FAST_PROBE only): shader
+// cycles per phase summed over all waves: [0] band loads + ring writes, [1] compass + list,
+// [2] exact test + score, [3] NMS + mask + append, [4] whole wave, [5] bands, [6] survivors,
+// [7] corners.
+#ifdef MCS_FAST_PROBE
+__device__ unsigned long long g_fast_probe[8];
+#define FP_T(v) const long long v = __builtin_amdgcn_s_memtime()
+#define FP_ADD(k, v) (acc_[k] += (unsigned long long)(v))
+#else
+#define FP_T(v) do { } while (0)
+#define FP_ADD(k, v) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   __shared__ __attribute__((aligned(4096))) uint8_t lds[kLdsBytes];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -79,6 +92,10 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   const int ui = item * 4 + wv;
   if (ui >= a.nunits) return;
   const FastUnit u = a.units[ui];
+#ifdef MCS_FAST_PROBE
+  unsigned long long acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long t_begin_ = __builtin_amdgcn_s_memtime();
+#endif
   const int level = u.level, nc = u.ncells, wh = u.wy1 - u.wy0;
   int32_t* const cnt_out = a.cell_counts + (int64_t)f * a.ncells + u.cell0;
   if (wh <= 0) {
@@ -157,6 +174,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   const int nbands = (wh + kBand - 1) / kBand;
   int ncarry = 0;   // corners of the previous band's last row, at the front of the list
   for (int b = 0; b < nbands; b++) {
+    FP_T(t0_);
     const int y0 = 3 + b * kBand, y1 = min(y0 + kBand, 3 + wh);
     // rows y0 + 3 .. y0 + kBand + 2 arrive; the next band's rows go in flight
     uint32_t rows[6 + kBand];
@@ -201,6 +219,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       }
     }
 
+    FP_T(t1_);
+    FP_ADD(0, t1_ - t0_);
+    FP_ADD(5, 1);
     // ---- A: compass pre-test from the register window, 4 pixels per lane: a 9-long arc of the
     // 16-circle always holds two ADJACENT compass points (0/4/8/12), so a corner needs
     // (D0|D8)&(D4|D12) or (B0|B8)&(B4|B12) (D = darker than v-t, B = brighter than v+t), tested
@@ -241,6 +262,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       list[k3 ? pos3 : kListCap] = (uint16_t)(idx + 3);
     }
     dev::wave_sync();
+    FP_T(t2_);
+    FP_ADD(1, t2_ - t1_);
+    FP_ADD(6, ns);
 
     // ---- B: exact FAST test + score of the survivors, two per lane (batch j0: survivors
     // j0 + lane and j0 + 64 + lane in the low / high halves).  With d_k = v - p_k, cornerScore's
@@ -312,6 +336,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       nlast += __popcll(__ballot(ca && (ea >> 8) == y1 - 1)) + __popcll(__ballot(cb && (eb >> 8) == y1 - 1));
     }
     dev::wave_sync();
+    FP_T(t3_);
+    FP_ADD(2, t3_ - t2_);
+    FP_ADD(7, ncorn - ncarry);
 
     // ---- C: NMS (3x3 within the cell) + runByPixelsMask + append to the cell's slots
     const bool last_band = b + 1 == nbands;
@@ -376,9 +403,27 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       ncarry = nlast;
     }
     dev::wave_sync();
+    FP_T(t4_);
+    FP_ADD(3, t4_ - t3_);
   }
   if (lane < nc) cnt_out[lane] = cnt;
+#ifdef MCS_FAST_PROBE
+  acc_[4] += (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin_);
+  if (lane == 0)
+    for (int k = 0; k < 8; k++) atomicAdd(&g_fast_probe[k], acc_[k]);
+#endif
 }
+
+#ifdef MCS_FAST_PROBE
+extern "C" int mcs_debug_fast_probe(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_probe), sizeof(g_fast_probe)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_fast_probe), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 void launch_fast_rows(const FastRowArgs& a_in, hipStream_t st) {
   FastRowArgs a = a_in;

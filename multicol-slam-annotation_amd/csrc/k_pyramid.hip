@@ -134,18 +134,24 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
   // (row -1 = row 1, row -2 = row 2, row dh = row dh-2, row dh+1 = row dh-3)
   auto emit = [&](int y, int r) {
     (void)r;
-    // window weights (wave-uniform, 4 bits each, row r-4 first)
-    const uint32_t wts = (y >= 2 && y + 2 <= dh - 1) ? 0x11111u     // interior
-                       : y == 0 ? 0x22100u                            // rows 2 1 0 1 2
-                       : y == 1 ? 0x11210u                            // rows 1 0 1 2 3
-                       : y == dh - 2 ? 0x12110u                       // rows dh-4..dh-1, dh-2
-                       : 0x12200u;                                    // dh-3 dh-2 dh-1 dh-2 dh-3
-    uint32_t s01 = 0, s23 = 0;
+    uint32_t s01, s23;
+    if (y >= 2 && y + 2 <= dh - 1) {   // interior row (wave-uniform): plain 5-row sum
+      s01 = (win[0][0] + win[1][0] + win[2][0]) + (win[3][0] + win[4][0]);
+      s23 = (win[0][1] + win[1][1] + win[2][1]) + (win[3][1] + win[4][1]);
+    } else {
+      // the two top / bottom rows: window weights (2 bits each, row r-4 first) fold the
+      // mirrored rows in; weight * sum by selects and a shift (no 32-bit multiply)
+      const uint32_t wts = y == 0 ? 0x22100u                          // rows 2 1 0 1 2
+                         : y == 1 ? 0x11210u                          // rows 1 0 1 2 3
+                         : y == dh - 2 ? 0x12110u                     // rows dh-4..dh-1, dh-2
+                         : 0x12200u;                                  // dh-3 dh-2 dh-1 dh-2 dh-3
+      s01 = 0; s23 = 0;
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const uint32_t wi = (wts >> (4 * i)) & 15u;
-      s01 += wi * win[i][0];
-      s23 += wi * win[i][1];
+      for (int i = 0; i < 5; i++) {
+        const uint32_t wi = (wts >> (4 * i)) & 15u;   // 0, 1 or 2
+        s01 += (wi & 1u ? win[i][0] : 0u) + (wi & 2u ? win[i][0] << 1 : 0u);
+        s23 += (wi & 1u ? win[i][1] : 0u) + (wi & 2u ? win[i][1] << 1 : 0u);
+      }
     }
     if (core_lane) {
       const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |

@@ -132,6 +132,8 @@ SIGNATURES = {
     "mcs_ba_read_timing": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32]),
     "mcs_ba_read_host_timing": (ctypes.c_int, [_P, _P, _P, _I32]),
     "mcs_ba_check_structure": (ctypes.c_int, [_P, _P, _P]),
+    "mcs_distinctive_descriptors_device": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P, _P, _P, _P]),
+    "mcs_update_normal_depth_device": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "mcs_pose_optimization": (ctypes.c_int, [_P] * 8),
     "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
     "mcs_search_for_triangulation_raw_masked": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),

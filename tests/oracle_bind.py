@@ -43,6 +43,8 @@ _SIGS = {
     "oracle_search_for_triangulation_raw_ex": (_I, [_P, _P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _D, _I, _P]),
     "oracle_check_dist_epipolar_line": (_I, [_P, _P, _P, _D, _P]),
     "oracle_compute_e_rig": (_I, [_P, _P, _P, _I, _P]),
+    "oracle_distinctive_descriptors": (_I, [_P, _P, _I, _P, _P, _I, _P]),
+    "oracle_update_normal_depth": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "oracle_frame_grid": (_I, [_I, _P, _P, _P, _I, _P, _P]),
     "oracle_window_candidates": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I]),
     # DBoW2 vocabulary oracle
