@@ -72,6 +72,40 @@ def alg_bytes_pyr_fast(level_wh):
     return sum(px[l - 1] + px[l] for l in range(1, len(px))) + sum(px)
 
 
+def baseline_cpus(k):
+    """The first k CPUs of this process's allowed set: the CPU baseline legs pin their threads
+    to them (taskset-style, one thread per CPU) so the timing does not migrate across cores."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return []
+    return cpus[:k]
+
+
+class pinned_thread:
+    """Pin the calling thread to one CPU while a single-threaded baseline leg runs; the
+    thread's previous CPU set is restored afterwards."""
+
+    def __init__(self, cpu):
+        self.cpu = cpu
+
+    def __enter__(self):
+        self.old = None
+        if self.cpu is not None and hasattr(os, "sched_setaffinity"):
+            self.old = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, {self.cpu})
+        return self
+
+    def __exit__(self, *exc):
+        if self.old is not None:
+            os.sched_setaffinity(0, self.old)
+        return False
+
+
+def pin_note(cpus):
+    return "threads pinned one per CPU to %s (sched_setaffinity)" % (cpus,) if cpus else "unpinned"
+
+
 def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     """Oracle (CPU restatement) on a bounded sample: one thread per camera, like the
     reference's `#pragma omp parallel for num_threads(nrCams)` (src/cMultiFrame.cpp:128);
@@ -83,9 +117,12 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     descs = [[None] * ncams for _ in range(n_multiframes)]
     top2 = [[None] * ncams for _ in range(n_multiframes - 1)]
     lock = threading.Lock()
+    cpus = baseline_cpus(ncams)
 
     def work(c):
         nonlocal nkp
+        if len(cpus) == ncams:   # fresh thread: pinned for its whole life
+            os.sched_setaffinity(0, {cpus[c]})
         for t in range(n_multiframes):
             k, d = ob.extract(imgs[t * ncams + c], masks[c], nfeatures=nfeatures)
             kpss[t][c] = k
@@ -103,7 +140,8 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     for th in ths:
         th.join()
     dt = time.perf_counter() - t0
-    sample = "%d multi-frames x %d cams (extract+match), oracle restatement" % (n_multiframes, ncams)
+    sample = "%d multi-frames x %d cams (extract+match), oracle restatement; %s" % (
+        n_multiframes, ncams, pin_note(cpus if len(cpus) == ncams else []))
     return nkp / dt / 1e3, sample, ncams, (kpss, descs, top2)
 
 
@@ -247,12 +285,15 @@ def run_global_ba(args, rank, world, local_rank, dev):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from tests import oracle_bind as ob
         o = mba.BAOptions(max_iterations=1, terminate_max_iter=15)
-        t0 = time.perf_counter()
-        rr = ob.ba_optimize(pr, options=o)
-        tc = time.perf_counter() - t0
+        cpus = baseline_cpus(1)
+        with pinned_thread(cpus[0] if cpus else None):
+            t0 = time.perf_counter()
+            rr = ob.ba_optimize(pr, options=o)
+            tc = time.perf_counter() - t0
         cpu = {"value": round(rr["report"].iterations / tc, 4), "unit": "GlobalBA iters/s",
                "cores": 1, "kind": "port",
-               "sample": "1 LM iteration of config E (oracle restatement, dense LDL^T, single thread)"}
+               "sample": "1 LM iteration of config E (oracle restatement, dense LDL^T, single "
+                         "thread); " + pin_note(cpus)}
     return out, cpu
 
 
@@ -379,12 +420,15 @@ def run_bow(args, rank, world, dev, stream, d_desc, n_valid):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from tests import oracle_bind as ob
         sample = flat[: min(n, 200000)].cpu().numpy()
-        t0 = time.perf_counter()
-        ob.vocab_words(v, sample, 4)
-        tc = time.perf_counter() - t0
+        cpus = baseline_cpus(1)
+        with pinned_thread(cpus[0] if cpus else None):
+            t0 = time.perf_counter()
+            ob.vocab_words(v, sample, 4)
+            tc = time.perf_counter() - t0
         cpu = {"value": round(len(sample) / tc, 1), "unit": "descriptors/s", "cores": 1,
                "kind": "port", "sample": "%d descriptor slots of the step, oracle restatement "
-                                         "(vocabulary build included)" % len(sample)}
+                                         "(vocabulary build included); %s" % (
+                                             len(sample), pin_note(cpus))}
     return out, cpu
 
 
@@ -437,7 +481,8 @@ def selftest_dist(rank, world):
     assert torch.equal(g, want), g
     xch = mba.TorchExchange(10, dev)
     xch.buf.fill_(float(rank + 1))
-    assert xch._allreduce(None, 0, 0, 60) == 0
+    assert xch.shard.stream_ordered == 0     # CPU buffer: synchronous reduction
+    assert xch._allreduce(None, 0, 0, 60, None) == 0
     assert float(xch.buf[0]) == world * (world + 1) / 2
     if rank == 0:
         print(json.dumps({"selftest": "ok", "n_gpus": world, "ms_per_step": dt * 1e3,
@@ -603,12 +648,15 @@ def main():
                        len(pr["edge_pose"]))}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             from tests import oracle_bind as ob
-            t0 = time.perf_counter()
-            o = ob.local_ba(pr)
-            tc = time.perf_counter() - t0
+            cpus = baseline_cpus(1)
+            with pinned_thread(cpus[0] if cpus else None):
+                t0 = time.perf_counter()
+                o = ob.local_ba(pr)
+                tc = time.perf_counter() - t0
             cpu_ba = {"value": round((o["report1"].iterations + o["report2"].iterations) / tc, 2),
                       "unit": "LocalBA iters/s", "cores": 1, "kind": "port",
-                      "sample": "1 LocalBA call (config C), oracle restatement, single thread"}
+                      "sample": "1 LocalBA call (config C), oracle restatement, single thread; " +
+                                pin_note(cpus)}
 
     bow, cpu_bow = run_bow(args, rank, world, dev, stream, d_desc, kp_per_step)
     gba, cpu_gba = run_global_ba(args, rank, world, local_rank, dev)

@@ -187,17 +187,27 @@ int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double
  * three scalars, so every rank takes the same LM decisions (lock step).
  *
  * The library never talks to the interconnect itself: `allreduce` (e.g. torch.distributed /
- * RCCL on the caller's side) reduces xchg[offset, offset + count) in place across ranks and
- * returns 0 when done.  The library synchronises its stream before every call and reads the
- * buffer only after the callback returned. */
+ * RCCL on the caller's side) reduces xchg[offset, offset + count) in place across ranks.  It is
+ * called with the library's stream (hipStream_t) and returns 0 on success:
+ *   stream_ordered == 0: the library synchronises its stream before every call and reads the
+ *       buffer only after the callback returned (the callback completes the reduction);
+ *   stream_ordered != 0: the library does NOT synchronise; the callback enqueues the
+ *       reduction so that it starts after all work already on `stream` and completes before
+ *       any work enqueued on `stream` after the call (RCCL on that stream, or a side stream
+ *       joined by events) and may return before it has run.  The per-iteration exchanges of
+ *       the reduced camera system then cost no host round trip; the LM-control scalars are
+ *       reduced on the device too and read back once per trial.
+ * Every rank issues the same sequence of calls (same offsets and counts). */
 enum { MCS_REDUCE_SUM = 0, MCS_REDUCE_MAX = 1 };
-typedef int32_t (*mcs_ba_allreduce_fn)(void* user, int32_t op, int64_t offset, int64_t count);
+typedef int32_t (*mcs_ba_allreduce_fn)(void* user, int32_t op, int64_t offset, int64_t count,
+                                       void* stream);
 typedef struct mcs_ba_shard {
   int32_t rank, world;
   double* xchg;                  /* device buffer of >= mcs_ba_xchg_doubles(n_poses) doubles */
   int64_t xchg_cap;              /* its size in doubles */
   mcs_ba_allreduce_fn allreduce;
   void* user;
+  int32_t stream_ordered;        /* see above */
 } mcs_ba_shard;
 
 /* Exchange-buffer size (doubles) for problems with up to n_poses pose vertices. */
@@ -217,7 +227,8 @@ int mcs_global_ba(mcs_ba_ctx* c, const mcs_ba_problem* p, int32_t pose_only, dou
                   const mcs_ba_shard* shard);
 
 /* Stage timing (device time from HIP events on the context's stream; the exchange stage is
- * host wall time around the allreduce callback).  Stages: 0 linearize (errors, Jacobians,
+ * the stream time of the reduced-system all-reduce when the shard is stream_ordered, else the
+ * host wall time around the callback).  Stages: 0 linearize (errors, Jacobians,
  * Hpp / Hll / b), 1 Schur (Hll^-1, Y = Hpl Hll^-1, reduced camera system), 2 exchange
  * (all-reduce of the reduced system, sharded runs only), 3 dense LDL^T solve, 4 update
  * (back-substitution, oplus, chi2).  ms[] accumulates over calls until read with reset. */

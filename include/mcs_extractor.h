@@ -39,7 +39,8 @@ typedef struct mcs_extractor_params {
   int32_t patch_size;      /* 32 (unused) */
   int32_t fast_threshold;  /* 20 (5 for the initialisation extractor) */
   int32_t use_agast;       /* must be 0 (AGAST: MCS_ERR_UNSUPPORTED) */
-  int32_t fast_agast_type; /* must be 2 == TYPE_9_16 */
+  int32_t fast_agast_type; /* FastFeatureDetector type: 2 TYPE_9_16 (default), 1 TYPE_7_12,
+                              0 TYPE_5_8 (mdBRIEFextractorOct.cpp:871-872, 916-917) */
   int32_t do_dbrief;       /* 1 = dBRIEF (needs mcs_extractor_set_cam_models) */
   int32_t learn_masks;     /* 1 = mdBRIEF: 3 rotated patterns -> descriptor + stability mask
                               (src/mdBRIEFextractorOct.cpp:410-554; needs camera models) */

@@ -259,6 +259,7 @@ struct Dev {
   // system
   double* Hpp; double* bp; double* Hll; double* bl; double* Dinv; double* db;
   double* S; double* bs; double* xp;   // S: lower 64x64 tiles (ldlt.hpp), bs / xp: 64 T
+  int T;                               // tiles per side of S
   double* hdiag; double* bpf;          // [6 np] Hpp diagonal and b_p (all-reduced when sharded)
   double* red;                         // reduction scratch
   // trial bookkeeping folded into k_point_trial (each was a 4-5 us copy / fill launch)
@@ -749,7 +750,7 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
     if (bi == bj && c > a) return;   // lower triangle of the diagonal block only
     double s0 = 0.0;
     if (bi == bj) { s0 = d.Hpp[36 * bi + 6 * a + c]; if (a == c) s0 += lam0; }
-    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c)] = s0 - v;
+    d.S[ldlt::sidx(6 * bi + a, 6 * bj + c, d.T)] = s0 - v;
   } else if (lane < 42 && bi == bj) {
     const int a = lane - 36;
     d.bs[6 * bi + a] = d.bp[6 * bi + a] - v;
@@ -1174,14 +1175,16 @@ struct Packer {
 
 unsigned gb(int n) { return (unsigned)std::max(1, (n + 255) / 256); }
 
-// Exchange-buffer layout (offsets in doubles) for T tiles and np active poses; the head of
-// the buffer is reused for the structure exchange (pose activity counts) before T is known.
+// Exchange-buffer layout (offsets in doubles) for T tiles and np active poses: [bs | S tiles |
+// hdiag | bpf | scalars]; bs first so that bs and the leading (non-zero) diagonals of S are one
+// range.  The head of the buffer is reused for the structure exchange (pose activity counts)
+// before T is known.
 struct XLayout {
   size_t S, bs, hdiag, bpf, sc, total;
   XLayout(int T, int np) {
-    S = 0;
-    bs = ldlt::tile_doubles(T);
-    hdiag = bs + (size_t)ldlt::TB * T;
+    bs = 0;
+    S = (size_t)ldlt::TB * T;
+    hdiag = S + ldlt::tile_doubles(T);
     bpf = hdiag + 6 * (size_t)np;
     sc = bpf + 6 * (size_t)np;
     total = sc + 16;
@@ -1199,6 +1202,7 @@ struct Shard {
   double* xchg = nullptr;
   mcs_ba_allreduce_fn fn = nullptr;
   void* user = nullptr;
+  bool ordered = false;   // stream_ordered: the callback enqueues on st, no host drain
 };
 
 // One optimize() call split in two so that LocalBA's second round can reuse the first
@@ -1231,6 +1235,7 @@ struct Optimizer {
   int32_t* it_nch_dev = nullptr;   // chunks of each item's block (checked by the test hook)
   int nblk = 0;
   XLayout X{1, 0};
+  size_t xs_count = 0;   // doubles of the per-trial exchange: bs + the non-zero diagonals of S
   int nl_glob = 0, nae_glob = 0;
   double *d_poses = nullptr, *d_points = nullptr, *d_scalar = nullptr, *d_part = nullptr;
   int* d_flag = nullptr;
@@ -1247,16 +1252,18 @@ struct Optimizer {
     if (!q) he = hipErrorOutOfMemory;
     return q;
   }
-  // collective over xchg[off, off+cnt) (stream drained first); no-op on one rank
+  // collective over xchg[off, off+cnt); no-op on one rank.  Stream-ordered shards get it
+  // enqueued on st behind the producing kernels; otherwise the stream is drained first and the
+  // callback completes it (its host time is the exchange stage).
   int allreduce(int op, size_t off, size_t cnt) {
     if (!sharded || cnt == 0) return MCS_OK;
-    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    if (!sh.ordered) MCS_HIP_CHECK(hipStreamSynchronize(st));
     const auto t0 = std::chrono::steady_clock::now();
-    if (sh.fn(sh.user, op, (int64_t)off, (int64_t)cnt) != 0) {
+    if (sh.fn(sh.user, op, (int64_t)off, (int64_t)cnt, (void*)st) != 0) {
       set_error("BA: allreduce callback failed");
       return MCS_ERR_HIP;
     }
-    if (c->timing)
+    if (c->timing && !sh.ordered)
       c->acc_ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MCS_OK;
   }
@@ -1292,6 +1299,7 @@ struct Optimizer {
       }
       sh.rank = shard_in->rank; sh.world = shard_in->world; sh.xchg = shard_in->xchg;
       sh.fn = shard_in->allreduce; sh.user = shard_in->user;
+      sh.ordered = shard_in->stream_ordered != 0;
     }
     sharded = sh.world > 1;
     st = c->st;
@@ -1330,6 +1338,24 @@ struct Optimizer {
       return MCS_ERR_UNSUPPORTED;
     }
     X = XLayout(T, s.np);
+    xs_count = X.hdiag - X.bs;
+    if (sharded && T > 1) {
+      // Tiles of S below the widest tile diagonal any rank's points touch are zero on every
+      // rank (their blocks have no pairs; the padding rows there are zero too), so the
+      // exchange stops at that diagonal: bs + diagonals 0 .. w of the diagonal-major tiles.
+      int w = 1;   // diagonal pose blocks straddling a tile boundary reach diagonal 1
+      for (int q = 0; q < s.nl; q++) {
+        int lo = INT32_MAX, hi = -1;
+        for (int e = s.pt_ptr[q]; e < s.pt_ptr[q + 1]; e++) {
+          const int h = s.pt_h[e];
+          if (h >= 0) { lo = std::min(lo, h); hi = std::max(hi, h); }
+        }
+        if (hi >= 0) w = std::max(w, (6 * hi + 5) / ldlt::TB - (6 * lo) / ldlt::TB);
+      }
+      double wd = w;
+      if ((rc = allreduce_host(&wd, 1, MCS_REDUCE_MAX, X.sc))) return rc;
+      xs_count = (size_t)ldlt::TB * T + ldlt::band_tiles((int)wd + 1, T) * ldlt::TB * ldlt::TB;
+    }
     NE = p->n_edges;
     double *d_poses_bk = nullptr, *d_points_bk = nullptr;
     {
@@ -1365,6 +1391,7 @@ struct Optimizer {
     d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
     d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
     d.S = sh.xchg + X.S; d.bs = sh.xchg + X.bs; d.hdiag = sh.xchg + X.hdiag; d.bpf = sh.xchg + X.bpf;
+    d.T = T;
     d.xp = dz((size_t)ldlt::TB * T);
     d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
     // bounds of the device-built pair lists / items: a point with k active edges gives at most
@@ -1393,7 +1420,7 @@ struct Optimizer {
     d.n_pose_dbl = 6 * p->n_poses; d.n_point_dbl = 3 * p->n_points;
     d.flag = d_flag;
     g_state = gb(std::max(d.n_pose_dbl, d.n_point_dbl));
-    sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
+    sig_path = !sharded && d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
     const int rp = enqueue_pairs();
     hc.mark(c->host_ms, 2);
     return rp;
@@ -1508,7 +1535,7 @@ struct Optimizer {
     s.aedge.swap(keep);
     nae_glob = d.nae;
     nl_glob = nl_left;
-    sig_path = d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
+    sig_path = !sharded && d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
     hc.mark(c->host_ms, 4);
     return MCS_OK;
   }
@@ -1547,7 +1574,7 @@ struct Optimizer {
       return MCS_OK;
     };
     // one LM trial (push, Schur, solve, update, chi2), enqueued on st; lambda in d (by value)
-    auto enqueue_trial = [&]() -> int {
+    auto enqueue_trial = [&](bool stop_now) -> int {
       int rc2;
       rec(2);
       // also pushes the state (poses / points -> backups) and resets the solve flag
@@ -1558,7 +1585,7 @@ struct Optimizer {
         // one tile (LocalBA): the padding is applied inside the fused solve, after the exchange
         if (T > 1) MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, sh.rank == 0 ? 1.0 : 0.0, st));
         rec(3);
-        if ((rc2 = allreduce(MCS_REDUCE_SUM, X.S, X.hdiag - X.S))) return rc2;   // S tiles | bs
+        if ((rc2 = allreduce(MCS_REDUCE_SUM, X.bs, xs_count))) return rc2;   // bs | S band
         rec(4);
         if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st));
         else MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st));
@@ -1571,6 +1598,20 @@ struct Optimizer {
       if (sig_path) {
         Sum3 q{{d.rchi, d.red, d.red + s.nl}, {d.nae, s.nl, s.np}};
         hipLaunchKernelGGL(k_reduce3, dim3(3), dim3(1024), 0, st, q, (const int*)d_flag, c->sig, ++c->sig_seq);
+      } else if (sharded) {
+        // chi2 and the points' model decrease are partial sums: reduce them straight into the
+        // exchange buffer next to the stop flag, all-reduce them there and read back once
+        // (pinned[0..2] = the summed {chi2, points' decrease, stop}; pinned[3] = the poses'
+        // decrease, replicated; pinned[5] = the solve flag, identical on every rank)
+        reduce_dev<false>(d.rchi, d.nae, sh.xchg + X.sc, d_part, st);
+        reduce_dev<false>(d.red, s.nl, sh.xchg + X.sc + 1, d_part, st);
+        reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
+        c->pinned[7] = stop_now ? 1.0 : 0.0;
+        MCS_HIP_CHECK(hipMemcpyAsync(sh.xchg + X.sc + 2, c->pinned + 7, 8, hipMemcpyHostToDevice, st));
+        if ((rc2 = allreduce(MCS_REDUCE_SUM, X.sc, 3))) return rc2;
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned, sh.xchg + X.sc, 24, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 3, d_scalar + 2, 8, hipMemcpyDeviceToHost, st));
+        MCS_HIP_CHECK(hipMemcpyAsync(c->pinned + 5, d_scalar + 5, 8, hipMemcpyDeviceToHost, st));
       } else {
         reduce_dev<false>(d.red, s.nl, d_scalar + 1, d_part, st);
         reduce_dev<false>(d.red + s.nl, s.np, d_scalar + 2, d_part, st);
@@ -1652,21 +1693,22 @@ struct Optimizer {
           // (replayed per trial) measured no faster than these direct launches
           d.lam = lambda;
           d.lam0 = sh.rank == 0 ? lambda : 0.0;
-          if ((rc = enqueue_trial())) return rc;
+          if ((rc = enqueue_trial(*stop != 0))) return rc;
           int fl;   // identical on every rank (same reduced system)
           if ((rc = wait_trial(&fl))) return rc;
           if (c->timing) {
             if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
+            if (sh.ordered) c->acc_ms[2] += ms(3, 4);
             c->acc_ms[1] += ms(2, 3);
             c->acc_ms[3] += ms(4, 5);
             c->acc_ms[4] += ms(5, 6);
             c->n_trial++;
             c->last_n = n;
           }
-          double tr[3] = {c->pinned[0], c->pinned[1], (double)(*stop != 0)};
-          const double scale_pose = c->pinned[2];
-          if ((rc = allreduce_host(tr, 3, MCS_REDUCE_SUM, sc))) return rc;
-          agreed_stop = tr[2] > 0;
+          // sharded: summed on the device by enqueue_trial
+          const double tr[3] = {c->pinned[0], c->pinned[1], sharded ? c->pinned[2] : 0.0};
+          const double scale_pose = sharded ? c->pinned[3] : c->pinned[2];
+          agreed_stop = sharded ? tr[2] > 0 : *stop != 0;
           double tempChi = tr[0];
           if (fl) tempChi = std::numeric_limits<double>::max();
           rho = currentChi - tempChi;
@@ -2198,7 +2240,7 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
   const size_t NT = ldlt::tile_doubles(T), Np = (size_t)ldlt::TB * T;
   std::vector<double> hA(NT, 0.0), hb(Np, 0.0);
   for (int r = 0; r < n; r++)
-    for (int c = 0; c <= r; c++) hA[ldlt::sidx(r, c)] = S[(size_t)r * n + c];
+    for (int c = 0; c <= r; c++) hA[ldlt::sidx(r, c, T)] = S[(size_t)r * n + c];
   for (int r = 0; r < n; r++) hb[r] = b[r];
   double *dA = nullptr, *db = nullptr, *dx = nullptr, *dL = nullptr, *dI = nullptr, *dz = nullptr;
   int* dflag = nullptr;

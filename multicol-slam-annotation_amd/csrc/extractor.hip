@@ -128,6 +128,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
   fa.cell_counts = h->d_cell_counts;
   fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
+  fa.pattern = pl.p.fast_agast_type == 2 ? 16 : pl.p.fast_agast_type == 1 ? 12 : 8;
   fa.nframes = F;
   fill_level_ptrs(pl, fa.lp);
   const bool wide = pl.scale_factor > 1.5;

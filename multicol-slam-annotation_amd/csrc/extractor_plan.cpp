@@ -50,9 +50,15 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     set_error("desc_size must be 16, 32 or 64 (src/cTracking.cpp:133)");
     return MCS_ERR_ARG;
   }
-  if (p.use_agast || p.fast_agast_type != 2) {
-    set_error("only FAST TYPE_9_16 (fastAgastType 2, useAgast 0) is implemented");
+  // FastFeatureDetector types TYPE_5_8 = 0, TYPE_7_12 = 1, TYPE_9_16 = 2.  AGAST
+  // (AgastFeatureDetector's generated decision trees, OpenCV) is not implemented.
+  if (p.use_agast) {
+    set_error("AGAST (useAgast != 0) is not implemented; FAST types 0, 1, 2 are");
     return MCS_ERR_UNSUPPORTED;
+  }
+  if (p.fast_agast_type < 0 || p.fast_agast_type > 2) {
+    set_error("fastAgastType must be 0 (TYPE_5_8), 1 (TYPE_7_12) or 2 (TYPE_9_16)");
+    return MCS_ERR_ARG;
   }
   pl.p = p;
   pl.W = W; pl.H = H; pl.nlevels = p.nlevels;

@@ -60,6 +60,42 @@ __device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
 }
 
 __device__ __forceinline__ int fr_max3(int a, int b, int c) { return max(max(a, b), c); }
+
+// FAST TYPE_7_12 / TYPE_5_8 of one pixel (OpenCV FAST_t<12> / <8> + cornerScore; restated in
+// oracle/extractor_oracle.cpp fast_small): the circle from the ring (pixel e = y << 8 | x),
+// the quick test on the SAME pixel pairs as for 16 with wrapped offsets (pixel[k] =
+// pixel[k mod P]), a (K+1)-arc with K = P / 2 on the side(s) the quick test left, and
+// score + 1 = max(t, best dark arc minimum, best bright arc minimum).  Returns score + 1, or 0.
+template <int P>
+__device__ __forceinline__ int fast_small(const uint8_t* lds, uint32_t ring_base, int e, int t) {
+  constexpr int K = P / 2;
+  // (dx, dy) of OpenCV's offsets12 / offsets8
+  constexpr int c12[12][2] = {{0, 2}, {1, 2}, {2, 1}, {2, 0}, {2, -1}, {1, -2},
+                              {0, -2}, {-1, -2}, {-2, -1}, {-2, 0}, {-2, 1}, {-1, 2}};
+  constexpr int c8[8][2] = {{0, 1}, {1, 1}, {1, 0}, {1, -1}, {0, -1}, {-1, -1}, {-1, 0}, {-1, 1}};
+  auto at = [&](int dx, int dy) -> int {
+    return lds[((uint32_t)(e + dy * 256 + dx) & 0xFFFu) | ring_base];
+  };
+  const int v = at(0, 0);
+  int d[P];
+#pragma unroll
+  for (int k = 0; k < P; k++) d[k] = v - (P == 12 ? at(c12[k][0], c12[k][1]) : at(c8[k % 8][0], c8[k % 8][1]));
+  // tab bits: 1 = darker than v - t (d > t), 2 = brighter than v + t (d < -t)
+  auto tb = [&](int k) -> int { const int q = d[k % P]; return (q > t ? 1 : 0) | (q < -t ? 2 : 0); };
+  const int qd = (tb(0) | tb(8)) & (tb(2) | tb(10)) & (tb(4) | tb(12)) & (tb(6) | tb(14)) &
+                 (tb(1) | tb(9)) & (tb(3) | tb(11)) & (tb(5) | tb(13)) & (tb(7) | tb(15));
+  int dark = -256, bright = -256;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    int mn = d[k], mxv = d[k];
+#pragma unroll
+    for (int j = 1; j <= K; j++) { mn = min(mn, d[(k + j) % P]); mxv = max(mxv, d[(k + j) % P]); }
+    dark = max(dark, mn);
+    bright = max(bright, -mxv);
+  }
+  const bool corner = ((qd & 1) && dark > t) || ((qd & 2) && bright > t);
+  return corner ? max(max(t, dark), bright) : 0;
+}
 }  // namespace
 
 // Tuning probe (tools/gpu/fast_probe.py, variant builds with -DMCS_FAST_PROBE only): shader
@@ -75,6 +111,7 @@ __device__ unsigned long long g_fast_probe[8];
 #define FP_ADD(k, v) do { } while (0)
 #endif
 
+template <int PAT>
 __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   __shared__ __attribute__((aligned(4096))) uint8_t lds[kLdsBytes];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -240,9 +277,11 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       const uint32_t nv = ~c1;
       auto dk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c1, ~q, a.rbits), a.kk, 0u); };
       auto bk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(q, nv, a.rbits), a.kk, 0u); };
-      const uint32_t s = (y < y1) ? ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
-                                      ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm)
-                                  : 0u;
+      // 12 / 8 point circles: no pre-test, every detection pixel goes to the exact test
+      const uint32_t s = (y >= y1) ? 0u
+                         : PAT != 16 ? detm
+                                     : ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
+                                         ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm);
       // compaction: the lane's survivor count c (0..4) as three ballots of its bits gives the
       // lane's exclusive prefix by mbcnt; the four entries are written unconditionally, those
       // of non-survivors to a dummy slot
@@ -275,7 +314,21 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     // max(t, dark, bright).  Corners are compacted in place behind the carried ones (write
     // index <= read index, all reads of a batch precede its writes): raster order is kept.
     int ncorn = ncarry, nlast = 0;   // nlast: corners on the band's last row
-    for (int j0 = 0; j0 < ns; j0 += 128) {
+    if (PAT != 16) {
+      for (int j0 = 0; j0 < ns; j0 += 64) {
+        const int ja = j0 + lane;
+        const int ea = list[ncarry + min(ja, ns - 1)];
+        const int s1 = fast_small<PAT == 16 ? 12 : PAT>(lds, ring_base, ea, t);
+        const bool ca = ja < ns && s1 > 0;
+        if (ca) sc_at(ea, 0, 0) = (uint8_t)s1;
+        const uint64_t bal_a = __ballot(ca);
+        // every read of this batch precedes its writes (ja >= write index)
+        if (ca) list[ncorn + __popcll(bal_a & lt)] = (uint16_t)ea;
+        ncorn += __popcll(bal_a);
+        nlast += __popcll(__ballot(ca && (ea >> 8) == y1 - 1));
+      }
+    }
+    for (int j0 = 0; PAT == 16 && j0 < ns; j0 += 128) {
       const int ja = j0 + lane, jb = j0 + 64 + lane;
       const int ea = list[ncarry + min(ja, ns - 1)], eb = list[ncarry + min(jb, ns - 1)];
       // ring rows y-3 .. y+3 of both survivors, pointing at column x - 3
@@ -426,6 +479,7 @@ extern "C" int mcs_debug_fast_probe(unsigned long long* out, int reset) {
 #endif
 
 void launch_fast_rows(const FastRowArgs& a_in, hipStream_t st) {
+  // (pattern 12 / 8: the compare constants are unused)
   FastRowArgs a = a_in;
   // byte-wise compare constants of the compass pre-test: v_lerp_u8(v, ~p, r) =
   // floor((v - p + 255 + r) / 2) per byte is >= K exactly when v - p > t (K = (t + 256 + r) / 2,
@@ -436,7 +490,9 @@ void launch_fast_rows(const FastRowArgs& a_in, hipStream_t st) {
   a.rbits = r * 0x01010101u;
   a.kk = (K <= 255 ? (~(K - 1) & 0xFFu) : 0u) * 0x01010101u;
   const unsigned g = xcd_grid(a.nframes, (a.nunits + 3) / 4);
-  hipLaunchKernelGGL(k_fast_rows, dim3(g), dim3(256), 0, st, a);
+  if (a.pattern == 12) hipLaunchKernelGGL(k_fast_rows<12>, dim3(g), dim3(256), 0, st, a);
+  else if (a.pattern == 8) hipLaunchKernelGGL(k_fast_rows<8>, dim3(g), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_fast_rows<16>, dim3(g), dim3(256), 0, st, a);
 }
 
 }  // namespace mcs

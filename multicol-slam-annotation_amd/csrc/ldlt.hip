@@ -286,7 +286,7 @@ __device__ __forceinline__ double gemv_row(const double* M, const double* v) {
 
 __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* __restrict__ b,
                                                double* __restrict__ L, double* __restrict__ Linv,
-                                               double* __restrict__ z, int k, int* flag,
+                                               double* __restrict__ z, int k, int T, int* flag,
                                                const int* skip) {
   if (skip && *skip) return;
   extern __shared__ double sm[];
@@ -316,11 +316,11 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   // A_ij entries this thread updates at the end (accumulator layout, kept in registers)
   d2 vK[8], vX[8], vY[8];
   double aij[4][4];
-  fetch_tile(vK, A + toff(k, k));
+  fetch_tile(vK, A + toff(k, k, T));
   if (wg > 0) {
-    fetch_tile(vX, A + toff(i, k));
-    if (j != i) fetch_tile(vY, A + toff(j, k));
-    const double* Aij = A + toff(i, j);
+    fetch_tile(vX, A + toff(i, k, T));
+    if (j != i) fetch_tile(vY, A + toff(j, k, T));
+    const double* Aij = A + toff(i, j, T);
     const int col = 16 * w + r16;
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
   gemm_xyt(sX, sY, p);
   PANEL_STAMP(4);
   {
-    double* Aij = A + toff(i, j);
+    double* Aij = A + toff(i, j, T);
     const int col = 16 * w + r16;
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
       }
   }
   if (i == j) {
-    double* Lik = L + toff(i, k);
+    double* Lik = L + toff(i, k, T);
     for (int e = t; e < TB * TB; e += 256) Lik[e] = sX[(e >> 6) * LS + (e & 63)];
     const double s = gemv_row(sX, su);
     if ((t & 3) == 0) b[i * TB + (t >> 2)] -= s;
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
   for (int k = T - 1; k >= 0; k--) {
     double s0 = 0.0, s1 = 0.0;
     for (int ib = k + 1; ib < T; ib++) {
-      const double* Lik = L + toff(ib, k);
+      const double* Lik = L + toff(ib, k, T);
       const double* xi = sx + ib * TB;
       s0 += Lik[g * TB + c] * xi[g];
       s1 += Lik[(g + 16) * TB + c] * xi[g + 16];
@@ -448,7 +448,7 @@ __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int
   const int Np = T * TB;
   const int r = n + blockIdx.x;   // one workgroup per padding row
   if (r >= Np) return;
-  for (int c = threadIdx.x; c <= r; c += blockDim.x) A[sidx(r, c)] = (c == r) ? dv : 0.0;
+  for (int c = threadIdx.x; c <= r; c += blockDim.x) A[sidx(r, c, T)] = (c == r) ? dv : 0.0;
   // the strict-upper part of the last diagonal tile in the padding columns of rows < n is
   // never read by the factorisation (lower triangle only)
   if (threadIdx.x == 0) b[r] = 0.0;
@@ -549,7 +549,7 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
   for (int k = 0; k < T; k++) {
     const int m = T - 1 - k;
     const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);
-    hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, flag, skip);
+    hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, T, flag, skip);
   }
   hipLaunchKernelGGL(k_backward, dim3(1), dim3(kBwdNT), (size_t)T * TB * sizeof(double), st,
                      (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T, skip);

@@ -4,9 +4,13 @@
 // Eigen SimplicialLDLT without pivoting; an exact zero pivot fails the solve) for the Schur
 // complement produced by BlockSolver<6,3>::solve (block_solver.hpp:354-486).
 //
-// Storage: the symmetric matrix is held as its lower 64x64 tiles, tile (I, J) (I >= J) at
-// toff(I, J), each tile row-major.  n is padded to Np = 64 T with an identity block (zero
-// right-hand side), which leaves the solution of the leading n x n system unchanged.
+// Storage: the symmetric matrix is held as its lower 64x64 tiles in diagonal-major order --
+// diagonal d = I - J (d = 0: the T diagonal tiles, then the T - 1 tiles of the first
+// sub-diagonal, ...), J ascending along a diagonal -- each tile row-major.  A banded system
+// (the reduced camera system of keyframes that share points with their neighbours) keeps all
+// of its non-zero tiles in one leading range, so the sharded exchange reduces just that range
+// (ba.hip).  n is padded to Np = 64 T with an identity block (zero right-hand side), which
+// leaves the solution of the leading n x n system unchanged.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -16,13 +20,17 @@ namespace ldlt {
 
 constexpr int TB = 64;
 
-__host__ __device__ inline size_t toff(int I, int J) {
-  return ((size_t)I * (I + 1) / 2 + J) * (TB * TB);
+// tiles on the diagonals 0 .. d-1 of a T x T tile triangle
+__host__ __device__ inline size_t band_tiles(int d, int T) {
+  return (size_t)d * T - (size_t)d * (d - 1) / 2;
+}
+__host__ __device__ inline size_t toff(int I, int J, int T) {
+  return (band_tiles(I - J, T) + J) * (TB * TB);
 }
 // element (r, c) with r >= c (callers never address the strict upper triangle of a
 // diagonal tile through this)
-__host__ __device__ inline size_t sidx(int r, int c) {
-  return toff(r / TB, c / TB) + (size_t)(r % TB) * TB + (c % TB);
+__host__ __device__ inline size_t sidx(int r, int c, int T) {
+  return toff(r / TB, c / TB, T) + (size_t)(r % TB) * TB + (c % TB);
 }
 inline int tiles_for(int n) { return (n + TB - 1) / TB; }
 inline size_t tile_doubles(int T) { return (size_t)T * (T + 1) / 2 * TB * TB; }

@@ -485,15 +485,16 @@ class Solver:
 # ---------------------------------------------------------------------------
 HUBER_GLOBAL = float(np.sqrt(5.991))     # cOptimizer::BundleAdjustment thHuber (src/cOptimizer.cpp:161)
 
+# (user, op, offset, count, hipStream_t of the library)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
-                                ctypes.c_int64)
+                                ctypes.c_int64, ctypes.c_void_p)
 
 
 class BAShard(ctypes.Structure):
     """Mirror of mcs_ba_shard (include/mcs_ba.h)."""
     _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32), ("xchg", ctypes.c_void_p),
                 ("xchg_cap", ctypes.c_int64), ("allreduce", ALLREDUCE_FN),
-                ("user", ctypes.c_void_p)]
+                ("user", ctypes.c_void_p), ("stream_ordered", ctypes.c_int32)]
 
 
 def ring_rig(ncams=8, size=1024, radius=0.12, phase_deg=10.0):
@@ -643,8 +644,11 @@ def shard_problem(pr, rank, world):
 class TorchExchange:
     """mcs_ba_shard backed by torch.distributed: the exchange buffer is a torch tensor on the
     rank's GPU and the callback all-reduces a slice of it (backend "nccl" = RCCL over xGMI).
-    The library drains its stream before calling; the callback returns after the collective
-    has completed on the device."""
+
+    On a GPU the shard is stream_ordered: the callback issues the all-reduce with the library's
+    stream as torch's current stream, so RCCL starts after the kernels that produced the slice
+    and the library's next kernels wait for it on the device -- no host synchronisation per
+    exchange.  A CPU buffer (gloo) is reduced synchronously (stream_ordered = 0)."""
 
     def __init__(self, n_poses, device, group=None):
         import torch
@@ -656,16 +660,29 @@ class TorchExchange:
         cap = int(lib().mcs_ba_xchg_doubles(int(n_poses)))
         self.buf = torch.zeros(cap, dtype=torch.float64, device=device)
         self._cb = ALLREDUCE_FN(self._allreduce)
-        self.shard = BAShard(self.rank, self.world, self.buf.data_ptr(), cap, self._cb, None)
+        self.shard = BAShard(self.rank, self.world, self.buf.data_ptr(), cap, self._cb, None,
+                             1 if self.buf.is_cuda else 0)
+        self._streams = {}
         self.calls = 0
 
-    def _allreduce(self, user, op, off, cnt):
+    def _stream(self, handle):
+        s = self._streams.get(handle)
+        if s is None:
+            s = self.torch.cuda.ExternalStream(handle, device=self.buf.device)
+            self._streams[handle] = s
+        return s
+
+    def _allreduce(self, user, op, off, cnt, stream=None):
         try:
             t = self.buf[off:off + cnt]
             rop = self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX
-            self.dist.all_reduce(t, op=rop, group=self.group)
             if self.buf.is_cuda:
-                self.torch.cuda.synchronize(self.buf.device)
+                # the NCCL process group orders the collective after the current stream's work
+                # and makes the current stream wait for it (no host wait)
+                with self.torch.cuda.stream(self._stream(stream)):
+                    self.dist.all_reduce(t, op=rop, group=self.group)
+            else:
+                self.dist.all_reduce(t, op=rop, group=self.group)
             self.calls += 1
             return 0
         except Exception:   # never raise through the C stack

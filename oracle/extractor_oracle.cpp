@@ -220,21 +220,95 @@ bool fast_is_corner(const Img& im, int x, int y, int threshold) {
   return false;
 }
 
-// FastFeatureDetector(th, nonmax=true, TYPE_9_16)::detect(roi, kps, maskRoi):
-// FAST on the ROI [x0,x1)x[y0,y1) of `im`, then runByPixelsMask.  Output
-// coordinates are ROI-local, emitted row-major.
+// FAST TYPE_7_12 / TYPE_5_8 (FastFeatureDetector types 1 / 0) -- OpenCV 3.x FAST_t<12> /
+// FAST_t<8> with cornerScore<12> / <8> [ext, OpenCV 3.1 fast.cpp + fast_score.cpp, published
+// algorithm restated; OpenCV is absent here, so these two types are parity unpinned]:
+//   makeOffsets: the pattern's circle, then pixel[k] = pixel[k - patternSize] up to k = 24
+//   quick test on tab bits (1: p < v - t, 2: p > v + t) of pixel pairs (0,8) (2,10) (4,12)
+//     (6,14) (1,9) (3,11) (5,13) (7,15) -- the SAME pair list as for 16, so with 12 / 8 points
+//     the wrapped offsets make it stricter than the arc test
+//   corner: d & 1 and more than K = patternSize / 2 contiguous darker pixels among the
+//     N = patternSize + K + 1 wrapped ones (d & 2: brighter); score: cornerScore's
+//     a0 / b0 loops over every (K+1)-arc
+const int kCircle12[12][2] = {{0, 2}, {1, 2}, {2, 1}, {2, 0}, {2, -1}, {1, -2},
+                              {0, -2}, {-1, -2}, {-2, -1}, {-2, 0}, {-2, 1}, {-1, 2}};
+const int kCircle8[8][2] = {{0, 1}, {1, 1}, {1, 0}, {1, -1}, {0, -1}, {-1, -1}, {-1, 0}, {-1, 1}};
+
+// pat = 12 or 8; returns the score (cornerScore) of a corner, -1 for no corner
+int fast_small(const Img& im, int x, int y, int threshold, int pat) {
+  const int (*circ)[2] = pat == 12 ? kCircle12 : kCircle8;
+  const int K = pat / 2, N = pat + K + 1;
+  const int v = im.at(y, x);
+  int px[25];
+  for (int k = 0; k < 25; k++) px[k] = im.at(y + circ[k % pat][1], x + circ[k % pat][0]);
+  auto tab = [&](int p) { return p - v < -threshold ? 1 : p - v > threshold ? 2 : 0; };
+  int d = tab(px[0]) | tab(px[8]);
+  if (d == 0) return -1;
+  d &= tab(px[2]) | tab(px[10]);
+  d &= tab(px[4]) | tab(px[12]);
+  d &= tab(px[6]) | tab(px[14]);
+  if (d == 0) return -1;
+  d &= tab(px[1]) | tab(px[9]);
+  d &= tab(px[3]) | tab(px[11]);
+  d &= tab(px[5]) | tab(px[13]);
+  d &= tab(px[7]) | tab(px[15]);
+  bool corner = false;
+  if (d & 1) {
+    int cnt = 0;
+    for (int k = 0; k < N && !corner; k++) {
+      if (px[k] < v - threshold) { if (++cnt > K) corner = true; } else cnt = 0;
+    }
+  }
+  if (!corner && (d & 2)) {
+    int cnt = 0;
+    for (int k = 0; k < N && !corner; k++) {
+      if (px[k] > v + threshold) { if (++cnt > K) corner = true; } else cnt = 0;
+    }
+  }
+  if (!corner) return -1;
+  // cornerScore<pat>: d[k] = v - pixel k (wrapped), a0 over the (K+1)-arcs' minima, b0 over
+  // their maxima, as the reference's a / b loops (which only skip arcs that cannot win)
+  int dd[25];
+  for (int k = 0; k < 25; k++) dd[k] = v - px[k];
+  int a0 = threshold;
+  for (int k = 0; k < pat; k++) {
+    int a = dd[k];
+    for (int j = 1; j <= K; j++) a = std::min(a, dd[k + j]);
+    a0 = std::max(a0, a);
+  }
+  int b0 = -a0;
+  for (int k = 0; k < pat; k++) {
+    int b = dd[k];
+    for (int j = 1; j <= K; j++) b = std::max(b, dd[k + j]);
+    b0 = std::min(b0, b);
+  }
+  return -b0 - 1;
+}
+
+// FastFeatureDetector(th, nonmax=true, type)::detect(roi, kps, maskRoi) (type 2 = TYPE_9_16,
+// 1 = TYPE_7_12, 0 = TYPE_5_8): FAST on the ROI [x0,x1)x[y0,y1) of `im`, then
+// runByPixelsMask.  Output coordinates are ROI-local, emitted row-major.
 void fast_detect_roi(const Img& im, const Img* mask, int x0, int y0, int x1, int y1,
-                     int threshold, std::vector<Cand>& out) {
+                     int threshold, std::vector<Cand>& out, int fast_type = 2) {
   threshold = std::min(std::max(threshold, 0), 255);
   int cols = x1 - x0, rows = y1 - y0;
   std::vector<int> score((size_t)std::max(rows, 0) * std::max(cols, 0), 0);
   std::vector<uint8_t> corner(score.size(), 0);
   for (int i = 3; i < rows - 3; i++)
-    for (int j = 3; j < cols - 3; j++)
-      if (fast_is_corner(im, x0 + j, y0 + i, threshold)) {
-        corner[(size_t)i * cols + j] = 1;
-        score[(size_t)i * cols + j] = (uint8_t)fast_score16(im, x0 + j, y0 + i, threshold);
+    for (int j = 3; j < cols - 3; j++) {
+      if (fast_type == 2) {
+        if (fast_is_corner(im, x0 + j, y0 + i, threshold)) {
+          corner[(size_t)i * cols + j] = 1;
+          score[(size_t)i * cols + j] = (uint8_t)fast_score16(im, x0 + j, y0 + i, threshold);
+        }
+      } else {
+        const int sc = fast_small(im, x0 + j, y0 + i, threshold, fast_type == 1 ? 12 : 8);
+        if (sc >= 0) {
+          corner[(size_t)i * cols + j] = 1;
+          score[(size_t)i * cols + j] = (uint8_t)sc;
+        }
       }
+    }
   auto S = [&](int i, int j) { return score[(size_t)i * cols + j]; };
   for (int i = 3; i < rows - 3; i++)
     for (int j = 3; j < cols - 3; j++) {
@@ -595,7 +669,8 @@ std::vector<int> features_per_level(const Params& p) {  // ctor :167-179
 
 // per-level FAST cell sweep (ComputeKeyPointsOctTree :874-949), candidates in
 // reference order with coordinates relative to minBorder
-void level_candidates(const Img& im, const Img* mask, int fastTh, std::vector<KP>& out) {
+void level_candidates(const Img& im, const Img* mask, int fastTh, std::vector<KP>& out,
+                      int fast_type = 2) {
   const double Wc = 30.0;
   const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
   const int maxBorderX = im.w - EDGE_THRESHOLD + 3, maxBorderY = im.h - EDGE_THRESHOLD + 3;
@@ -613,7 +688,7 @@ void level_candidates(const Img& im, const Img* mask, int fastTh, std::vector<KP
       if (iniX >= maxBorderX - 6) continue;
       if (maxX > maxBorderX) maxX = maxBorderX;
       std::vector<Cand> cell;
-      fast_detect_roi(im, mask, (int)iniX, (int)iniY, (int)maxX, (int)maxY, fastTh, cell);
+      fast_detect_roi(im, mask, (int)iniX, (int)iniY, (int)maxX, (int)maxY, fastTh, cell, fast_type);
       for (auto& c : cell)
         out.push_back({(float)(c.x + j * wCell), (float)(c.y + i * hCell), (float)c.score, (int)out.size()});
     }
@@ -678,18 +753,23 @@ int oracle_box_blur5(const uint8_t* src, int w, int h, uint8_t* dst) {
 
 // FAST candidates of one level in reference order; xyr out as int triples
 // (x_rel, y_rel, score); mask may be NULL.
-int oracle_level_candidates(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
-                            int* xys_out, int cap, int* n_out) {
+int oracle_level_candidates_type(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
+                                 int fast_type, int* xys_out, int cap, int* n_out) {
   Img im; im.create(w, h); std::memcpy(im.d.data(), img, (size_t)w * h);
   Img mk; if (mask) { mk.create(w, h); std::memcpy(mk.d.data(), mask, (size_t)w * h); }
   std::vector<KP> c;
-  level_candidates(im, mask ? &mk : nullptr, fastTh, c);
+  level_candidates(im, mask ? &mk : nullptr, fastTh, c, fast_type);
   *n_out = (int)c.size();
   if ((int)c.size() > cap) return -1;
   for (size_t i = 0; i < c.size(); i++) {
     xys_out[3 * i] = (int)c[i].x; xys_out[3 * i + 1] = (int)c[i].y; xys_out[3 * i + 2] = (int)c[i].response;
   }
   return 0;
+}
+
+int oracle_level_candidates(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
+                            int* xys_out, int cap, int* n_out) {
+  return oracle_level_candidates_type(img, mask, w, h, fastTh, 2, xys_out, cap, n_out);
 }
 
 // octree on candidate triples (relative coords); returns selected candidate indices in output order
@@ -748,11 +828,12 @@ float oracle_ic_angle(const uint8_t* img, int w, int h, int cx, int cy, int* m01
 // Full extractor: mdBRIEFextractorOct::operator() (:1244-1337).  ORB when cam == nullptr
 // (do_dbrief = learn_masks = 0); dBRIEF / mdBRIEF otherwise.  kps/desc/desc_masks
 // caller-allocated (cap keypoints; desc_masks nullable).  Returns 0, or -1 if cap too small.
-int oracle_extract_ex(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
-                      float scale_factor, int nlevels, int fast_threshold, int desc_size,
-                      int vresize_mode, int do_dbrief, int learn_masks, const mcs_cam_model* cam,
-                      oracle_keypoint* kps, uint8_t* desc, uint8_t* desc_masks, int cap,
-                      int* n_out) {
+int oracle_extract_ex2(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
+                       float scale_factor, int nlevels, int fast_threshold, int desc_size,
+                       int vresize_mode, int do_dbrief, int learn_masks, const mcs_cam_model* cam,
+                       oracle_keypoint* kps, uint8_t* desc, uint8_t* desc_masks, int cap,
+                       int* n_out, int fast_type) {
+  if (fast_type < 0 || fast_type > 2) return -3;
   Params p{nfeatures, scale_factor, nlevels, fast_threshold, desc_size, vresize_mode};
   std::vector<Level> lv; std::vector<double> sf, isf;
   level_sizes(W, H, p, lv, sf, isf);
@@ -772,7 +853,7 @@ int oracle_extract_ex(const uint8_t* image, int W, int H, const uint8_t* mask, i
   const int minBorder = EDGE_THRESHOLD - 3;
   for (int l = 0; l < nlevels; l++) {
     std::vector<KP> cands;
-    level_candidates(pyr[l], mask ? &mpyr[l] : nullptr, fast_threshold, cands);
+    level_candidates(pyr[l], mask ? &mpyr[l] : nullptr, fast_threshold, cands, fast_type);
     all[l] = distribute_octree(cands, minBorder, pyr[l].w - EDGE_THRESHOLD + 3, minBorder,
                                pyr[l].h - EDGE_THRESHOLD + 3, nPerLevel[l]);
     for (auto& k : all[l]) { k.x += minBorder; k.y += minBorder; }
@@ -819,6 +900,16 @@ int oracle_extract_ex(const uint8_t* image, int W, int H, const uint8_t* mask, i
     off += (int)all[l].size();
   }
   return 0;
+}
+
+int oracle_extract_ex(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,
+                      float scale_factor, int nlevels, int fast_threshold, int desc_size,
+                      int vresize_mode, int do_dbrief, int learn_masks, const mcs_cam_model* cam,
+                      oracle_keypoint* kps, uint8_t* desc, uint8_t* desc_masks, int cap,
+                      int* n_out) {
+  return oracle_extract_ex2(image, W, H, mask, nfeatures, scale_factor, nlevels, fast_threshold,
+                            desc_size, vresize_mode, do_dbrief, learn_masks, cam, kps, desc,
+                            desc_masks, cap, n_out, 2);
 }
 
 int oracle_extract(const uint8_t* image, int W, int H, const uint8_t* mask, int nfeatures,

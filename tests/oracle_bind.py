@@ -28,11 +28,13 @@ _SIGS = {
     "oracle_resize_nearest": (_I, [_P, _I, _I, _P, _I, _I]),
     "oracle_box_blur5": (_I, [_P, _I, _I, _P]),
     "oracle_level_candidates": (_I, [_P, _P, _I, _I, _I, _P, _I, _P]),
+    "oracle_level_candidates_type": (_I, [_P, _P, _I, _I, _I, _I, _P, _I, _P]),
     "oracle_octree": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _P]),
     "oracle_ic_angle": (_F, [_P, _I, _I, _I, _I, _P, _P]),
     "oracle_harris_responses": (_I, [_P, _I, _I, _P, _I, _I, _F, _P]),
     "oracle_extract": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _P, _P, _I, _P]),
     "oracle_extract_ex": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
+    "oracle_extract_ex2": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _I]),
     "oracle_cam_world_to_img": (_I, [_P, _D, _D, _D, _P]),
     "oracle_cam_img_to_world": (_I, [_P, _D, _D, _P]),
     # matcher oracle
@@ -143,14 +145,15 @@ def mask_pyramid(mask, nlevels=8, scale=1.2):
     return levels
 
 
-def level_candidates(level_img, level_mask, fast_th):
+def level_candidates(level_img, level_mask, fast_th, fast_type=2):
+    """FAST candidates of one level; fast_type: 2 TYPE_9_16, 1 TYPE_7_12, 0 TYPE_5_8."""
     h, w = level_img.shape
     cap = w * h // 4 + 16
     out = np.zeros(3 * cap, np.int32)
     n = ctypes.c_int()
-    rc = lib().oracle_level_candidates(_p(np.ascontiguousarray(level_img)),
-                                       _p(None if level_mask is None else np.ascontiguousarray(level_mask)),
-                                       w, h, fast_th, _p(out), cap, ctypes.byref(n))
+    rc = lib().oracle_level_candidates_type(_p(np.ascontiguousarray(level_img)),
+                                            _p(None if level_mask is None else np.ascontiguousarray(level_mask)),
+                                            w, h, fast_th, fast_type, _p(out), cap, ctypes.byref(n))
     assert rc == 0
     return out[:3 * n.value].reshape(-1, 3)
 
@@ -169,7 +172,7 @@ def octree(cands, w, h, N):
 
 
 def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, desc_size=32,
-            mode=1):
+            mode=1, fast_type=2):
     img = np.ascontiguousarray(img, np.uint8)
     H, W = img.shape
     cap = nfeatures * 2 + 64 * nlevels
@@ -177,8 +180,13 @@ def extract(img, mask=None, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, de
     desc = np.zeros((cap, desc_size), np.uint8)
     n = ctypes.c_int()
     m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
-    rc = lib().oracle_extract(_p(img), W, H, _p(m), nfeatures, scale, nlevels, fast_th,
-                              desc_size, mode, _p(kps), _p(desc), cap, ctypes.byref(n))
+    if fast_type == 2:
+        rc = lib().oracle_extract(_p(img), W, H, _p(m), nfeatures, scale, nlevels, fast_th,
+                                  desc_size, mode, _p(kps), _p(desc), cap, ctypes.byref(n))
+    else:
+        rc = lib().oracle_extract_ex2(_p(img), W, H, _p(m), nfeatures, scale, nlevels, fast_th,
+                                      desc_size, mode, 0, 0, None, _p(kps), _p(desc), None, cap,
+                                      ctypes.byref(n), fast_type)
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
 

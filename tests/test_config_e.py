@@ -61,10 +61,10 @@ def test_gpu_config_e_matches_oracle(gpu, eproblem, eoracle, egpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 8])
-def test_gpu_config_e_sharded_lockstep(gpu, eproblem, egpu, world):
+@pytest.mark.parametrize("world,ordered", [(2, False), (8, True)])
+def test_gpu_config_e_sharded_lockstep(gpu, eproblem, egpu, world, ordered):
     from mcs_amd import ba
-    X = ThreadExchange(world, len(eproblem["poses"]))
+    X = ThreadExchange(world, len(eproblem["poses"]), ordered=ordered)
     out = [None] * world
     err = [None] * world
 
@@ -82,6 +82,12 @@ def test_gpu_config_e_sharded_lockstep(gpu, eproblem, egpu, world):
         t.join(600)
     assert all(e is None for e in err), err
     assert all(X.calls[r] == X.calls[0] for r in range(world))
+    # config E's reduced system is banded (12 of 19 tile diagonals): the per-trial exchange
+    # (bs + leading diagonals) is shorter than the whole tile triangle
+    n = 6 * int(out[0][0]["report"].n_active_poses)
+    T = (n + 63) // 64
+    big = {c[2] for c in X.calls[0] if c[0] == 0 and c[1] == 0 and c[2] >= 64 * T}
+    assert len(big) == 1 and big.pop() < 64 * T + T * (T + 1) // 2 * 4096
     for r in range(1, world):
         assert np.array_equal(out[r][0]["poses"], out[0][0]["poses"])
         assert out[r][0]["report"].iterations == out[0][0]["report"].iterations

@@ -207,36 +207,72 @@ def test_gpu_global_ba_matches_oracle(gpu, gproblem, pose_only):
 
 class ThreadExchange:
     """In-process stand-in for the collective: `world` ranks run on threads of one process,
-    each with its own solver context / stream and exchange buffer on the same GPU."""
+    each with its own solver context / stream and exchange buffer on the same GPU.
 
-    def __init__(self, world, n_poses):
+    ordered=False: the library drains its stream before each call; rank 0 sums the slices and
+    every rank returns once the sum is on the device.  ordered=True (stream_ordered shards, as
+    TorchExchange on a GPU): nobody waits on the host -- every rank records an event on its
+    stream, rank 0's stream waits for all of them and sums, and every rank's stream waits for
+    rank 0's; the callback returns as soon as that is enqueued."""
+
+    def __init__(self, world, n_poses, ordered=False):
         import torch
         from mcs_amd import ba, lib
-        self.world = world
+        self.world, self.ordered = world, ordered
         cap = int(lib().mcs_ba_xchg_doubles(int(n_poses)))
         self.bufs = [torch.zeros(cap, dtype=torch.float64, device="cuda") for _ in range(world)]
         self.bar = threading.Barrier(world)
         self.calls = [[] for _ in range(world)]
+        self.ev = [None] * world
+        self.done = None
+        self.streams = {}
         self.fns, self.shards = [], []
         for r in range(world):
-            fn = ba.ALLREDUCE_FN(lambda u, op, off, cnt, r=r: self._cb(r, op, off, cnt))
+            fn = ba.ALLREDUCE_FN(lambda u, op, off, cnt, st, r=r: self._cb(r, op, off, cnt, st))
             self.fns.append(fn)
-            self.shards.append(ba.BAShard(r, world, self.bufs[r].data_ptr(), cap, fn, None))
+            self.shards.append(ba.BAShard(r, world, self.bufs[r].data_ptr(), cap, fn, None,
+                                          1 if ordered else 0))
 
-    def _cb(self, r, op, off, cnt):
+    def _reduce(self, op, off, cnt):
+        import torch
+        sl = [b[off:off + cnt] for b in self.bufs]
+        for t in sl[1:]:                # in place: no allocation on a foreign stream
+            if op == 0:
+                sl[0].add_(t)
+            else:
+                torch.maximum(sl[0], t, out=sl[0])
+        for t in sl[1:]:
+            t.copy_(sl[0])
+
+    def _cb(self, r, op, off, cnt, stream):
         import torch
         try:
             self.calls[r].append((op, off, cnt))
+            if not self.ordered:
+                self.bar.wait(60)
+                if r == 0:
+                    self._reduce(op, off, cnt)
+                    torch.cuda.synchronize()
+                self.bar.wait(60)
+                return 0
+            s = self.streams.get(stream)
+            if s is None:
+                s = self.streams[stream] = torch.cuda.ExternalStream(stream)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            self.ev[r] = ev
             self.bar.wait(60)
             if r == 0:
-                sl = [b[off:off + cnt] for b in self.bufs]
-                acc = sl[0].clone()
-                for t in sl[1:]:
-                    acc = acc + t if op == 0 else torch.maximum(acc, t)
-                for t in sl:
-                    t.copy_(acc)
-                torch.cuda.synchronize()
+                with torch.cuda.stream(s):
+                    for e in self.ev[1:]:
+                        s.wait_event(e)
+                    self._reduce(op, off, cnt)
+                    done = torch.cuda.Event()
+                    done.record(s)
+                self.done = done
             self.bar.wait(60)
+            if r != 0:
+                s.wait_event(self.done)
             return 0
         except Exception:
             return 1
@@ -250,17 +286,21 @@ class ThreadExchange:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_sharded_global_ba_lockstep(gpu, gproblem, world):
+@pytest.mark.parametrize("world,ordered", [(2, False), (3, False), (2, True), (3, True)])
+def test_gpu_sharded_global_ba_lockstep(gpu, gproblem, world, ordered):
     from mcs_amd import ba
-    X = ThreadExchange(world, len(gproblem["poses"]))
+    X = ThreadExchange(world, len(gproblem["poses"]), ordered=ordered)
     out = [None] * world
     err = [None] * world
+    stages = [None] * world
 
     def run(r):
         try:
             sub, rng, _ = ba.shard_problem(gproblem, r, world)
-            out[r] = (ba.Solver().global_ba(sub, exchange=X.member(r), trace=20), rng)
+            S = ba.Solver()
+            S.enable_timing(ordered)   # the stage clock must not change the call sequence
+            out[r] = (S.global_ba(sub, exchange=X.member(r), trace=20), rng)
+            stages[r] = S.read_timing()
         except Exception as e:   # surfaced below
             err[r] = e
 
@@ -272,6 +312,14 @@ def test_gpu_sharded_global_ba_lockstep(gpu, gproblem, world):
     assert all(e is None for e in err), err
     # every rank took the same collectives and ended with bit-identical poses
     assert all(X.calls[r] == X.calls[0] for r in range(world))
+    # the per-trial reduced-system exchange covers bs + the leading (non-zero) tile diagonals
+    # only: strictly less than the whole tile triangle once the system has 3+ tiles
+    n = 6 * int(out[0][0]["report"].n_active_poses)
+    T = (n + 63) // 64
+    big = [c for c in X.calls[0] if c[0] == 0 and c[1] == 0 and c[2] >= 64 * T]
+    assert big and all(c[2] <= 64 * T + T * (T + 1) // 2 * 4096 for c in big)
+    if ordered:   # exchange stage = stream time of the all-reduce
+        assert all(st[0]["exchange"] > 0 for st in stages), stages
     for r in range(1, world):
         assert np.array_equal(out[r][0]["poses"], out[0][0]["poses"])
         assert out[r][0]["report"].iterations == out[0][0]["report"].iterations

@@ -25,7 +25,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < n; r++) rhs[r] = std::sin(0.01 * r);
   std::vector<double> tiles(tile_doubles(T));
   for (int r = 0; r < Np; r++)
-    for (int c = 0; c <= r; c++) tiles[sidx(r, c)] = M[(size_t)r * Np + c];
+    for (int c = 0; c <= r; c++) tiles[sidx(r, c, T)] = M[(size_t)r * Np + c];
   double *dA, *db, *dx, *dL, *dLi, *dz;
   int* dflag;
   (void)hipMalloc(&dA, tiles.size() * 8); (void)hipMalloc(&db, Np * 8); (void)hipMalloc(&dx, Np * 8);
