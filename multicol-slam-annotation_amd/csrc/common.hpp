@@ -36,6 +36,15 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Round a byte pointer down to its dword.  Pointer arithmetic (not an integer round trip)
 // keeps the global address space, so loads stay global_load (a flat_load also counts on
 // lgkmcnt and every LDS wait would then wait for it).
+// a wave-uniform pointer moved to SGPRs: stores / loads through it + a 32-bit lane offset use
+// the saddr form (no 64-bit address arithmetic per lane)
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ const uint32_t* align_down4(const uint8_t* p) {
   return reinterpret_cast<const uint32_t*>(p - ((uintptr_t)p & 3));
 }

@@ -14,13 +14,15 @@
 //
 // The run is streamed in bands of kBand detection rows:
 //   load  the band's new raw rows (one dword per lane, issued one band ahead) enter a
-//         register window (rows y0-3 .. y0+kBand+2) and a 16-row LDS ring; with a 256 B row
-//         stride the ring address of pixel (y, x) + (dy, dx) is ((y << 8 | x) + (dy << 8) + dx)
-//         & 0xFFF
+//         register window (rows y0-3 .. y0+kBand+2), and all kBand + 6 rows of that window are
+//         written to a linear LDS band window (256 B per row): a survivor's 7 x 7 neighbourhood
+//         is then one base address + immediate offsets
 //   A     compass pre-test per quad from the register window, 4 pixels per lane, survivors
 //         -> list in raster order
-//   B     exact test + score of the survivors in full 64-lane batches from the ring: score + 1
-//         into an 8-row score ring, corners compacted in place (raster order)
+//   B     exact test + score of the survivors in full 64-lane batches from the band window:
+//         score + 1 into a linear score window (rows y0-2 .. y0+kBand; the two rows above the
+//         band are carried over from the previous band), corners compacted in place (raster
+//         order)
 //   C     NMS of every corner whose lower neighbour row is scored (the band's last row waits
 //         for the next band), the mask bit, and the append to the cell's slot list: raster
 //         order within a cell, the order OpenCV's FAST emits them in.
@@ -36,12 +38,12 @@ namespace {
 constexpr int kBand = MCS_FAST_BAND;   // detection rows per band (3, 4 or 8)
 static_assert(kBand >= 3 && kBand <= 8, "band height");
 // score rows alive at once: the NMS of a band reads rows y0 - 2 .. y1 and the band zeroes
-// y0 .. y0 + kBand, so kBand + 3 distinct rows share the ring
-constexpr int kScoreRows = kBand + 3 <= 8 ? 8 : 16;
-// LDS: the four waves' raw rings (16 x 256 B, 4 KB aligned), then their score rings (8 x 256 B,
-// 2 KB aligned), then their lists (carried corners, then the band's survivors, compacted in
-// place into its corners).  The alignment lets a ring address be (offset & mask) | base.
-constexpr int kRingBytes = 4096, kScoreBytes = kScoreRows * 256;
+// y0 .. y0 + kBand, so the score window holds rows y0 - 2 .. y0 + kBand
+constexpr int kScoreRows = kBand + 3;
+// LDS: the four waves' raw band windows (kBand + 6 rows of 256 B), then their score windows,
+// then their lists (carried corners, then the band's survivors, compacted in place into its
+// corners)
+constexpr int kRingBytes = (kBand + 6) * 256, kScoreBytes = kScoreRows * 256;
 // a run's detection span is <= 246 px (kFastUnitSpan - 6): <= 246 carried corners + 246 kBand
 // survivors
 constexpr int kListCap = 248 + kBand * 248;
@@ -68,13 +70,14 @@ __device__ __forceinline__ int fr_max3(int a, int b, int c) { return max(max(a, 
 // score + 1 = max(t, best dark arc minimum, best bright arc minimum).  Returns score + 1, or 0.
 template <int P>
 __device__ __forceinline__ int fast_small(const uint8_t* lds, uint32_t ring_base, int e, int t) {
+  // ring_base: LDS byte of pixel (y, x) = ring_base + e (e = y << 8 | x) in the band window
   constexpr int K = P / 2;
   // (dx, dy) of OpenCV's offsets12 / offsets8
   constexpr int c12[12][2] = {{0, 2}, {1, 2}, {2, 1}, {2, 0}, {2, -1}, {1, -2},
                               {0, -2}, {-1, -2}, {-2, -1}, {-2, 0}, {-2, 1}, {-1, 2}};
   constexpr int c8[8][2] = {{0, 1}, {1, 1}, {1, 0}, {1, -1}, {0, -1}, {-1, -1}, {-1, 0}, {-1, 1}};
   auto at = [&](int dx, int dy) -> int {
-    return lds[((uint32_t)(e + dy * 256 + dx) & 0xFFFu) | ring_base];
+    return lds[ring_base + (uint32_t)(e + dy * 256 + dx)];
   };
   const int v = at(0, 0);
   int d[P];
@@ -113,16 +116,18 @@ __device__ unsigned long long g_fast_probe[8];
 
 template <int PAT>
 __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
-  __shared__ __attribute__((aligned(4096))) uint8_t lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t ring_base = (uint32_t)wv * kRingBytes;
   const uint32_t sc_base = kScoreBase + (uint32_t)wv * kScoreBytes;
   uint32_t* const ring32 = reinterpret_cast<uint32_t*>(lds + ring_base);
   uint8_t* const sc8 = lds + sc_base;
   uint16_t* const list = reinterpret_cast<uint16_t*>(lds + kListBase + wv * 2 * (kListCap + 2));
-  // score-ring byte of pixel e = (y << 8 | x) moved by (dy, dx)
+  // band-relative LDS bases, set per band: pixel e = (y << 8 | x) of the band is raw byte
+  // raw_rel + e and score byte sc_rel + e
+  uint32_t raw_rel = 0, sc_rel = 0;
   auto sc_at = [&](int e, int dy, int dx) -> uint8_t& {
-    return lds[((uint32_t)(e + dy * 256 + dx) & (uint32_t)(kScoreBytes - 1)) | sc_base];
+    return lds[sc_rel + (uint32_t)(e + dy * 256 + dx)];
   };
   int f, item;
   if (!xcd_frame_map(blockIdx.x, a.nframes, (a.nunits + 3) / 4, &f, &item)) return;
@@ -174,20 +179,18 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   };
   auto fix_row = [&](int r, uint32_t own) -> uint32_t {
     const uint32_t sh = (uint32_t)((uintptr_t)(row0 + r * pitch) & 3);
-    const uint32_t nxt = __builtin_amdgcn_update_dpp(0u, own, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
+    const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0x130 /*wave_shl:1*/, 0xF, 0xF, true);
     return __builtin_amdgcn_alignbyte(nxt, own, sh);
   };
-  auto put_row = [&](int r, uint32_t v) { ring32[((r & 15) << 6) + lane] = v; };
   // mask bytes of raw row r (all 0xFF without a mask)
   auto load_mrow = [&](int r) -> uint32_t {
     if (!mrow0) return 0xFFFFFFFFu;
     return reinterpret_cast<const uint32_t*>(mrow0 + r * mpitch)[lane];
   };
 
-  // the score ring starts zeroed: rows outside the detection window read as non-corners
+  // the score window starts zeroed: rows outside the detection window read as non-corners
 #pragma unroll
-  for (int i = 0; i < kScoreBytes / 1024; i++)
-    *reinterpret_cast<uint4*>(sc8 + 1024 * i + 16 * lane) = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = 0; i < kScoreRows; i++) *reinterpret_cast<uint32_t*>(sc8 + 256 * i + 4 * lane) = 0u;
   // register window: rows y0 - 3 .. y0 + 2 of the current band (the compass reads registers;
   // the exact test reads the ring)
   uint32_t w[6];
@@ -203,10 +206,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
 #pragma unroll
   for (int i = 0; i < kBand; i++) mpf[i] = load_mrow(kBand + 4 + i);
 #pragma unroll
-  for (int i = 0; i < 6; i++) {
-    w[i] = fix_row(i, w[i]);
-    put_row(i, w[i]);
-  }
+  for (int i = 0; i < 6; i++) w[i] = fix_row(i, w[i]);
 
   const int nbands = (wh + kBand - 1) / kBand;
   int ncarry = 0;   // corners of the previous band's last row, at the front of the list
@@ -218,10 +218,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
 #pragma unroll
     for (int i = 0; i < 6; i++) rows[i] = w[i];
 #pragma unroll
-    for (int i = 0; i < kBand; i++) {
-      rows[6 + i] = fix_row(y0 + 3 + i, pf[i]);
-      put_row(y0 + 3 + i, rows[6 + i]);
-    }
+    for (int i = 0; i < kBand; i++) rows[6 + i] = fix_row(y0 + 3 + i, pf[i]);
     if (b > 0) {   // mask rows y0 - 1 .. y0 + kBand
 #pragma unroll
       for (int i = 0; i < 2; i++) m[i] = m[kBand + i];
@@ -236,12 +233,24 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 6; i++) w[i] = rows[kBand + i];
-    // zero this band's score rows and the row below them: on the last band that row lies
-    // below the window and must read as zero (its ring slot held a row above y0 - 2, which no
-    // NMS of this band reads)
+    // the band window: raw rows y0 - 3 .. y0 + kBand + 2 at window rows 0 .. kBand + 5 (the
+    // previous band's reads of the window are all done: in-order LDS within the wave)
 #pragma unroll
-    for (int i = 0; i <= kBand; i++)
-      *reinterpret_cast<uint32_t*>(sc8 + (((y0 + i) & (kScoreRows - 1)) << 8) + 4 * lane) = 0u;
+    for (int i = 0; i < kBand + 6; i++) ring32[(i << 6) + lane] = rows[i];
+    raw_rel = ring_base - (uint32_t)((y0 - 3) << 8);
+    // score window rows y0 - 2 .. y0 + kBand: the previous band's rows y0 - 2, y0 - 1 (its
+    // window rows kBand, kBand + 1) move to rows 0, 1; this band's rows and the row below them
+    // are zeroed (on the last band that row lies below the detection window and must read 0)
+    if (b > 0) {
+      const uint32_t c0 = *reinterpret_cast<const uint32_t*>(sc8 + 256 * kBand + 4 * lane);
+      const uint32_t c1 = *reinterpret_cast<const uint32_t*>(sc8 + 256 * (kBand + 1) + 4 * lane);
+      dev::wave_sync();
+      *reinterpret_cast<uint32_t*>(sc8 + 4 * lane) = c0;
+      *reinterpret_cast<uint32_t*>(sc8 + 256 + 4 * lane) = c1;
+#pragma unroll
+      for (int i = 2; i < kScoreRows; i++) *reinterpret_cast<uint32_t*>(sc8 + 256 * i + 4 * lane) = 0u;
+    }
+    sc_rel = sc_base - (uint32_t)((y0 - 2) << 8);
 
     // A band whose mask rows y0 - 1 .. y0 + kBand are all zero emits nothing, and nothing it
     // scores is read by an NMS that can emit (the neighbour bands' corners on rows y0 - 1 and
@@ -270,8 +279,8 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     for (int i = 0; i < kBand; i++) {
       const int y = y0 + i;
       const uint32_t c1 = rows[i + 3], up = rows[i] /* q8 */, dn = rows[i + 6] /* q0 */;
-      const uint32_t L = __builtin_amdgcn_update_dpp(0u, c1, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
-      const uint32_t R = __builtin_amdgcn_update_dpp(0u, c1, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
+      const uint32_t L = (uint32_t)__builtin_amdgcn_mov_dpp((int)c1, 0x138 /*wave_shr:1*/, 0xF, 0xF, true);
+      const uint32_t R = (uint32_t)__builtin_amdgcn_mov_dpp((int)c1, 0x130 /*wave_shl:1*/, 0xF, 0xF, true);
       const uint32_t rt = __builtin_amdgcn_alignbyte(R, c1, 3u);   // q4: x+3..x+6
       const uint32_t lf = __builtin_amdgcn_alignbyte(c1, L, 1u);   // q12: x-3..x
       const uint32_t nv = ~c1;
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       for (int j0 = 0; j0 < ns; j0 += 64) {
         const int ja = j0 + lane;
         const int ea = list[ncarry + min(ja, ns - 1)];
-        const int s1 = fast_small<PAT == 16 ? 12 : PAT>(lds, ring_base, ea, t);
+        const int s1 = fast_small<PAT == 16 ? 12 : PAT>(lds, raw_rel, ea, t);
         const bool ca = ja < ns && s1 > 0;
         if (ca) sc_at(ea, 0, 0) = (uint8_t)s1;
         const uint64_t bal_a = __ballot(ca);
@@ -331,15 +340,12 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     for (int j0 = 0; PAT == 16 && j0 < ns; j0 += 128) {
       const int ja = j0 + lane, jb = j0 + 64 + lane;
       const int ea = list[ncarry + min(ja, ns - 1)], eb = list[ncarry + min(jb, ns - 1)];
-      // ring rows y-3 .. y+3 of both survivors, pointing at column x - 3
-      uint32_t ra[7], rb[7];
-#pragma unroll
-      for (int i = 0; i < 7; i++) {
-        ra[i] = ((uint32_t)(ea + (i - 3) * 256 - 3) & 0xFFFu) | ring_base;
-        rb[i] = ((uint32_t)(eb + (i - 3) * 256 - 3) & 0xFFFu) | ring_base;
-      }
+      // band-window bytes of both survivors' (y - 3, x - 3): the 7 x 7 neighbourhood is at
+      // immediate offsets from them
+      const uint8_t* const pa0 = lds + (raw_rel + (uint32_t)ea - 3u * 256u - 3u);
+      const uint8_t* const pb0 = lds + (raw_rel + (uint32_t)eb - 3u * 256u - 3u);
       auto pix = [&](int dy, int dx) -> h2 {
-        const uint32_t pa = lds[ra[dy + 3] + dx + 3], pb = lds[rb[dy + 3] + dx + 3];
+        const uint32_t pa = pa0[(dy + 3) * 256 + dx + 3], pb = pb0[(dy + 3) * 256 + dx + 3];
         return __builtin_bit_cast(h2, pa | (pb << 16));
       };
       h2 p[16];
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       p[4] = pix(0, 3);   p[5] = pix(-1, 3);  p[6] = pix(-2, 2);  p[7] = pix(-3, 1);
       p[8] = pix(-3, 0);  p[9] = pix(-3, -1); p[10] = pix(-2, -2); p[11] = pix(-1, -3);
       p[12] = pix(0, -3); p[13] = pix(1, -3); p[14] = pix(2, -2); p[15] = pix(3, -1);
-      const int va = lds[ra[3] + 3], vb = lds[rb[3] + 3];
+      const int va = pa0[3 * 256 + 3], vb = pb0[3 * 256 + 3];
       h2 mx[16], mn[16];
 #pragma unroll
       for (int k = 0; k < 16; k++) {

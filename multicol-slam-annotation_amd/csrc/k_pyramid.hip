@@ -77,7 +77,8 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
       // the right neighbour is read at sx + 1 even where resize clamps it to sx (the last
       // source column): alpha1 is 0 there, and sx + 1 stays inside the staged LDS row
       sx[k] = min(max(a.xofs[p] - c_lo, 0), c_hi - c_lo);
-      aa[k] = (uint32_t)(uint16_t)a.alpha[2 * p] | ((uint32_t)(uint16_t)a.alpha[2 * p + 1] << 16);
+      // alpha << 4 (alpha <= 2048, so <= 32768 still fits u16): the dot product is s << 4
+      aa[k] = ((uint32_t)(uint16_t)a.alpha[2 * p] | ((uint32_t)(uint16_t)a.alpha[2 * p + 1] << 16)) << 4;
       simd |= (p < a.simd_end) << k;
     }
   } else {
@@ -128,44 +129,46 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
   uint32_t win[5][2];   // packed u16 5-sums of raw rows r-4..r (win[4] = newest)
 #pragma unroll
   for (int i = 0; i < 5; i++) win[i][0] = win[i][1] = 0;
-  int next_emit = seg0;
-  // blurred row y from the window of raw rows r-4..r (r = y+2, or r = dh-1 for the last two
-  // rows); BORDER_REFLECT_101 at the top / bottom folds mirrored rows into window weights
-  // (row -1 = row 1, row -2 = row 2, row dh = row dh-2, row dh+1 = row dh-3)
-  auto emit = [&](int y, int r) {
-    (void)r;
-    uint32_t s01, s23;
-    if (y >= 2 && y + 2 <= dh - 1) {   // interior row (wave-uniform): plain 5-row sum
-      s01 = (win[0][0] + win[1][0] + win[2][0]) + (win[3][0] + win[4][0]);
-      s23 = (win[0][1] + win[1][1] + win[2][1]) + (win[3][1] + win[4][1]);
-    } else {
-      // the two top / bottom rows: window weights (2 bits each, row r-4 first) fold the
-      // mirrored rows in; weight * sum by selects and a shift (no 32-bit multiply)
-      const uint32_t wts = y == 0 ? 0x22100u                          // rows 2 1 0 1 2
-                         : y == 1 ? 0x11210u                          // rows 1 0 1 2 3
-                         : y == dh - 2 ? 0x12110u                     // rows dh-4..dh-1, dh-2
-                         : 0x12200u;                                  // dh-3 dh-2 dh-1 dh-2 dh-3
-      s01 = 0; s23 = 0;
-#pragma unroll
-      for (int i = 0; i < 5; i++) {
-        const uint32_t wi = (wts >> (4 * i)) & 15u;   // 0, 1 or 2
-        s01 += (wi & 1u ? win[i][0] : 0u) + (wi & 2u ? win[i][0] << 1 : 0u);
-        s23 += (wi & 1u ? win[i][1] : 0u) + (wi & 2u ? win[i][1] << 1 : 0u);
-      }
-    }
+  // blurred row y from the window sums: (2s + 25) / 50 = (s * 671090 + 8388625) >> 24 for
+  // s <= 25 * 255 (exhaustively checked, tests/test_oracle_cpu.py), the quotient is the top
+  // byte, and v_perm packs the four top bytes
+  auto store_blur = [&](int y, uint32_t s01, uint32_t s23) {
     if (core_lane) {
-      const uint32_t o = div50(2 * (s01 & 0xFFFF) + 25) | (div50(2 * (s01 >> 16) + 25) << 8) |
-                         (div50(2 * (s23 & 0xFFFF) + 25) << 16) | (div50(2 * (s23 >> 16) + 25) << 24);
-      *reinterpret_cast<uint32_t*>(blrf + (int64_t)y * a.bpitch + xb) = o;
+      const uint32_t q0 = (s01 & 0xFFFFu) * 671090u + 8388625u, q1 = (s01 >> 16) * 671090u + 8388625u;
+      const uint32_t q2 = (s23 & 0xFFFFu) * 671090u + 8388625u, q3 = (s23 >> 16) * 671090u + 8388625u;
+      const uint32_t o = __builtin_amdgcn_perm(q1, q0, 0x0C0C0703u) | __builtin_amdgcn_perm(q3, q2, 0x07030C0Cu);
+      *reinterpret_cast<uint32_t*>(dev::uniform_ptr(blrf + (int64_t)y * a.bpitch) + (uint32_t)xb) = o;
     }
   };
+  // interior row y = r - 2 (2 <= y <= dh - 3): plain 5-row sum of the window
+  auto emit_interior = [&](int y) {
+    store_blur(y, (win[0][0] + win[1][0] + win[2][0]) + (win[3][0] + win[4][0]),
+               (win[0][1] + win[1][1] + win[2][1]) + (win[3][1] + win[4][1]));
+  };
+  // the two top / bottom rows: BORDER_REFLECT_101 folds mirrored rows into window weights
+  // (2 bits each, row r-4 first; row -1 = row 1, row -2 = row 2, row dh = row dh-2,
+  // row dh+1 = row dh-3); weight * sum by selects and a shift (no 32-bit multiply)
+  auto emit_border = [&](int y) {
+    const uint32_t wts = y == 0 ? 0x22100u                          // rows 2 1 0 1 2
+                       : y == 1 ? 0x11210u                          // rows 1 0 1 2 3
+                       : y == dh - 2 ? 0x12110u                     // rows dh-4..dh-1, dh-2
+                       : 0x12200u;                                  // dh-3 dh-2 dh-1 dh-2 dh-3
+    uint32_t s01 = 0, s23 = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint32_t wi = (wts >> (4 * i)) & 15u;   // 0, 1 or 2
+      s01 += (wi & 1u ? win[i][0] : 0u) + (wi & 2u ? win[i][0] << 1 : 0u);
+      s23 += (wi & 1u ? win[i][1] : 0u) + (wi & 2u ? win[i][1] << 1 : 0u);
+    }
+    store_blur(y, s01, s23);
+  };
   auto push_row = [&](int r, uint32_t v) {
-    if (RESIZE && core_lane && r >= seg0 && r < seg1)
-      *reinterpret_cast<uint32_t*>(dstf + (int64_t)r * a.dpitch + xb) = v;
-    // lane neighbours by DPP wave shifts (VALU, no LDS round trip); lane 0 / 63 get 0, and
-    // those lanes are halo lanes whose blurred output is never stored
-    const uint32_t L = __builtin_amdgcn_update_dpp(0u, v, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
-    const uint32_t R = __builtin_amdgcn_update_dpp(0u, v, 0x130 /*wave_shl:1*/, 0xF, 0xF, false);
+    if (RESIZE && core_lane && r >= seg0 && r < seg1)   // row base uniform, lane offset >= 0
+      *reinterpret_cast<uint32_t*>(dev::uniform_ptr(dstf + (int64_t)r * a.dpitch) + (uint32_t)xb) = v;
+    // lane neighbours by DPP wave shifts (VALU, no LDS round trip); lane 0 / 63 read 0
+    // (bound_ctrl), and those lanes are halo lanes whose blurred output is never stored
+    const uint32_t L = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138 /*wave_shr:1*/, 0xF, 0xF, true);
+    const uint32_t R = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130 /*wave_shl:1*/, 0xF, 0xF, true);
     const uint32_t sc = __builtin_amdgcn_sad_u8(v, 0u, 0u);
     const uint32_t l2 = (L >> 16) & 0xFF, l3 = L >> 24, c0 = v & 0xFF, c3 = v >> 24;
     const uint32_t r0 = R & 0xFF, r1 = (R >> 8) & 0xFF;
@@ -174,8 +177,17 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
     for (int i = 0; i < 4; i++) { win[i][0] = win[i + 1][0]; win[i][1] = win[i + 1][1]; }
     win[4][0] = h0 | (h1 << 16);
     win[4][1] = h2 | (h3 << 16);
-    const int upto = (r == dh - 1) ? dh - 1 : r - 2;
-    for (; next_emit <= upto && next_emit < seg1; next_emit++) emit(next_emit, r);
+    // blurred row y = r - 2 once rows y-2 .. y+2 are in (all wave-uniform); the last row of
+    // the level also closes the two bottom rows
+    const int y = r - 2;
+    if (y >= seg0 && y < seg1) {
+      if (y >= 2 && y <= dh - 3) emit_interior(y);
+      else emit_border(y);
+    }
+    if (r == dh - 1) {
+      if (dh - 2 >= seg0 && dh - 2 < seg1 && dh - 2 > y) emit_border(dh - 2);
+      if (dh - 1 >= seg0 && dh - 1 < seg1 && dh - 1 > y) emit_border(dh - 1);
+    }
   };
   auto pack4 = [&](const int (&h)[4]) {
     return (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
@@ -212,29 +224,56 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
     // wave-uniform: every pixel of the strip (mirrors included) is in the SSE2 range (all
     // strips but the one holding the scalar tail), so the per-pixel select disappears
     const bool wave_sse = __ballot(simd != 15) == 0;
+    // hcur / hprev: horizontal sums s << 4 of the two newest source rows (the alphas are
+    // pre-shifted); xcur / xprev: their SSE2 operands (s >> 4) << 8 = (s << 4) & ~0xFF
     int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
+    uint32_t xprev[4] = {0, 0, 0, 0}, xcur[4] = {0, 0, 0, 0};
     int r = r_begin;
     uint32_t tr = row_tab(r);
     auto consume = [&](int sr, const uint32_t (&v)[NDW]) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) hprev[k] = hcur[k];
+      for (int k = 0; k < 4; k++) { hprev[k] = hcur[k]; xprev[k] = xcur[k]; }
       stage_and_gather(sr, v, hcur);
-      while (r < r_end && (int)(tr >> 16) == sr) {
-        const bool same = (int)(tr & 0xFFFF) == sr;
-        const uint32_t bb = row_beta(r);
-        const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
-        int o[4];
-        if (wave_sse) {
+      // two copies of the row loop, so that nothing of the scalar form is hoisted into the
+      // SSE2 one (wave-uniform choice)
+      if (wave_sse) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) xcur[k] = (uint32_t)hcur[k] & 0x00FFFF00u;   // hcur < 2^24
+        while (r < r_end && (int)(tr >> 16) == sr) {
+          const bool same = (int)(tr & 0xFFFF) == sr;
+          const uint32_t bb = row_beta(r);
+          // SSE2 form as (x0 b0 >> 16) = mulhi_u24(x0 << 8, b0 << 8) (sse_vres8); b in [0, 2048]
+          const uint32_t B0 = (bb & 0xFFFFu) << 8, B1 = (bb >> 16) << 8;
+          // both taps on this source row (the clamped edge rows, rare): xprev takes its value,
+          // and every later output row of this source row is such a row too.  The empty asm
+          // keeps this a scalar branch: if-converted, the selects would also hide the 24-bit
+          // operand range and turn the products into quarter-rate v_mul_hi_u32
+          if (same) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 4; k++) xprev[k] = xcur[k];
+          }
+          int o[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) o[k] = (int)sse_vres8(xprev[k], xcur[k], B0, B1);
+          push_row(r, pack4(o));
+          r++;
+          if (r < r_end) tr = row_tab(r);
+        }
+      } else {
+        asm volatile("" ::: "memory");   // nothing of this form is speculated into the SSE2 loop
+        while (r < r_end && (int)(tr >> 16) == sr) {
+          const bool same = (int)(tr & 0xFFFF) == sr;
+          const uint32_t bb = row_beta(r);
+          const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
+          int o[4];
 #pragma unroll
           for (int k = 0; k < 4; k++)
-            o[k] = vres_sse(sse_x(same ? hcur[k] : hprev[k]), sse_x(hcur[k]), b0, b1);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; k++) o[k] = vres(same ? hcur[k] : hprev[k], hcur[k], b0, b1, (simd >> k) & 1);
+            o[k] = vres((same ? hcur[k] : hprev[k]) >> 4, hcur[k] >> 4, b0, b1, (simd >> k) & 1);
+          push_row(r, pack4(o));
+          r++;
+          if (r < r_end) tr = row_tab(r);
         }
-        push_row(r, pack4(o));
-        r++;
-        if (r < r_end) tr = row_tab(r);
       }
     };
 #pragma unroll

@@ -26,6 +26,19 @@ __device__ __forceinline__ int vres_sse(uint32_t x0, uint32_t y0, int b0, int b1
   const uint32_t t = ((x0 * ((uint32_t)b0 & 0xFFFu)) >> 16) + ((y0 * ((uint32_t)b1 & 0xFFFu)) >> 16);
   return (int)min(255u, (t + 2u) >> 2);
 }
+// The SSE2 form with both products as one v_mul_hi_u32_u24 each: with X = x0 << 8 (< 2^24 for
+// x0 <= 32640) and B = b << 8 (<= 2^19), X * B >> 32 = x0 * b >> 16 exactly; the sum of the two
+// terms is <= 1020, so (t + 2) >> 2 <= 255 and the u8 clamp is a no-op.
+// (written as the instruction: left to the 64-bit pattern, a loop-carried operand whose range
+// the compiler cannot see becomes v_mul_lo_u32 + v_mul_hi_u32 + v_mad_u64_u32, quarter rate)
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a_vgpr, uint32_t b_sgpr) {
+  uint32_t d;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(d) : "s"(b_sgpr), "v"(a_vgpr));
+  return d;
+}
+__device__ __forceinline__ uint32_t sse_vres8(uint32_t X0, uint32_t Y0, uint32_t B0, uint32_t B1) {
+  return (mulhi_u24(X0, B0) + mulhi_u24(Y0, B1) + 2u) >> 2;
+}
 __device__ __forceinline__ int vres_fixed(int s0, int s1, int b0, int b1) {
   const uint32_t u0 = __builtin_amdgcn_ubfe((uint32_t)s0, 0, 20), u1 = __builtin_amdgcn_ubfe((uint32_t)s1, 0, 20);
   return (int)min(255u, (u0 * ((uint32_t)b0 & 0xFFFu) + u1 * ((uint32_t)b1 & 0xFFFu) + (1u << 21)) >> 22);

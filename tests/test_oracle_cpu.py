@@ -136,3 +136,29 @@ def test_library_reports_no_device_on_cpu_host(built):
         pytest.skip("GPU present")
     with pytest.raises(mcs_amd.McsError):
         mcs_amd.Extractor(mcs_amd.ExtractorParams(), 754, 480)
+
+
+def test_pyramid_fixed_point_forms_are_exact():
+    """The integer rewrites k_pyr_rows relies on, checked over their whole operand ranges
+    (csrc/pyr_math.hpp, csrc/k_pyramid.hip):
+      * box blur: (2s + 25) // 50 == (s * 671090 + 8388625) >> 24 for every 5x5 sum s of u8,
+        with no 32-bit overflow (the quotient is the top byte);
+      * SSE2 vertical resize: (x0 * b) >> 16 == ((x0 << 8) * (b << 8)) >> 32 with both
+        operands < 2^24 (v_mul_hi_u32_u24), x0 = s >> 4 for s = p0 a0 + p1 a1, p <= 255,
+        a0 + a1 = 2048, b in [0, 2048]; and x0 << 8 == (s << 4) & ~0xFF."""
+    s = np.arange(0, 25 * 255 + 1, dtype=np.int64)
+    q = s * 671090 + 8388625
+    assert q.max() < 2 ** 32
+    assert np.array_equal(q >> 24, (2 * s + 25) // 50)
+    rng = np.random.default_rng(0)
+    p = rng.integers(0, 256, size=(2, 200000), dtype=np.int64)
+    a0 = rng.integers(0, 2049, size=200000, dtype=np.int64)
+    sv = p[0] * a0 + p[1] * (2048 - a0)
+    sv = np.concatenate([sv, [0, 255 * 2048]])
+    x0 = sv >> 4
+    X = (sv << 4) & ~0xFF
+    assert np.array_equal(X, x0 << 8) and X.max() < 2 ** 24
+    for b in (0, 1, 2, 511, 1024, 1707, 2047, 2048):
+        assert np.array_equal((X * (b << 8)) >> 32, (x0 * b) >> 16)
+    # and the sum of the two taps never needs the u8 clamp
+    assert ((x0.max() * 2048) >> 16) <= 1020
