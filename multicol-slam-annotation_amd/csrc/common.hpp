@@ -38,12 +38,16 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // lgkmcnt and every LDS wait would then wait for it).
 // a wave-uniform pointer moved to SGPRs: stores / loads through it + a 32-bit lane offset use
 // the saddr form (no 64-bit address arithmetic per lane)
+// (rebuilt as a global-address-space pointer: from a plain integer the compiler would treat it
+// as generic and emit flat instructions, which also count against lgkmcnt)
 template <typename T>
 __device__ __forceinline__ T* uniform_ptr(T* p) {
+  typedef __attribute__((address_space(1))) T GT;
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+  GT* g = (GT*)(((uint64_t)hi << 32) | lo);
+  return (T*)g;
 }
 __device__ __forceinline__ const uint32_t* align_down4(const uint8_t* p) {
   return reinterpret_cast<const uint32_t*>(p - ((uintptr_t)p & 3));

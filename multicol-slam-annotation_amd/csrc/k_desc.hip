@@ -91,6 +91,17 @@ __device__ __forceinline__ int rot_round(double px, double py, double ca, double
   return xaxis ? (int)rint(__dsub_rn(__dmul_rn(px, ca), __dmul_rn(py, sa)))
                : (int)rint(__dadd_rn(__dmul_rn(px, sa), __dmul_rn(py, ca)));
 }
+// the same rounding as one add: for |v| < 2^51, v + 1.5 * 2^52 rounds v to an integer in the
+// current (nearest-even) mode, and that integer, two's complement, is the low word of the sum
+__device__ __forceinline__ int rint_magic(double v) {
+  return (int)__double2loint(__dadd_rn(v, 6755399441055744.0));
+}
+__device__ __forceinline__ int rot_x(double px, double py, double ca, double sa) {
+  return rint_magic(__dsub_rn(__dmul_rn(px, ca), __dmul_rn(py, sa)));
+}
+__device__ __forceinline__ int rot_y(double px, double py, double ca, double sa) {
+  return rint_magic(__dadd_rn(__dmul_rn(px, sa), __dmul_rn(py, ca)));
+}
 
 // Both patches (raw r=16 for the moments, blurred r=21 for the rotated pattern) are staged
 // into LDS with aligned dword loads right after the keypoint is known, so a keypoint costs
@@ -173,6 +184,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   // (one per test round) instead of LDS reads
   __shared__ uint32_t s_icw[2][kRawH * kRawW];
   __shared__ uint32_t s_pat[512];
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
   // wave index as a scalar: the pair, its level and counts are wave-uniform
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
@@ -202,57 +215,72 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   const int cx = (int)(pk & 0xFFF) + kMinBorder, cy = (int)((pk >> 12) & 0xFFF) + kMinBorder;
   const int score = (int)(pk >> 24);
   const int pitch = L.pitch, bp = L.bpitch;
-  const uint8_t* img = (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride
-                                : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off;
-  const uint8_t* blr = a.blur + (int64_t)f * a.blur_fstride + L.img_off;
-  // ---- raw patch into registers, blurred patch into LDS (independent loads, issued together)
+  // frame / level bases are wave-uniform (both keypoints of a wave share frame and level):
+  // SGPR bases + 32-bit lane offsets, no 64-bit address arithmetic per load
+  const uint8_t* const img = dev::uniform_ptr(
+      (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off);
+  const uint8_t* const blr = dev::uniform_ptr(a.blur + (int64_t)f * a.blur_fstride + L.img_off);
+  // ---- raw patch: dword q = hl + 32k (row q / 9, column q % 9) of the 33 x 9 dwords per
+  // lane, consecutive lanes on consecutive dwords (coalesced); blurred patch into LDS
+  // (independent loads, issued together).  Offsets are 32-bit from the uniform bases: with
+  // r = q / 9 = (57 q) >> 9 (exact for q < 320), the dword's byte offset is
+  // r (pitch - 36) + 4 q + the patch origin.
   const int mis = (cx - 21) & kBlrAlign;
   uint32_t raw[10];
+  uint32_t rq[10];
   {
-    const uint8_t* r0 = img + (int64_t)(cy - kHalfPatch) * pitch + (cx - kHalfPatch);
+    const uint32_t o0 = (uint32_t)((cy - kHalfPatch) * pitch + (cx - kHalfPatch)) + 4u * (uint32_t)hl;
+    const uint32_t pm = (uint32_t)(pitch - 4 * kRawW);
+#pragma unroll
+    // every load is unconditional (lanes past the patch re-read its last dword / chunk, unused):
+    // a register loaded on one path only would be merged after a wait for all loads in flight
+    for (int k = 0; k < 10; k++) {
+      const uint32_t q = (uint32_t)(hl + 32 * k);
+      rq[k] = (q * 57u) >> 9;
+      const uint32_t qc = min(q, (uint32_t)(kRawH * kRawW - 1));
+      const uint32_t off = ((qc * 57u) >> 9) * pm + o0 + 4u * (qc - (uint32_t)hl);
+      const uint32_t* ap = reinterpret_cast<const uint32_t*>(img + (off & ~3u));
+      raw[k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], off & 3u);
+    }
+    const uint32_t bo = (uint32_t)((cy - 21) * bp + (cx - 21 - mis));
+    uint4 bv[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {      // chunk q = hl + 32k: row q >> 2, 16-byte chunk q & 3
+      const int qc = min(hl + 32 * k, kBlrH * 4 - 1);
+      bv[k] = *reinterpret_cast<const uint4*>(blr + (bo + (uint32_t)((qc >> 2) * bp + 16 * (qc & 3))));
+    }
+    uint8_t* const sb = &s_blr[slot][(hl >> 2) * kBlrRow + 16 * (hl & 3)];
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+      if (hl + 32 * k < kBlrH * 4) *reinterpret_cast<uint4*>(sb + 8 * k * kBlrRow) = bv[k];
+  }
+  dev::wave_sync();
+  // ---- IC_Angle: integer moments over the circular r=16 patch (see c_icw; exact integer
+  // sums): m10 = sum (u+16) I - 16 S, m01 = sum (v+16) I - 16 S with v + 16 = the row
+  float angle;
+  {
+    uint32_t a10 = 0, aS = 0, a01 = 0;
 #pragma unroll
     for (int k = 0; k < 10; k++) {
       const int q = hl + 32 * k;
-      raw[k] = 0u;
       if (q < kRawH * kRawW) {
-        const int r = q / kRawW, c = q - kRawW * r;
-        raw[k] = load_aligned_dword(r0 + (int64_t)r * pitch + 4 * c);
+        a10 = __builtin_amdgcn_udot4(s_icw[0][q], raw[k], a10, false);
+        const uint32_t d0 = __builtin_amdgcn_udot4(s_icw[1][q], raw[k], 0u, false);
+        aS += d0;
+        a01 += rq[k] * d0;
       }
     }
-    const uint8_t* b0 = blr + (int64_t)(cy - 21) * bp + (cx - 21 - mis);
-#ifndef MCS_DESC_BLR48
+    int S = (int)aS, m10 = (int)a10, m01 = (int)a01;
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int q = hl + 32 * k;        // chunk q: row q >> 2, 16-byte chunk q & 3
-      if (q < kBlrH * 4) {
-        const uint4 v = *reinterpret_cast<const uint4*>(b0 + (int64_t)(q >> 2) * bp + 16 * (q & 3));
-        *reinterpret_cast<uint4*>(&s_blr[slot][(q >> 2) * kBlrRow + 16 * (q & 3)]) = v;
-      }
+    for (int o = 16; o > 0; o >>= 1) {
+      S += __shfl_xor(S, o, 64);
+      m10 += __shfl_xor(m10, o, 64);
+      m01 += __shfl_xor(m01, o, 64);
     }
-#else
-    uint32_t bv[17];
-#pragma unroll
-    for (int k = 0; k < 17; k++) {      // dword q: row q / 12, dword q % 12
-      const int q = hl + 32 * k;
-      bv[k] = 0u;
-      if (q < kBlrH * 12) {
-        const int r = q / 12, c = q - 12 * r;
-        bv[k] = *reinterpret_cast<const uint32_t*>(b0 + (int64_t)r * bp + 4 * c);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 17; k++) {
-      const int q = hl + 32 * k;
-      if (q < kBlrH * 12) {
-        const int r = q / 12, c = q - 12 * r;
-        *reinterpret_cast<uint32_t*>(&s_blr[slot][r * kBlrRow + 4 * c]) = bv[k];
-      }
-    }
-#endif
+    m10 -= kHalfPatch * S;
+    m01 -= kHalfPatch * S;
+    angle = fast_atan2_dev((float)m01, (float)m10);
   }
-  dev::wave_sync();
-  // ---- IC_Angle: integer moments over the circular r=16 patch
-  const float angle = ic_angle_regs(raw, hl, s_icw[0], s_icw[1]);
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const double theta = (double)__fmul_rn(angle, DEG2RADf);
@@ -266,8 +294,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
     const uint32_t pw = s_pat[t];
     const double px0 = (double)(int)(int8_t)(pw & 0xFF), py0 = (double)(int)(int8_t)((pw >> 8) & 0xFF);
     const double px1 = (double)(int)(int8_t)((pw >> 16) & 0xFF), py1 = (double)(int)(int8_t)(pw >> 24);
-    const int o0 = rot_round(px0, py0, ca, sa, false) * kBlrRow + rot_round(px0, py0, ca, sa, true);
-    const int o1 = rot_round(px1, py1, ca, sa, false) * kBlrRow + rot_round(px1, py1, ca, sa, true);
+    const int o0 = rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa);
+    const int o1 = rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa);
     const uint64_t b = __ballot(bc[o0] < bc[o1]);
     if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
   }

@@ -162,3 +162,15 @@ def test_pyramid_fixed_point_forms_are_exact():
         assert np.array_equal((X * (b << 8)) >> 32, (x0 * b) >> 16)
     # and the sum of the two taps never needs the u8 clamp
     assert ((x0.max() * 2048) >> 16) <= 1020
+
+
+def test_descriptor_integer_and_rounding_forms_are_exact():
+    """k_orient_desc (csrc/k_desc.hip): the raw-patch row of dword q is (57 q) >> 9 == q // 9
+    for every lane's q < 320; and rint_magic(v) = low word of v + 1.5 * 2^52 equals rint(v)
+    (round half to even) for the rotated pattern coordinates, |v| <= 15 * sqrt(2)."""
+    q = np.arange(320)
+    assert np.array_equal((q * 57) >> 9, q // 9)
+    v = np.concatenate([np.arange(-25, 25.01, 0.25), np.random.default_rng(1).uniform(-22, 22, 100000)])
+    m = (v + 6755399441055744.0).view(np.int64) & 0xFFFFFFFF
+    m = np.where(m >= 2 ** 31, m - 2 ** 32, m)
+    assert np.array_equal(m, np.rint(v).astype(np.int64))
