@@ -170,10 +170,33 @@ __device__ __forceinline__ v4i expand16(uint32_t bits) {
   return r;
 }
 
+// KEYED form (every train index < 2^13): the matrix cores produce the top-2 key up to the
+// train index.  Train bits map to -64 (set) / +64 (clear), query bits to +64 (set) / -64
+// (clear), so the product sum is -4096 (256 - 2 Hamming) = 2^13 Hamming - 2^20, and
+// key = sum + (2^20 + tile base) + the row's offset (one v_add3, the offset an inline constant)
+// = 2^13 Hamming + train index, ordered as (Hamming, train index) by min / med3 (< 2^22).
+__device__ __forceinline__ uint32_t expand4_64(uint32_t nib) {   // set -> 0xC0, clear -> 0x40
+  const uint32_t m = (nib * 0x00204081u) & 0x01010101u;
+  return (m << 7) | 0x40404040u;
+}
+__device__ __forceinline__ v4i expand16_64(uint32_t bits) {
+  v4i r;
+  r.x = (int)expand4_64(bits & 0xF);
+  r.y = (int)expand4_64((bits >> 4) & 0xF);
+  r.z = (int)expand4_64((bits >> 8) & 0xF);
+  r.w = (int)expand4_64((bits >> 12) & 0xF);
+  return r;
+}
+constexpr int kKeyBits = 13;
+
 constexpr int kMfTileT = 64;            // trains per LDS tile
 constexpr int kMfPitch = 256 + 16;      // expanded train row (bytes), padded against bank conflicts
 
-__global__ __launch_bounds__(256) void k_top2_mfma32(
+#ifndef MCS_TOP2_MINB
+#define MCS_TOP2_MINB 4   // 128 VGPRs, accumulators in VGPRs (no AGPR reads); measured 0.47 -> 0.44 ms
+#endif
+template <bool KEYED>
+__global__ __launch_bounds__(256, MCS_TOP2_MINB) void k_top2_mfma32(
     const uint8_t* __restrict__ qbase, const uint8_t* __restrict__ tbase,
     const int32_t* __restrict__ counts, const int32_t* __restrict__ pairs, int64_t set_stride,
     int nq_fixed, int nt_fixed, int cap_out, int32_t* __restrict__ best_idx,
@@ -207,7 +230,8 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
 #pragma unroll
     for (int s = 0; s < 8; s++) w[s] = qd[s];
 #pragma unroll
-    for (int s = 0; s < 8; s++) bq[c][s] = expand16((w[s] >> (16 * h)) & 0xFFFF);
+    for (int s = 0; s < 8; s++)   // KEYED: query set -> +64, i.e. the train map of ~bits
+      bq[c][s] = KEYED ? expand16_64(~(w[s] >> (16 * h)) & 0xFFFF) : expand16((w[s] >> (16 * h)) & 0xFFFF);
   }
   uint32_t k1[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, k2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
   // train tile bits, one tile ahead: the next tile's loads are in flight while this one is
@@ -234,7 +258,8 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
       const int tr = e >> 3, dw = e & 7;
       const uint32_t bits = cb[r];
       uint8_t* dst = s_t + tr * kMfPitch + dw * 32;
-      const v4i lo = expand16(bits & 0xFFFF), hi = expand16(bits >> 16);
+      const v4i lo = KEYED ? expand16_64(bits & 0xFFFF) : expand16(bits & 0xFFFF);
+      const v4i hi = KEYED ? expand16_64(bits >> 16) : expand16(bits >> 16);
       *reinterpret_cast<v4i*>(dst) = lo;
       *reinterpret_cast<v4i*>(dst + 16) = hi;
     }
@@ -243,6 +268,7 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
 #pragma unroll
     for (int st = 0; st < 2; st++) {
       if (st * 32 >= ntile) break;
+      const int tb = t0 + st * 32 + 4 * h;
       v16i acc0 = {0}, acc1 = {0};
       const uint8_t* arow = s_t + (st * 32 + col) * kMfPitch + 16 * h;
 #pragma unroll
@@ -251,8 +277,30 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
         acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[0][s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[1][s], acc1, 0, 0, 0);
       }
-      const int tb = t0 + st * 32 + 4 * h;
       const bool full = st * 32 + 32 <= ntile;
+      if (KEYED) {
+        const uint32_t tbk = (uint32_t)tb + (1u << 20);
+        uint32_t key0[16], key1[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          key0[r] = (uint32_t)acc0[r] + tbk + (uint32_t)((r & 3) + 8 * (r >> 2));
+          key1[r] = (uint32_t)acc1[r] + tbk + (uint32_t)((r & 3) + 8 * (r >> 2));
+        }
+        if (!full) {   // the last, partial tile (a scalar branch: no selects in full tiles)
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int r = 0; r < 16; r++)
+            if (tb + (r & 3) + 8 * (r >> 2) >= nt) { key0[r] = 0xFFFFFFFFu; key1[r] = 0xFFFFFFFFu; }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          k2[0] = med3_u32(k1[0], key0[r], k2[0]);
+          k1[0] = min(k1[0], key0[r]);
+          k2[1] = med3_u32(k1[1], key1[r], k2[1]);
+          k1[1] = min(k1[1], key1[r]);
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const int trow = tb + (r & 3) + 8 * (r >> 2);
@@ -276,10 +324,12 @@ __global__ __launch_bounds__(256) void k_top2_mfma32(
     if (h == 0 && qi < nq) {
       const int64_t o = (int64_t)p * cap_out + qi;
       const bool h1 = b1 != 0xFFFFFFFFu, h2 = b2 != 0xFFFFFFFFu;
-      best_idx[o] = h1 ? (int)(b1 & 0xFFFF) : -1;
-      best_dist[o] = h1 ? (int)(b1 >> 16) : none;
-      second_idx[o] = h2 ? (int)(b2 & 0xFFFF) : -1;
-      second_dist[o] = h2 ? (int)(b2 >> 16) : none;
+      constexpr int kIb = KEYED ? kKeyBits : 16;
+      constexpr uint32_t kIm = (1u << kIb) - 1u;
+      best_idx[o] = h1 ? (int)(b1 & kIm) : -1;
+      best_dist[o] = h1 ? (int)(b1 >> kIb) : none;
+      second_idx[o] = h2 ? (int)(b2 & kIm) : -1;
+      second_dist[o] = h2 ? (int)(b2 >> kIb) : none;
     }
   }
 }
@@ -445,7 +495,8 @@ int mcs_hamming_top2_device(const uint8_t* d_q, int32_t nq, const uint8_t* d_t, 
   if (nq <= 0) return MCS_OK;
   if (nt > 65535) { set_error("top2: at most 65535 train descriptors"); return MCS_ERR_ARG; }
   if (bytes == 32) {
-    hipLaunchKernelGGL(k_top2_mfma32, dim3((nq + 255) / 256, 1), dim3(256), 0, (hipStream_t)stream,
+    auto* kfn = nt <= (1 << kKeyBits) ? k_top2_mfma32<true> : k_top2_mfma32<false>;
+    hipLaunchKernelGGL(kfn, dim3((nq + 255) / 256, 1), dim3(256), 0, (hipStream_t)stream,
                        d_q, d_t, (const int32_t*)nullptr, (const int32_t*)nullptr, (int64_t)0, nq,
                        nt, nq, d_best_idx, d_best_dist, d_second_idx, d_second_dist);
     MCS_HIP_CHECK(hipGetLastError());
@@ -468,8 +519,9 @@ int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts
   if (n_pairs <= 0) return MCS_OK;
   if (!d_desc || !d_counts || !d_pairs || cap <= 0) return MCS_ERR_ARG;
   if (cap > 65535) { set_error("top2: capacity above 65535"); return MCS_ERR_ARG; }
-  if (bytes == 32) {
-    hipLaunchKernelGGL(k_top2_mfma32, dim3((cap + 255) / 256, n_pairs), dim3(256), 0,
+  if (bytes == 32) {   // a pair's train count is <= cap
+    auto* kfn = cap <= (1 << kKeyBits) ? k_top2_mfma32<true> : k_top2_mfma32<false>;
+    hipLaunchKernelGGL(kfn, dim3((cap + 255) / 256, n_pairs), dim3(256), 0,
                        (hipStream_t)stream, d_desc, d_desc, d_counts, d_pairs,
                        (int64_t)cap * bytes, 0, 0, cap, d_best_idx, d_best_dist, d_second_idx,
                        d_second_dist);
