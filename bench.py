@@ -66,6 +66,27 @@ def pmc_traffic(alg_bytes):
         return {}
 
 
+def sq_issue():
+    """VALU issue utilisation per SIMD of the pyramid + FAST kernels from the committed SQ pass
+    (tools/sq_summary.py --json: 4 * SQ_ACTIVE_INST_VALU / 1024 SIMDs / (SQ_BUSY_CYCLES / 32
+    SQs), MI355X_MICROARCH.md counter units).  These kernels are issue-bound, not HBM-bound:
+    this is the roofline that actually binds them."""
+    tf = os.path.join(ROOT, "profiles", "sq_issue.json")
+    if not os.path.exists(tf):
+        return {}
+    try:
+        d = json.load(open(tf))
+        k = d["kernels"]
+        out = {"method": d.get("method"), "source": d.get("source", tf)}
+        for name, key in (("k_pyr_rows<true, 2>", "pyramid"), ("k_fast_rows<16>", "fast"),
+                          ("k_orient_desc", "orient_desc"), ("k_top2_mfma32<true>", "match_mfma")):
+            if name in k:
+                out[key + "_valu_util"] = k[name]["valu_util"]
+        return {"issue": out}
+    except (KeyError, ValueError):
+        return {}
+
+
 def alg_bytes_pyr_fast(level_wh):
     """B = sum_{l>=1}(|L_{l-1}| + |L_l|) + sum_l |L_l|  (SURVEY.md §8(d))."""
     px = [int(w) * int(h) for w, h in level_wh]
@@ -620,6 +641,7 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": None, "alg_bytes_per_call": bpf * F}
         roofline.update(pmc_traffic(bpf * F))
+        roofline.update(sq_issue())
 
     # ---- LocalBA (config C): 10 local MultiKeyFrames + 3 fixed observers, 3k points, ~20k edges
     localba = None

@@ -40,6 +40,28 @@ if "SQ_LDS_IDX_ACTIVE" in next(iter(acc.values()), {}):
             k[:28], w, 100 * c.get("SQ_ACTIVE_INST_VALU", 0) / wc,
             bc / (idx - bc) if idx > bc else 0.0, c.get("SQ_LEVEL_WAVES", 0) / busy,
             c.get("SQ_INST_CYCLES_SALU", 0) / w))
+# Issue utilisation per SIMD (MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* count
+# quad-cycles; SQ_BUSY_CYCLES is summed over the 32 SQs (8 XCDs x 4 SEs) in cycles): a VALU
+# instruction occupies its SIMD for one quad-cycle, so
+#   valu_util = 4 * SQ_ACTIVE_INST_VALU / 1024 SIMDs / (SQ_BUSY_CYCLES / 32)
+# is the fraction of the kernel's busy time each SIMD spent issuing VALU (MFMA included).
+NSQ, NSIMD = 32, 1024
+if "SQ_BUSY_CYCLES" in next(iter(acc.values()), {}):
+    util = {}
+    print("%-28s %9s %10s" % ("kernel", "valu_util", "waves/SIMD"))
+    for k, c in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+        busy = c.get("SQ_BUSY_CYCLES", 0) / NSQ
+        if busy <= 0 or "SQ_ACTIVE_INST_VALU" not in c:
+            continue
+        u = 4 * c["SQ_ACTIVE_INST_VALU"] / NSIMD / busy
+        occ = 4 * c.get("SQ_WAVE_CYCLES", 0) / NSIMD / busy
+        util[k] = {"valu_util": round(u, 3), "waves_per_simd": round(occ, 2), "dispatches": len(cnt[k])}
+        print("%-28s %9.3f %10.2f" % (k[:28], u, occ))
+    for a in sys.argv:
+        if a.startswith("--json="):
+            import json
+            json.dump({"source": path, "method": "4*SQ_ACTIVE_INST_VALU/1024/(SQ_BUSY_CYCLES/32)",
+                       "kernels": util}, open(a[7:], "w"), indent=1)
 if "--all" in sys.argv:
     for k, c in sorted(acc.items()):
         if not k.startswith(("k_", "pyr", "fast", "ldlt", "ba::", "voc")) and "k_" not in k:
