@@ -602,11 +602,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if args.stage_timing:
-        ex.enable_timing(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    # timed region: the production path, no stage events between the kernels
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
@@ -616,7 +612,16 @@ def main():
     dt = time.perf_counter() - t0
     # matcher device time of the last step (events on the launch stream)
     match_ms_last = ev_m0.elapsed_time(ev_m1)
-    stages, ncalls = ex.read_timing() if args.stage_timing else ({}, 0)
+    # per-stage kernel times for the roofline: a few extra, untimed steps with the stage
+    # events on (which run the stages back to back on one stream)
+    stages, ncalls = {}, 0
+    if args.stage_timing:
+        ex.enable_timing(True)
+        for _ in range(max(2, min(5, args.steps))):
+            step(False)
+        torch.cuda.synchronize()
+        stages, ncalls = ex.read_timing()
+        ex.enable_timing(False)
 
     kp_per_step = int(d_cnt.sum().item())
     dt_max, kp_tot = reduce_over_ranks(dt, kp_per_step * args.steps, dev, world)
