@@ -8,6 +8,7 @@
 #include "common.hpp"
 #include "extractor_kernels.hpp"
 #include "pyr_math.hpp"
+#include <type_traits>
 
 namespace mcs {
 
@@ -224,70 +225,70 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
     // wave-uniform: every pixel of the strip (mirrors included) is in the SSE2 range (all
     // strips but the one holding the scalar tail), so the per-pixel select disappears
     const bool wave_sse = __ballot(simd != 15) == 0;
-    // hcur / hprev: horizontal sums s << 4 of the two newest source rows (the alphas are
-    // pre-shifted); xcur / xprev: their SSE2 operands (s >> 4) << 8 = (s << 4) & ~0xFF
-    int hprev[4] = {0, 0, 0, 0}, hcur[4] = {0, 0, 0, 0};
-    uint32_t xprev[4] = {0, 0, 0, 0}, xcur[4] = {0, 0, 0, 0};
-    int r = r_begin;
-    uint32_t tr = row_tab(r);
-    auto consume = [&](int sr, const uint32_t (&v)[NDW]) {
+    // Two instances of the row loop, one per vertical form (the wave-uniform choice is made once,
+    // so nothing of the scalar form is hoisted into the SSE2 loop).  The horizontal sums s << 4
+    // (alphas pre-shifted) and the SSE2 operands (s >> 4) << 8 = (s << 4) & ~0xFF of the two
+    // newest source rows ping-pong between register sets A and B by source-row parity (kPF is
+    // even), so no per-row copies.
+    static_assert(kPF % 2 == 0, "source-row ping-pong needs an even rows-in-flight count");
+    auto run = [&](auto sse_tag) {
+      constexpr bool SSE = decltype(sse_tag)::value;
+      int hA[4] = {0, 0, 0, 0}, hB[4] = {0, 0, 0, 0};
+      uint32_t xA[4] = {0, 0, 0, 0}, xB[4] = {0, 0, 0, 0};
+      int r = r_begin;
+      uint32_t tr = row_tab(r);
+      auto consume = [&](int sr, const uint32_t (&v)[NDW], int (&hc)[4], uint32_t (&xc)[4],
+                         int (&hp)[4], uint32_t (&xp)[4]) {
+        stage_and_gather(sr, v, hc);
+        if (SSE) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) { hprev[k] = hcur[k]; xprev[k] = xcur[k]; }
-      stage_and_gather(sr, v, hcur);
-      // two copies of the row loop, so that nothing of the scalar form is hoisted into the
-      // SSE2 one (wave-uniform choice)
-      if (wave_sse) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) xcur[k] = (uint32_t)hcur[k] & 0x00FFFF00u;   // hcur < 2^24
+          for (int k = 0; k < 4; k++) xc[k] = (uint32_t)hc[k] & 0x00FFFF00u;   // hc < 2^24
+        }
         while (r < r_end && (int)(tr >> 16) == sr) {
           const bool same = (int)(tr & 0xFFFF) == sr;
           const uint32_t bb = row_beta(r);
-          // SSE2 form as (x0 b0 >> 16) = mulhi_u24(x0 << 8, b0 << 8) (sse_vres8); b in [0, 2048]
-          const uint32_t B0 = (bb & 0xFFFFu) << 8, B1 = (bb >> 16) << 8;
-          // both taps on this source row (the clamped edge rows, rare): xprev takes its value,
-          // and every later output row of this source row is such a row too.  The empty asm
-          // keeps this a scalar branch: if-converted, the selects would also hide the 24-bit
-          // operand range and turn the products into quarter-rate v_mul_hi_u32
-          if (same) {
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < 4; k++) xprev[k] = xcur[k];
-          }
           int o[4];
+          if (SSE) {
+            // (x0 b0 >> 16) = mulhi_u24(x0 << 8, b0 << 8) (sse_vres8); b in [0, 2048]
+            const uint32_t B0 = (bb & 0xFFFFu) << 8, B1 = (bb >> 16) << 8;
+            // both taps on this source row (the clamped edge rows, rare): the previous set
+            // takes its value (every later output row of this source row is such a row too).
+            // The empty asm keeps this a scalar branch: if-converted, the selects would also
+            // hide the 24-bit operand range (quarter-rate v_mul_hi_u32)
+            if (same) {
+              asm volatile("" ::: "memory");
 #pragma unroll
-          for (int k = 0; k < 4; k++) o[k] = (int)sse_vres8(xprev[k], xcur[k], B0, B1);
+              for (int k = 0; k < 4; k++) xp[k] = xc[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) o[k] = (int)sse_vres8(xp[k], xc[k], B0, B1);
+          } else {
+            const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              o[k] = vres((same ? hc[k] : hp[k]) >> 4, hc[k] >> 4, b0, b1, (simd >> k) & 1);
+          }
           push_row(r, pack4(o));
           r++;
           if (r < r_end) tr = row_tab(r);
         }
-      } else {
-        asm volatile("" ::: "memory");   // nothing of this form is speculated into the SSE2 loop
-        while (r < r_end && (int)(tr >> 16) == sr) {
-          const bool same = (int)(tr & 0xFFFF) == sr;
-          const uint32_t bb = row_beta(r);
-          const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
-          int o[4];
+      };
 #pragma unroll
-          for (int k = 0; k < 4; k++)
-            o[k] = vres((same ? hcur[k] : hprev[k]) >> 4, hcur[k] >> 4, b0, b1, (simd >> k) & 1);
-          push_row(r, pack4(o));
-          r++;
-          if (r < r_end) tr = row_tab(r);
+      for (int u = 0; u < kPF; u++)
+        if (sr0 + u <= sr1) load_row(sr0 + u, pf[u]);
+      for (int sr = sr0; sr <= sr1; sr += kPF) {   // kPF source rows in flight
+#pragma unroll
+        for (int u = 0; u < kPF; u++) {
+          if (sr + u <= sr1) {
+            if (u & 1) consume(sr + u, pf[u], hB, xB, hA, xA);
+            else consume(sr + u, pf[u], hA, xA, hB, xB);
+            if (sr + u + kPF <= sr1) load_row(sr + u + kPF, pf[u]);
+          }
         }
       }
     };
-#pragma unroll
-    for (int u = 0; u < kPF; u++)
-      if (sr0 + u <= sr1) load_row(sr0 + u, pf[u]);
-    for (int sr = sr0; sr <= sr1; sr += kPF) {   // kPF source rows in flight
-#pragma unroll
-      for (int u = 0; u < kPF; u++) {
-        if (sr + u <= sr1) {
-          consume(sr + u, pf[u]);
-          if (sr + u + kPF <= sr1) load_row(sr + u + kPF, pf[u]);
-        }
-      }
-    }
+    if (wave_sse) run(std::true_type{});
+    else run(std::false_type{});
   } else {
     auto consume = [&](int r, const uint32_t (&v)[NDW]) {
       int h[4];
