@@ -211,7 +211,7 @@ __device__ __forceinline__ void huber(double e, double delta, double dsqr, doubl
 // ---------------------------------------------------------------------------
 // Device-side Levenberg-Marquardt control (Optimizer::run_device): the accept / reject
 // decision, the lambda schedule, Raul's nBad stop and the terminate action of g2o run in
-// k_lm_end after every trial, so the host enqueues trial after trial without reading anything
+// k_edges_end after every trial, so the host enqueues trial after trial without reading anything
 // back.  Kernels of a step that is no longer needed (done) return at once; the linearisation
 // of a step runs only when the previous trial ended an iteration (lin).
 constexpr int kLmTraceCap = 64;
@@ -220,10 +220,11 @@ struct LmCtl {
   double chi0, lambda_final;
   int ni, qmax, nBad, it, iter;
   int done, lin, restore, stop_out, ext_stop;
-  int max_iterations, max_trials, terminate_max_iter, pad_;
+  int max_iterations, max_trials, terminate_max_iter;
+  unsigned arrive;   // k_edges_end's arrival counter (0 between launches)
   double trace[kLmTraceCap];
 };
-// host-coherent progress word of run_device (written by k_lm_end after every step)
+// host-coherent progress word of run_device (written by k_edges_end after every step)
 struct LmSig { uint64_t seq; int32_t done, iter; int32_t ext_stop, pad_; };
 
 struct Dev {
@@ -424,48 +425,88 @@ __host__ __device__ inline double cube_rn(double x) {
   return h + (he + pe * x);
 }
 
-// The end of a device-driven step in one launch (one workgroup): the trial's three sums
-// (robust chi2, points' and poses' model decrease; summed exactly as k_reduce3's three
-// workgroups do, or taken from sc when reduce_dev already formed them), the LM control
-// (lm_control) and the pop of a rejected trial by every thread.
+// The end of a device-driven step, run by the last-arriving workgroup of k_edges_end: the
+// trial's three sums from the workgroup partials (each summed exactly as k_reduce3's 1024-thread
+// workgroups do: 1024 strided slots, then the LDS tree -- emulated here by kRedNT threads, so
+// the bits are the same), the LM control (lm_control) and the pop of a rejected trial.
 __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig);
-__global__ __launch_bounds__(1024) void k_lm_end(Dev d, Sum3 q, int have_sums, double* sc,
-                                                 const int* flag, LmSig* sig, uint64_t seq) {
+struct LmEnd { double* sc; const int* flag; LmSig* sig; uint64_t seq; };
+__device__ __forceinline__ void lm_publish(const LmCtl* c, const LmEnd& le) {
+  // relaxed: a stale `done` only costs the host one more (no-op) step
+  __hip_atomic_store(&le.sig->done, c->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&le.sig->iter, c->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&le.sig->seq, le.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
   __shared__ double s[1024];
   __shared__ int rej;
   LmCtl* c = d.ctl;
   const int t = threadIdx.x;
-  if (!c->done) {
-    if (have_sums != 1) {   // 0: the per-element arrays; 2: workgroup partials (q says which)
-      for (int b = 0; b < 3; b++) {
-        const double* v = q.v[b];
-        double acc = 0.0;
-        for (int i = t; i < q.n[b]; i += 1024) acc = acc + v[i];
-        s[t] = acc;
-        __syncthreads();
-        for (int o = 512; o > 0; o >>= 1) {
-          if (t < o) s[t] = s[t] + s[t + o];
-          __syncthreads();
-        }
-        if (t == 0) sc[b] = s[0];
-        __syncthreads();
-      }
-    }
-    if (t == 0) {
-      lm_control(c, sc, *flag, sig);
-      rej = c->restore;
+  for (int b = 0; b < 3; b++) {
+    const double* v = q.v[b];
+#pragma unroll
+    for (int u = 0; u < 1024 / kRedNT; u++) {
+      const int ts = t + u * kRedNT;
+      double acc = 0.0;
+      for (int i = ts; i < q.n[b]; i += 1024) acc = acc + v[i];
+      s[ts] = acc;
     }
     __syncthreads();
-    if (rej) {   // pop: every pose and point back to the backups of the trial's push
-      for (int i = t; i < d.n_pose_dbl; i += 1024) d.poses[i] = d.push_poses[i];
-      for (int i = t; i < d.n_point_dbl; i += 1024) d.points[i] = d.push_points[i];
+    for (int o = 512; o > 0; o >>= 1) {
+      for (int ts = t; ts < o; ts += kRedNT) s[ts] = s[ts] + s[ts + o];
+      __syncthreads();
     }
+    if (t == 0) le.sc[b] = s[0];
+    __syncthreads();
   }
-  if (t == 0) {   // relaxed: a stale `done` only costs the host one more (no-op) step
-    __hip_atomic_store(&sig->done, c->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&sig->iter, c->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&sig->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) {
+    lm_control(c, le.sc, *le.flag, le.sig);
+    rej = c->restore;
   }
+  __syncthreads();
+  if (rej) {   // pop: every pose and point back to the backups of the trial's push
+    for (int i = t; i < d.n_pose_dbl; i += kRedNT) d.poses[i] = d.push_poses[i];
+    for (int i = t; i < d.n_point_dbl; i += kRedNT) d.points[i] = d.push_points[i];
+  }
+  if (t == 0) lm_publish(c, le);
+}
+
+// The trial's evaluation (k_edges without linearisation: error, robust chi2, workgroup partial)
+// and the end of the step in one launch: each workgroup releases its partial and counts itself
+// in; the last one (device-scope counter, agent-scope acquire) closes the step.  A step past
+// the end still publishes its sequence number (workgroup 0), as the host waits for each.
+__global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d, Sum3 q, LmEnd le) {
+  __shared__ int last;
+  LmCtl* c = d.ctl;
+  if (c->done) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) lm_publish(c, le);
+    return;
+  }
+  const int k = blockIdx.x * kRedNT + threadIdx.x;
+  double r0 = 0.0;
+  if (k < d.nae) {
+    const int e = d.aedge ? d.aedge[k] : k;
+    const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
+    double er[2];
+    edge_error(d.poses + 6 * pi, d.points + 3 * li, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
+    const double c2 = d.e_info[e] * (er[0] * er[0] + er[1] * er[1]);
+    double r1;
+    huber(c2, d.delta, d.dsqr, &r0, &r1);
+    d.err[2 * e] = er[0]; d.err[2 * e + 1] = er[1];
+    d.chi[e] = c2;
+    d.rchi[k] = r0;
+  }
+  const double sum = block_sum256(r0);
+  if (threadIdx.x == 0) {
+    d.part_chi[blockIdx.x] = sum;
+    __threadfence();   // release the partial before counting in
+    last = atomicAdd(&c->arrive, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();     // acquire: every workgroup's partial
+  if (threadIdx.x == 0) __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
+  lm_end_body(d, q, le);
 }
 
 // chi2 of the starting point -> currentChi (the optimize() call's activeRobustChi2)
@@ -483,7 +524,7 @@ __global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
   c->ni = 2;
   c->nBad = 0;
 }
-// after a trial (k_lm_end, one thread): OptimizationAlgorithmLevenberg::solve's accept / reject
+// after a trial (k_edges_end's last workgroup, one thread): OptimizationAlgorithmLevenberg::solve's accept / reject
 // (optimization_algorithm_levenberg.cpp:99-163) and, when the iteration ends, the terminate
 // action (sparse_optimizer_terminate_action.cpp:43-72) -- the arithmetic of the host driver
 // statement for statement.  sc = {robust chi2, points' model decrease, poses' model
@@ -508,7 +549,7 @@ __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig) {
     } else {
       c->lambda *= c->ni;
       c->ni *= 2;
-      c->restore = 1;   // k_lm_end pops the state right after this decision
+      c->restore = 1;   // k_edges_end pops the state right after this decision
     }
     c->qmax++;
     if (rho < 0 && c->qmax < c->max_trials && !stop) {
@@ -572,31 +613,78 @@ __device__ __forceinline__ double quad_sum(double v) {
   v += __shfl_xor(v, 2);
   return v;
 }
-__device__ __forceinline__ void points_build_body(const Dev& d, int block) {
+// D = Hll + lambda I -> D^-1 by cofactors (k_point_trial and k_build_trial: identical bits)
+__device__ __forceinline__ void dinv_of(const double* H, double lam, double (&Di)[9]) {
+  double D[9];
+  for (int k = 0; k < 9; k++) D[k] = H[k];
+  D[0] += lam; D[4] += lam; D[8] += lam;
+  const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
+  const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
+  const double id = 1.0 / det;
+  Di[0] = c00 * id; Di[3] = c01 * id; Di[6] = c02 * id;
+  Di[1] = (D[2] * D[7] - D[1] * D[8]) * id;
+  Di[4] = (D[0] * D[8] - D[2] * D[6]) * id;
+  Di[7] = (D[1] * D[6] - D[0] * D[7]) * id;
+  Di[2] = (D[1] * D[5] - D[2] * D[4]) * id;
+  Di[5] = (D[2] * D[3] - D[0] * D[5]) * id;
+  Di[8] = (D[0] * D[4] - D[1] * D[3]) * id;
+}
+// Y_e = Hpl_e Dinv of one (point, edge) entry whose pose is active
+__device__ __forceinline__ void y_of(const Dev& d, int e, const double (&Di)[9]) {
+  const double* B = d.hpl + 18 * e;
+  double bb[18];
+  for (int k = 0; k < 18; k++) bb[k] = B[k];
+  for (int a = 0; a < 6; a++)
+    for (int c = 0; c < 3; c++)
+      d.y[18 * e + 3 * a + c] = bb[3 * a] * Di[c] + bb[3 * a + 1] * Di[3 + c] + bb[3 * a + 2] * Di[6 + c];
+}
+
+// TRIAL (k_build_trial): the same quad then carries k_point_trial's point part -- Dinv, db and
+// the Y of the point's edges -- from the H and b it holds (LIN: just built; otherwise the
+// iteration's stored Hll / b_l: a rejected trial re-solves the same linearisation)
+template <bool TRIAL>
+__device__ __forceinline__ void points_build_body(const Dev& d, int block, bool lin) {
   const int gt = block * kRedNT + threadIdx.x;
   const int l = gt >> 2, sub = gt & 3;
   const bool act = l < d.nl;
   double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-  if (act) {
-    for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
-      const int e = d.pt_edges[q];
-      const double* jl = d.jl + 6 * e;
-      const double w = d.w[e];
-      const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
-      for (int a = 0; a < 3; a++) {
-        for (int bb = 0; bb < 3; bb++) H[3 * a + bb] += w * (jl[a] * jl[bb] + jl[3 + a] * jl[3 + bb]);
-        b[a] += jl[a] * we0 + jl[3 + a] * we1;
+  if (lin) {
+    if (act) {
+      for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
+        const int e = d.pt_edges[q];
+        const double* jl = d.jl + 6 * e;
+        const double w = d.w[e];
+        const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
+        for (int a = 0; a < 3; a++) {
+          for (int bb = 0; bb < 3; bb++) H[3 * a + bb] += w * (jl[a] * jl[bb] + jl[3 + a] * jl[3 + bb]);
+          b[a] += jl[a] * we0 + jl[3 + a] * we1;
+        }
       }
     }
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = quad_sum(H[i]);
+#pragma unroll
+    for (int i = 0; i < 3; i++) b[i] = quad_sum(b[i]);
+    if (act && sub == 0) {
+      for (int i = 0; i < 9; i++) d.Hll[9 * l + i] = H[i];
+      for (int i = 0; i < 3; i++) d.bl[3 * l + i] = b[i];
+      d.red[l] = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+    }
+  } else if (TRIAL && act) {
+    for (int i = 0; i < 9; i++) H[i] = d.Hll[9 * l + i];
+    for (int i = 0; i < 3; i++) b[i] = d.bl[3 * l + i];
   }
-#pragma unroll
-  for (int i = 0; i < 9; i++) H[i] = quad_sum(H[i]);
-#pragma unroll
-  for (int i = 0; i < 3; i++) b[i] = quad_sum(b[i]);
-  if (!act || sub != 0) return;
-  for (int i = 0; i < 9; i++) d.Hll[9 * l + i] = H[i];
-  for (int i = 0; i < 3; i++) d.bl[3 * l + i] = b[i];
-  d.red[l] = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+  if (!TRIAL || !act) return;
+  double Di[9];
+  dinv_of(H, lam_of(d), Di);
+  if (sub == 0) {
+    for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
+    for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
+  }
+  for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
+    const int e = d.pt_edges[q];
+    if (d.pose_h[d.e_pose[e]] >= 0) y_of(d, e, Di);
+  }
 }
 
 // Deterministic block sum of NV per-thread partials over a workgroup of NW waves: fixed
@@ -638,21 +726,38 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
   double acc[27];
 #pragma unroll
   for (int v = 0; v < 27; v++) acc[v] = 0.0;
-  for (int q = d.ps_ptr[i] + t; q < d.ps_ptr[i + 1]; q += kRedNT) {
-    const int e = d.ps_edges[q];
-    const double* jp = d.jp + 12 * e;
-    double j0[6], j1[6];
+  // a thread's edges t, t + 256, ... in that order; kU of them per pass with every load issued
+  // before the first sum (the edge -> Jacobian gather is two dependent round trips, and a
+  // pose has ~1500 edges at config C: one at a time the chain was the whole kernel).  Loads
+  // past the list read the last edge (unconditional: no merge waits) and are not summed.
+  constexpr int kU = 4;
+  const int q0 = d.ps_ptr[i], q1 = d.ps_ptr[i + 1];
+  for (int qb = q0 + t; qb < q1; qb += kU * kRedNT) {
+    int e[kU];
 #pragma unroll
-    for (int a = 0; a < 6; a++) { j0[a] = jp[a]; j1[a] = jp[6 + a]; }
-    const double w = d.w[e];
-    const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
+    for (int u = 0; u < kU; u++) e[u] = d.ps_edges[min(qb + u * kRedNT, q1 - 1)];
+    double j0[kU][6], j1[kU][6], w[kU], er0[kU], er1[kU];
 #pragma unroll
-    for (int v = 0; v < 21; v++) {
-      const int a = kUpper6[v][0], bb = kUpper6[v][1];
-      acc[v] += w * (j0[a] * j0[bb] + j1[a] * j1[bb]);
+    for (int u = 0; u < kU; u++) {
+      const double* jp = d.jp + 12 * e[u];
+#pragma unroll
+      for (int a = 0; a < 6; a++) { j0[u][a] = jp[a]; j1[u][a] = jp[6 + a]; }
+      w[u] = d.w[e[u]];
+      er0[u] = d.err[2 * e[u]];
+      er1[u] = d.err[2 * e[u] + 1];
     }
 #pragma unroll
-    for (int a = 0; a < 6; a++) acc[21 + a] += j0[a] * we0 + j1[a] * we1;
+    for (int u = 0; u < kU; u++) {
+      if (qb + u * kRedNT >= q1) break;
+      const double we0 = -w[u] * er0[u], we1 = -w[u] * er1[u];
+#pragma unroll
+      for (int v = 0; v < 21; v++) {
+        const int a = kUpper6[v][0], bb = kUpper6[v][1];
+        acc[v] += w[u] * (j0[u][a] * j0[u][bb] + j1[u][a] * j1[u][bb]);
+      }
+#pragma unroll
+      for (int a = 0; a < 6; a++) acc[21 + a] += j0[u][a] * we0 + j1[u][a] * we1;
+    }
   }
   constexpr int NW = kRedNT / 64;
   block_sum_vec<27, NW>(acc, sm);
@@ -671,7 +776,14 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
 __global__ __launch_bounds__(kRedNT) void k_build(Dev d) {
   if (lm_done(d) || (d.ctl && !d.ctl->lin)) return;
   if ((int)blockIdx.x < d.np) poses_build_body(d, blockIdx.x);
-  else points_build_body(d, blockIdx.x - d.np);
+  else points_build_body<false>(d, blockIdx.x - d.np, true);
+}
+
+// the trial's push (backup of every pose and point) and the solve-flag reset, grid-strided
+__device__ __forceinline__ void trial_push(const Dev& d, int q, int stride) {
+  for (int i = q; i < d.n_pose_dbl; i += stride) d.push_poses[i] = d.poses[i];
+  for (int i = q; i < d.n_point_dbl; i += stride) d.push_points[i] = d.points[i];
+  if (q == 0) *d.flag = 0;
 }
 
 // One thread per (point, edge) entry of the point CSR: D = Hll + lambda I -> Dinv (cofactors,
@@ -680,63 +792,43 @@ __global__ __launch_bounds__(kRedNT) void k_build(Dev d) {
 __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
   if (lm_done(d)) return;
   const int q = blockIdx.x * 256 + threadIdx.x;
-  const double lam = lam_of(d);
-  // the trial's push (backup of every pose and point) and the solve-flag reset ride along
-  {
-    const int stride = gridDim.x * 256;
-    for (int i = q; i < d.n_pose_dbl; i += stride) d.push_poses[i] = d.poses[i];
-    for (int i = q; i < d.n_point_dbl; i += stride) d.push_points[i] = d.points[i];
-    if (q == 0) *d.flag = 0;
-  }
+  trial_push(d, q, gridDim.x * 256);
   if (q >= d.npe) return;
   const int e = d.pt_edges[q];
   const int l = d.point_h[d.e_point[e]];
   const bool first = (q == d.pt_ptr[l]);
   const bool pose_act = d.pose_h[d.e_pose[e]] >= 0;
   if (!first && !pose_act) return;
-  double D[9];
-  for (int k = 0; k < 9; k++) D[k] = d.Hll[9 * l + k];
-  D[0] += lam; D[4] += lam; D[8] += lam;
-  const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
-  const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
-  const double id = 1.0 / det;
   double Di[9];
-  Di[0] = c00 * id; Di[3] = c01 * id; Di[6] = c02 * id;
-  Di[1] = (D[2] * D[7] - D[1] * D[8]) * id;
-  Di[4] = (D[0] * D[8] - D[2] * D[6]) * id;
-  Di[7] = (D[1] * D[6] - D[0] * D[7]) * id;
-  Di[2] = (D[1] * D[5] - D[2] * D[4]) * id;
-  Di[5] = (D[2] * D[3] - D[0] * D[5]) * id;
-  Di[8] = (D[0] * D[4] - D[1] * D[3]) * id;
+  dinv_of(d.Hll + 9 * l, lam_of(d), Di);
   if (first) {
     for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
     const double* b = d.bl + 3 * l;
     for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
   }
-  if (pose_act) {
-    const double* B = d.hpl + 18 * e;
-    double bb[18];
-    for (int k = 0; k < 18; k++) bb[k] = B[k];
-    for (int a = 0; a < 6; a++)
-      for (int c = 0; c < 3; c++)
-        d.y[18 * e + 3 * a + c] = bb[3 * a] * Di[c] + bb[3 * a + 1] * Di[3 + c] + bb[3 * a + 2] * Di[6 + c];
-  }
+  if (pose_act) y_of(d, e, Di);
 }
 
-__device__ __forceinline__ double readlane0_d(double v) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 0);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 0);
-  return __hiloint2double(hi, lo);
+// Device-driven steps after the first: k_build (when the step linearises) and k_point_trial in
+// one launch -- the point quads go on from their H / b to Dinv, db and Y (same arithmetic,
+// same bits), every thread takes part in the push.  Step 0 keeps the two launches: lambda's
+// initial value needs the built diagonal first.
+__global__ __launch_bounds__(kRedNT) void k_build_trial(Dev d) {
+  if (lm_done(d)) return;
+  const bool lin = d.ctl->lin != 0;
+  trial_push(d, blockIdx.x * kRedNT + threadIdx.x, gridDim.x * kRedNT);
+  if ((int)blockIdx.x < d.np) { if (lin) poses_build_body(d, blockIdx.x); }
+  else points_build_body<true>(d, blockIdx.x - d.np, lin);
 }
+
 
 // reduced camera system, lower blocks (i >= j): S_ij = [i==j](Hpp_i + lam0 I)
 //   - sum over (e1 in pose i, e2 in pose j, same point) Y_e1 Hpl_e2^T;
 // diagonal blocks also form bschur_i = b_i - sum_e Hpl_e db(point(e)).
 // Work items (host-built, `build_schur_items`): item = (block, chunk c of nch); chunk c covers
 // pairs [q0 + c*CH, ...) and, on a diagonal block, pose edges [e0 + c*CH, ...).  One wave per
-// item: lane L accumulates entries L, L+64, ... in registers, a fixed xor butterfly over the
-// lanes that can hold data (levels whose partners are all past the chunk add zeros and are
-// skipped) leaves the 42 sums in lane 0.  A block with one chunk (config E: ~90 pairs per
+// item: lane L accumulates entries L, L+64, ... in registers, a fixed recursive halving over
+// the wave (schur_halve) leaves each of the 42 sums in one lane.  A block with one chunk (config E: ~90 pairs per
 // block) writes S / bschur directly; otherwise the chunk's sums go to a partial slot and
 // the wave that completes the block's last chunk adds the slots in chunk order (config C: 55
 // blocks of thousands of pairs, so a
@@ -755,6 +847,32 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
     const int a = lane - 36;
     d.bs[6 * bi + a] = d.bp[6 * bi + a] - v;
   }
+}
+
+// one level of k_schur's recursive halving over N values: values [0, H) and [H, N) (zero-padded
+// to H) split by lane bit O; the lane keeps one half in acc[0, H)
+template <int N, int O>
+__device__ __forceinline__ void schur_halve(double (&acc)[42], int lane) {
+  constexpr int H = (N + 1) / 2;
+  const bool hi = (lane & O) != 0;
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    const double a = acc[i], b = (H + i < N) ? acc[H + i] : 0.0;
+    const double keep = hi ? b : a, give = hi ? a : b;
+    acc[i] = keep + __shfl_xor(give, O);
+  }
+}
+// the sum a lane holds after the six levels (-1: a padding slot).  The split points are the
+// static H of each level (21, 11, 6, 3, 2, 1); a lane's real count shrinks to n - H on the
+// high side, so some slots of the last levels are zero padding.
+__device__ __forceinline__ int schur_idx(int lane) {
+  constexpr int kH[6] = {21, 11, 6, 3, 2, 1};
+  int idx = 0, n = 42;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    if (lane & (32 >> k)) { idx += kH[k]; n -= kH[k]; } else n = n < kH[k] ? n : kH[k];
+  }
+  return n > 0 ? idx : -1;
 }
 
 __global__ __launch_bounds__(256) void k_schur(Dev d) {
@@ -799,20 +917,21 @@ __global__ __launch_bounds__(256) void k_schur(Dev d) {
       for (int a = 0; a < 6; a++) acc[36 + a] += B[3 * a] * g0 + B[3 * a + 1] * g1 + B[3 * a + 2] * g2;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    if (nact <= o) continue;    // wave-uniform
-#pragma unroll
-    for (int v = 0; v < 42; v++) acc[v] += __shfl_xor(acc[v], o);
-  }
-  double mine = 0.0;
-#pragma unroll
-  for (int v = 0; v < 42; v++) {
-    const double sv = readlane0_d(acc[v]);
-    if (lane == v) mine = sv;
-  }
-  if (slot < 0) schur_write(d, bi, bj, lam0, lane, mine);
-  else if (lane < 42) d.schur_part[(size_t)slot * 42 + lane] = mine;
+  (void)nact;
+  // the 42 wave sums by recursive halving: at level o a lane keeps the half of its values
+  // selected by lane bit o and adds its partner's copy of that half (own + partner: the same
+  // sum, bit for bit, as a full xor butterfly forms for every value), so 44 exchanges instead
+  // of 6 x 42, and sum v ends in one lane (schur_idx), which writes it
+  schur_halve<42, 32>(acc, lane);
+  schur_halve<21, 16>(acc, lane);
+  schur_halve<11, 8>(acc, lane);
+  schur_halve<6, 4>(acc, lane);
+  schur_halve<3, 2>(acc, lane);
+  schur_halve<2, 1>(acc, lane);
+  const int v = schur_idx(lane);
+  if (v < 0) return;
+  if (slot < 0) schur_write(d, bi, bj, lam0, v, acc[0]);
+  else d.schur_part[(size_t)slot * 42 + v] = acc[0];
 }
 
 // blocks split into several chunks: sum the chunk slots in chunk order, then write (one wave
@@ -1077,7 +1196,7 @@ struct mcs_ba_ctx {
   int32_t* pinned_i = nullptr;
   TrialSig* sig = nullptr;    // host-coherent trial outcome (k_reduce3)
   uint64_t sig_seq = 0;
-  LmSig* lsig = nullptr;      // host-coherent progress of the device-driven LM (k_lm_end)
+  LmSig* lsig = nullptr;      // host-coherent progress of the device-driven LM (k_edges_end)
   uint64_t lsig_seq = 0;
   void* pinned_ctl = nullptr; // host-pinned readback of the final LmCtl
   // host-pinned staging of a call's packed problem upload (grow-only)
@@ -1796,9 +1915,9 @@ struct Optimizer {
   }
 
   // Device-driven SparseOptimizer::optimize: the host enqueues LM steps (restore if the last
-  // trial was rejected, linearisation if it ended an iteration, one trial, k_lm_end) up to two
+  // trial was rejected, linearisation if it ended an iteration, one trial, k_edges_end) up to two
   // ahead of the device and watches the progress word only to stop enqueuing; the decisions
-  // are k_lm_end's.  Kernels of steps past the end return at once.
+  // are k_edges_end's.  Kernels of steps past the end return at once.
   int run_device(const mcs_ba_options* o, double* poses, double* points, double* edge_chi2,
                  volatile int32_t* stop_flag, mcs_ba_report* rep) {
     if (rep) {
@@ -1837,13 +1956,16 @@ struct Optimizer {
     }
     auto enqueue_step = [&](int step) -> int {
       hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
-      hipLaunchKernelGGL(k_build, dim3((unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT)), dim3(kRedNT), 0, st, dd);
+      const unsigned g_build = (unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT);
       if (step == 0) {   // iteration 0 is always step 0: lambda from the max diagonal
+        hipLaunchKernelGGL(k_build, dim3(g_build), dim3(kRedNT), 0, st, dd);
         reduce_dev<true>(d.red, s.nl, d_scalar + 1, d_part, st);
         reduce_dev<true>(d.hdiag, 6 * s.np, d_scalar + 2, d_part, st);
         hipLaunchKernelGGL(k_lm_lambda0, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
+        hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, dd);
+      } else {
+        hipLaunchKernelGGL(k_build_trial, dim3(g_build), dim3(kRedNT), 0, st, dd);
       }
-      hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, dd);
       if (s.np) {
         hipLaunchKernelGGL(k_schur, dim3((unsigned)((items_max + 3) / 4)), dim3(256), 0, st, dd);
         hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, dd, nblk);
@@ -1854,21 +1976,21 @@ struct Optimizer {
         }
       }
       hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, dd);
-      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 0);
-      // the trial's three sums from the workgroup partials of k_edges / k_update (a fixed
-      // order: partials in workgroup order, each a fixed in-workgroup tree)
+      // the trial's evaluation, then (last workgroup) its three sums from the workgroup
+      // partials of k_edges_end / k_update (a fixed order: partials in workgroup order, each a
+      // fixed in-workgroup tree), the LM decision and the pop of a rejected trial
       Sum3 q{{dd.part_chi, dd.part_pt, dd.part_ps}, {(int)g_edg, (int)g_upd, (int)g_upd}};
-      hipLaunchKernelGGL(k_lm_end, dim3(1), dim3(1024), 0, st, dd, q, 2, d_scalar,
-                         (const int*)d_flag, c->lsig, ++c->lsig_seq);
+      LmEnd le{d_scalar, (const int*)d_flag, c->lsig, ++c->lsig_seq};
+      hipLaunchKernelGGL(k_edges_end, dim3(g_edg), dim3(kRedNT), 0, st, dd, q, le);
       return hipGetLastError() == hipSuccess ? MCS_OK : MCS_ERR_HIP;
     };
-    // progress word of the step whose k_lm_end published sequence `want`
+    // progress word of the step whose k_edges_end published sequence `want`
     auto wait_seq = [&](uint64_t want) -> int {
       for (uint32_t k = 1;; k++) {
         if (__atomic_load_n(&c->lsig->seq, __ATOMIC_ACQUIRE) >= want) return MCS_OK;
         __builtin_ia32_pause();
         if ((k & 1023) == 0) {
-          c->lsig->ext_stop = *stop != 0;   // the caller's abort flag reaches k_lm_end
+          c->lsig->ext_stop = *stop != 0;   // the caller's abort flag reaches k_edges_end
           const hipError_t q = hipStreamQuery(st);
           if (q == hipSuccess) {
             if (__atomic_load_n(&c->lsig->seq, __ATOMIC_ACQUIRE) >= want) return MCS_OK;
