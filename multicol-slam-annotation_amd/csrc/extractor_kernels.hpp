@@ -53,7 +53,10 @@ inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
 #ifndef MCS_PYR_MAXROWS
 #define MCS_PYR_MAXROWS 64
 #endif
-  rows = std::min(MCS_PYR_MAXROWS, std::max(8, rows));
+#ifndef MCS_PYR_MINROWS
+#define MCS_PYR_MINROWS 8
+#endif
+  rows = std::min(MCS_PYR_MAXROWS, std::max(MCS_PYR_MINROWS, rows));
   a.seg_rows = rows;
   a.tiles_y = (dh + rows - 1) / rows;
 }
