@@ -103,8 +103,8 @@ __device__ __forceinline__ int fast_small(const uint8_t* lds, uint32_t ring_base
 
 // Tuning probe (tools/gpu/fast_probe.py, variant builds with -DMCS_FAST_PROBE only): shader
 // cycles per phase summed over all waves: [0] band loads + ring writes, [1] compass + list,
-// [2] exact test + score, [3] NMS + mask + append, [4] whole wave, [5] bands, [6] survivors,
-// [7] corners.
+// [2] exact test + score, [3] NMS + mask + append, [4] whole wave, [5] bands, [6] skipped
+// (fully masked) bands, [7] setup before the first band.
 #ifdef MCS_FAST_PROBE
 __device__ unsigned long long g_fast_probe[8];
 #define FP_T(v) const long long v = __builtin_amdgcn_s_memtime()
@@ -210,6 +210,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
 
   const int nbands = (wh + kBand - 1) / kBand;
   int ncarry = 0;   // corners of the previous band's last row, at the front of the list
+#ifdef MCS_FAST_PROBE
+  FP_ADD(7, __builtin_amdgcn_s_memtime() - t_begin_);
+#endif
   for (int b = 0; b < nbands; b++) {
     FP_T(t0_);
     const int y0 = 3 + b * kBand, y1 = min(y0 + kBand, 3 + wh);
@@ -261,6 +264,9 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       for (int i = 0; i < kBand + 2; i++) any |= m[i];
       if (__ballot(any != 0) == 0) {
         ncarry = 0;
+#ifdef MCS_FAST_PROBE
+        FP_ADD(6, __builtin_amdgcn_s_memtime() - t0_);
+#endif
         continue;
       }
     }
@@ -312,7 +318,6 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     dev::wave_sync();
     FP_T(t2_);
     FP_ADD(1, t2_ - t1_);
-    FP_ADD(6, ns);
 
     // ---- B: exact FAST test + score of the survivors, two per lane (batch j0: survivors
     // j0 + lane and j0 + 64 + lane in the low / high halves).  With d_k = v - p_k, cornerScore's
@@ -397,7 +402,6 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     dev::wave_sync();
     FP_T(t3_);
     FP_ADD(2, t3_ - t2_);
-    FP_ADD(7, ncorn - ncarry);
 
     // ---- C: NMS (3x3 within the cell) + runByPixelsMask + append to the cell's slots
     const bool last_band = b + 1 == nbands;

@@ -40,6 +40,7 @@ names = ["load+ring", "compass+list", "exact+score", "nms+mask+append"]
 print("k_fast_rows phase split (cycles summed over waves, one batch of %d frames):" % F)
 for k in range(4):
     print("  %-16s %6.1f %%" % (names[k], 100.0 * float(out[k]) / tot))
-print("  other (setup, skipped bands) %5.1f %%" % (100.0 * (tot - sum(float(out[k]) for k in range(4))) / tot))
-print("  bands %d  survivors/band %.1f  corners/band %.1f  cycles/band %.0f" % (
-    out[5], out[6] / max(1, out[5]), out[7] / max(1, out[5]), tot / max(1, out[5])))
+print("  skipped bands    %6.1f %%" % (100.0 * float(out[6]) / tot))
+print("  setup            %6.1f %%" % (100.0 * float(out[7]) / tot))
+print("  other            %6.1f %%" % (100.0 * (tot - sum(float(out[k]) for k in (0, 1, 2, 3, 6, 7))) / tot))
+print("  bands %d  cycles/band %.0f" % (out[5], tot / max(1, out[5])))
