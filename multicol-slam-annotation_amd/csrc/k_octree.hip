@@ -392,13 +392,21 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
 }
 
 
+// candidates kept in LDS per (frame, level): LDS per workgroup sets how many workgroups share
+// a CU (160 KB), and this latency-bound kernel lives on residency.  768 (39.5 KB) fits four
+// workgroups per CU, where 2048 (49.7 KB) fitted three: octree 0.374 -> 0.348 ms per config-B
+// step, although more (frame, level) lists then stay in global memory (1024: 41.5 KB, three
+// per CU, 0.394 ms)
+#ifndef MCS_OCT_CAP
+#define MCS_OCT_CAP 768
+#endif
 void launch_octree(const OctArgs& a, int max_list, hipStream_t st) {
   const unsigned g = xcd_grid(a.nframes, a.nlevels);
   int max_cells = 0;
   for (int l = 0; l < a.nlevels; l++) max_cells = std::max(max_cells, a.lv[l].cell_end - a.lv[l].cell_begin);
   // s_pref holds 2*MAXL cell prefixes (the plan rejects > kMaxCellsPerLevel = 2048)
   if (max_list <= 512 && max_cells <= 1024)
-    hipLaunchKernelGGL((k_octree<512, 2048>), dim3(g), dim3(kOctThreads), 0, st, a);
+    hipLaunchKernelGGL((k_octree<512, MCS_OCT_CAP>), dim3(g), dim3(kOctThreads), 0, st, a);
   else
     hipLaunchKernelGGL((k_octree<1024, 0>), dim3(g), dim3(kOctThreads), 0, st, a);
 }
