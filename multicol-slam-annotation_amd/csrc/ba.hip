@@ -1663,7 +1663,13 @@ struct Optimizer {
           volatile int32_t* stop_flag, mcs_ba_report* rep) {
     // one GPU and no per-stage timing: the LM control runs on the device (no per-trial
     // host round trip); sharded runs agree on every decision through the host exchange
-    if (!sharded && !c->timing) return run_device(o, poses, points, edge_chi2, stop_flag, rep);
+    // (the device loop records the chi2 trace of its first kLmTraceCap iterations only: a
+    // caller asking for a longer trace of a longer run gets the host-driven loop, which fills
+    // up to trace_cap like every other path)
+    const bool long_trace = rep && rep->trace_chi2 && rep->trace_cap > kLmTraceCap &&
+                            o->max_iterations > kLmTraceCap;
+    if (!sharded && !c->timing && !long_trace)
+      return run_device(o, poses, points, edge_chi2, stop_flag, rep);
     auto rec = [&](int k) { if (c->timing) (void)hipEventRecord(c->ev[k], st); };
     auto ms = [&](int a, int b) { float f = 0.f; (void)hipEventElapsedTime(&f, c->ev[a], c->ev[b]); return (double)f; };
     int rc;

@@ -173,12 +173,19 @@ int mcs_distinctive_descriptors_device(const uint8_t* d_desc, const uint8_t* d_m
                                        const int32_t* d_obs_ptr, const int32_t* d_obs_row,
                                        int32_t n_points, int32_t* d_best, uint8_t* d_out_desc,
                                        uint8_t* d_out_mask, void* stream) {
-  if (n_points < 0 || (bytes != 16 && bytes != 32 && bytes != 64)) {
+  if (n_points < 0) {
+    mcs::set_error("distinctive descriptors: n_points must be >= 0");
+    return MCS_ERR_ARG;
+  }
+  if (bytes != 16 && bytes != 32 && bytes != 64) {
     mcs::set_error("distinctive descriptors: bytes must be 16, 32 or 64");
     return MCS_ERR_ARG;
   }
   if (n_points == 0) return MCS_OK;
-  if (!d_desc || !d_obs_ptr || !d_obs_row || !d_best) return MCS_ERR_ARG;
+  if (!d_desc || !d_obs_ptr || !d_obs_row || !d_best) {
+    mcs::set_error("distinctive descriptors: null device pointer");
+    return MCS_ERR_ARG;
+  }
   const dim3 g((unsigned)((n_points + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
   const bool m = d_masks != nullptr;
@@ -195,11 +202,20 @@ int mcs_update_normal_depth_device(const double* d_points, int32_t n_points,
                                    const int32_t* d_ref_level, const double* d_scale,
                                    int32_t n_levels, double* d_normal, double* d_min_dist,
                                    double* d_max_dist, void* stream) {
-  if (n_points < 0 || n_levels < 2) return MCS_ERR_ARG;
+  if (n_points < 0) {
+    mcs::set_error("update normal/depth: n_points must be >= 0");
+    return MCS_ERR_ARG;
+  }
+  if (n_levels < 2) {
+    mcs::set_error("update normal/depth: n_levels must be >= 2");
+    return MCS_ERR_ARG;
+  }
   if (n_points == 0) return MCS_OK;
   if (!d_points || !d_obs_ptr || !d_obs_kf || !d_kf_center || !d_ref_kf || !d_ref_level ||
-      !d_scale || !d_normal || !d_min_dist || !d_max_dist)
+      !d_scale || !d_normal || !d_min_dist || !d_max_dist) {
+    mcs::set_error("update normal/depth: null device pointer");
     return MCS_ERR_ARG;
+  }
   hipLaunchKernelGGL(mcs::k_normal_depth, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, d_points, n_points, d_obs_ptr, d_obs_kf, d_kf_center,
                      d_ref_kf, d_ref_level, d_scale, n_levels, d_normal, d_min_dist, d_max_dist);

@@ -10,6 +10,7 @@ camera rays, observations = WorldToImg of visible points, octave ~ per-level bud
 pixel noise sigma = 0.5*1.2^octave, a few outliers, perturbed initial poses / points.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -645,12 +646,20 @@ class TorchExchange:
     """mcs_ba_shard backed by torch.distributed: the exchange buffer is a torch tensor on the
     rank's GPU and the callback all-reduces a slice of it (backend "nccl" = RCCL over xGMI).
 
-    On a GPU the shard is stream_ordered: the callback issues the all-reduce with the library's
-    stream as torch's current stream, so RCCL starts after the kernels that produced the slice
-    and the library's next kernels wait for it on the device -- no host synchronisation per
-    exchange.  A CPU buffer (gloo) is reduced synchronously (stream_ordered = 0)."""
+    Default (stream_ordered = 0): the library drains its stream before each call and the
+    callback returns only once the reduction is complete (the all-reduce is followed by a
+    device synchronisation), which is correct whatever ProcessGroupNCCL does with streams.
 
-    def __init__(self, n_poses, device, group=None):
+    stream_ordered = 1 (opt-in: argument, or MCS_BA_STREAM_ORDERED=1): the callback issues the
+    all-reduce with the library's stream as torch's current stream, so RCCL starts after the
+    kernels that produced the slice and the library's next kernels wait for it on the device --
+    no host synchronisation per exchange.  This relies on ProcessGroupNCCL making the external
+    stream wait for the collective; it has run only on gloo and on the single-GPU ThreadExchange
+    mock, never on real RCCL with world > 1, so it stays off until a 2-GPU run has shown ordered
+    == unordered (identical poses and iteration counts).  A CPU buffer (gloo) is always reduced
+    synchronously."""
+
+    def __init__(self, n_poses, device, group=None, stream_ordered=None):
         import torch
         import torch.distributed as dist
         from . import lib
@@ -660,8 +669,11 @@ class TorchExchange:
         cap = int(lib().mcs_ba_xchg_doubles(int(n_poses)))
         self.buf = torch.zeros(cap, dtype=torch.float64, device=device)
         self._cb = ALLREDUCE_FN(self._allreduce)
+        if stream_ordered is None:
+            stream_ordered = os.environ.get("MCS_BA_STREAM_ORDERED", "0") == "1"
+        self.ordered = bool(stream_ordered) and self.buf.is_cuda
         self.shard = BAShard(self.rank, self.world, self.buf.data_ptr(), cap, self._cb, None,
-                             1 if self.buf.is_cuda else 0)
+                             1 if self.ordered else 0)
         self._streams = {}
         self.calls = 0
 
@@ -676,11 +688,15 @@ class TorchExchange:
         try:
             t = self.buf[off:off + cnt]
             rop = self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX
-            if self.buf.is_cuda:
+            if self.ordered:
                 # the NCCL process group orders the collective after the current stream's work
                 # and makes the current stream wait for it (no host wait)
                 with self.torch.cuda.stream(self._stream(stream)):
                     self.dist.all_reduce(t, op=rop, group=self.group)
+            elif self.buf.is_cuda:
+                # the library drained its stream; complete the reduction before returning
+                self.dist.all_reduce(t, op=rop, group=self.group)
+                self.torch.cuda.synchronize(self.buf.device)
             else:
                 self.dist.all_reduce(t, op=rop, group=self.group)
             self.calls += 1

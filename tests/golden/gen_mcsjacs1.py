@@ -25,6 +25,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "multicol-slam-annotation_amd"))
+sys.path.insert(0, HERE)
+from safe_exec import safe_compile_eval, safe_eval  # noqa: E402
 
 _INT_LIT = re.compile(r"(?<![\w.])\d+(?![\w.])")
 
@@ -68,12 +70,12 @@ def compile_mcsjacs1(ref_root):
             continue  # zeros(): the output array starts zeroed
         m = re.fullmatch(r"const double (\w+) = (.+)", st)
         if m:
-            prog.append((m.group(1), None, compile(_to_py(m.group(2)), m.group(1), "eval")))
+            prog.append((m.group(1), None, safe_compile_eval(_to_py(m.group(2)), m.group(1))))
             continue
         m = re.fullmatch(r"jacs\((\d), (\d+)\) = (.+)", st)
         if m:
             prog.append((None, (int(m.group(1)), int(m.group(2))),
-                         compile(_to_py(m.group(3)), "jacs", "eval")))
+                         safe_compile_eval(_to_py(m.group(3)), "jacs")))
             continue
         raise ValueError("unparsed statement: %s" % st[:120])
     return prog
@@ -84,7 +86,7 @@ def eval_mcsjacs1(prog, pt3, M_t, M_c, camModelData):
            "M_c": [float(v) for v in M_c], "camModelData": [float(v) for v in camModelData]}
     jacs = np.zeros((2, 32))
     for name, ij, code in prog:
-        v = eval(code, env)
+        v = safe_eval(code, env)
         if name is not None:
             env[name] = float(v)
         else:

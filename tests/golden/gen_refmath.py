@@ -37,6 +37,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "multicol-slam-annotation_amd"))
+sys.path.insert(0, HERE)
+from safe_exec import safe_exec  # noqa: E402
 
 
 # ---------------------------------------------------------------- cv::Matx restatement [ext]
@@ -219,7 +221,9 @@ def translate(path, signature, pyname, params, outs=(), env=None, trace=()):
     if outs:
         ret.append("(%s,)" % ", ".join(outs))
     if trace:
-        ret.append("{%s}" % ", ".join("%r: locals().get(%r)" % (t, t) for t in trace))
+        # traced locals start as None (a branch may never assign them)
+        lines = ["%s = None" % t for t in trace] + lines
+        ret.append("{%s}" % ", ".join("%r: %s" % (t, t) for t in trace))
     if ret:
         # trace/out values are returned instead of (or beside) the reference's return value
         lines = [re.sub(r"^(\s*)return (.+)$", r"\1return (\2, %s)" % ", ".join(ret), x)
@@ -227,9 +231,10 @@ def translate(path, signature, pyname, params, outs=(), env=None, trace=()):
         if not any(x.strip().startswith("return ") for x in lines):
             lines.append("return (None, %s)" % ", ".join(ret))
     src = "def %s(%s):\n%s\n" % (pyname, ", ".join(params), "\n".join("    " + x for x in lines))
-    g = {"math": math, "Matx": Matx, "cv_norm": cv_norm}
+    g = {"math": math, "Matx": Matx, "cv_norm": cv_norm, "range": range}
     g.update(env or {})
-    exec(compile(src, "<ref:%s %s>" % (os.path.basename(path), pyname), "exec"), g)
+    # the source came from untrusted text: AST-whitelisted, run without builtins (safe_exec.py)
+    g = safe_exec(src, g, "<ref:%s %s>" % (os.path.basename(path), pyname))
     return g[pyname], src, len(_statements(body))
 
 
