@@ -258,7 +258,9 @@ int mcs_ba_check_structure(mcs_ba_ctx* c, const mcs_ba_problem* p, const uint8_t
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
                          int32_t* zero_pivot);
 /* Same, choosing the kernels: path 0 = what the BA uses (n <= 64: the fused one-tile solve,
- * else pad + panel steps + backward), path 1 = always pad + panel steps + backward.  Both
+ * else pad + the pipelined factorisation (one launch) + backward), path 1 = always pad + one
+ * panel launch per step + backward, path 2 = always pad + pipelined factorisation + backward
+ * (bitwise equal to path 1).  All
  * give bitwise equal x (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled). */
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
                             int32_t* zero_pivot, int32_t path);

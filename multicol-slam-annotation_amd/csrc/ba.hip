@@ -1215,6 +1215,7 @@ struct mcs_ba_ctx {
   // optional stage timing (mcs_ba_enable_timing): HIP events on st around each stage,
   // accumulated after the per-trial synchronisation the LM control needs anyway
   bool timing = false;
+  bool ldlt_pipe = true;   // pipelined LDL^T for multi-tile systems (MCS_LDLT_PIPE=0: per-step launches)
   hipEvent_t ev[8] = {};
   double acc_ms[MCS_BA_NSTAGES] = {};
   double host_ms[MCS_BA_NHOST] = {};   // host phases (mcs_ba_read_host_timing)
@@ -1529,6 +1530,19 @@ struct Optimizer {
     lw.L = dz(ldlt::tile_doubles(T));
     lw.Linv = dz((size_t)T * ldlt::TB * ldlt::TB);
     lw.z = dz((size_t)ldlt::TB * T);
+    // pipelined factorisation (one launch per solve) for every multi-tile system
+    lw.W = nullptr; lw.du = nullptr; lw.sync = nullptr; lw.tasks = nullptr; lw.ntasks = 0; lw.pipe_T = 0;
+    if (T >= 2 && T <= ldlt::kPipeMaxT && c->ldlt_pipe) {
+      const std::vector<int4>& tq = ldlt::pipe_tasks_host(T);
+      lw.W = dz(ldlt::tile_doubles(T));
+      lw.du = dz((size_t)T * 128);
+      lw.sync = (unsigned*)dz((ldlt::pipe_sync_words(T) + 1) / 2);
+      lw.tasks = (int4*)dz(2 * tq.size());
+      if (he == hipSuccess && lw.tasks)
+        he = hipMemcpyAsync(lw.tasks, tq.data(), tq.size() * sizeof(int4), hipMemcpyHostToDevice, st);
+      lw.ntasks = (int)tq.size();
+      lw.pipe_T = T;
+    }
     // scalars: [0] chi2 [1] point scale [2] pose scale [3] chi_now; the solve flag in [5] (one
     // 48-byte readback per trial)
     d_scalar = dz(8);
@@ -2074,6 +2088,10 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   mcs_ba_ctx* c = new (std::nothrow) mcs_ba_ctx();
   if (!c) return MCS_ERR_ARG;
   c->device = device;
+  {
+    const char* e = std::getenv("MCS_LDLT_PIPE");
+    c->ldlt_pipe = !(e && e[0] == '0');
+  }
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocDefault));
@@ -2356,7 +2374,7 @@ int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const doubl
 
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
                             int32_t* zero_pivot, int32_t path) {
-  if (!S || !b || !x || n < 1 || path < 0 || path > 1) return MCS_ERR_ARG;
+  if (!S || !b || !x || n < 1 || path < 0 || path > 2) return MCS_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     set_error("no HIP device visible (no CPU fallback)");
@@ -2391,7 +2409,14 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
     } else {
       chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
       ldlt::Work w{dL, dI, dz};
+      // path 0 and 2: the pipelined factorisation (one launch); path 1: one launch per step
+      const bool pipe = path == 2 || (path == 0 && T >= 2);
+      if (pipe && rc == MCS_OK) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
       chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
+      if (pipe) {
+        chk(hipStreamSynchronize(st), "sync");
+        ldlt::pipe_release(w);
+      }
     }
     std::vector<double> hx(Np);
     int32_t fl = 0;

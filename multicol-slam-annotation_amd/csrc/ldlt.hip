@@ -18,6 +18,8 @@
 #include <mutex>
 #include <set>
 #include <utility>
+#include <vector>
+#include <algorithm>
 
 namespace mcs {
 namespace ldlt {
@@ -124,6 +126,58 @@ __device__ __forceinline__ void offdiag_block(const double* sA, double* sI, int 
   for (int r = 0; r < 4; r++) sI[(16 * i + k4 + 4 * r) * LS + 16 * j + r16] = -xo[r];
 }
 
+// Panel elimination of columns P..P+15 by wave p (lane l = row l, a[] = row l of the panel),
+// the textbook right-looking step per column J = P + j:
+//   d = a_J[j] (readlane), r = 1/d (v_rcp_f64 + two Newton steps), l = a[j] r,
+//   a[m] -= l a_{P+m}[j]  (m > j)
+// Measured on gfx950 (tools/bench/lat_probe2.hip, one wave): a dependent f64 FMA 7 cycles and
+// an independent one 7 (f64 VALU issues at half the f32 rate), v_rcp_f64 18, readlane -> use
+// 27 per link but ~10 issue cycles per v_readlane_b32, LDS write -> uniform read -> use 77.
+// So the pivot and the next column's entry travel by readlane (they are on the
+// column-to-column chain), the other entries of the column by one LDS write and uniform
+// reads (off the chain: they feed the bulk updates), and every store is deferred past the
+// loop, so the 16 columns are one basic block with no exec-mask branches.  The arithmetic is
+// the same as a column-at-a-time elimination (same operations in the same order).
+// Outputs: L (strict lower) and D (diagonal) of the panel's columns in sA, C^T of the rows
+// below the panel in sA's strict upper triangle (row J, column l >= P + 16).  sx: 128
+// doubles of wave-private LDS scratch.
+__device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double (&a)[16], int* fail) {
+  const int l = threadIdx.x & 63;
+  double lv[16];
+  double dsel = 0.0;
+  bool zero = false;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const int J = P + j;
+    const double cj = a[j];
+    double* buf = sx + (j & 1) * 64;
+    if (j < 14) buf[l] = cj;
+    const double dj = readlane_d(cj, J);
+    zero = zero || (dj == 0.0);
+    if (l == J) dsel = cj;
+    double r = __builtin_amdgcn_rcp(dj);
+    r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
+    r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
+    const double lj = cj * r;
+    lv[j] = lj;
+    if (j < 15) {
+      a[j + 1] = __builtin_fma(-lj, readlane_d(cj, J + 1), a[j + 1]);
+#pragma unroll
+      for (int m = j + 2; m < 16; m++) a[m] = __builtin_fma(-lj, buf[P + m], a[m]);
+    }
+  }
+  // L on and above the diagonal too (scratch of the strict upper triangle; the diagonal is
+  // overwritten by D next, in-order LDS within the wave)
+#pragma unroll
+  for (int k = 0; k < 16; k++) sA[l * LS + P + k] = lv[k];
+  if (l >= P && l < P + 16) sA[l * LS + l] = dsel;
+  if (l >= P + 16) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) sA[(P + k) * LS + l] = a[k];
+  }
+  if (zero && l == 0) *fail = 1;
+}
+
 // LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, blocked by 16-column panels.
 //   panel p (wave p, lane = row): columns 16p..16p+15 are eliminated in registers; the value of
 //     column j at another row comes from v_readlane (one wave: no barrier, no LDS).  The wave
@@ -148,19 +202,8 @@ __device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
       double a[16];
 #pragma unroll
       for (int c = 0; c < 16; c++) a[c] = sA[l * LS + P + c];
-#ifdef MCS_LDLT_FACTOR_V1
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int J = P + j;
-        const double cj = a[j];
-        const double dj = readlane_d(cj, J);
-        const double lj = cj / dj;
-#pragma unroll
-        for (int m = j + 1; m < 16; m++) a[m] = __builtin_fma(-lj, readlane_d(cj, P + m), a[m]);
-        if (dj == 0.0 && l == 0) *fail = 1;
-        if (l >= J) sA[l * LS + J] = (l > J) ? lj : cj;
-        if (l >= P + 16) sA[J * LS + l] = cj;
-      }
+#ifndef MCS_LDLT_FACTOR_STD
+      panel_elim(sA, sI + 62 * LS, P, a, fail);
 #else
       // column broadcast through LDS (sI is scratch until the L^-1 phase): the wave writes its
       // unscaled column once and reads the pivot and the panel rows back with uniform
@@ -289,14 +332,16 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
                                                double* __restrict__ z, int k, int T, int* flag,
                                                const int* skip) {
   if (skip && *skip) return;
-  extern __shared__ double sm[];
+  extern __shared__ __attribute__((aligned(16))) double sm[];
   double* sK = sm;               // A_kk -> L_kk (strict lower) + D (diagonal)
   double* sI = sK + TB * LS;     // Linv_kk
   double* sX = sI + TB * LS;     // A_ik -> G_i = L_ik
   double* sY = sX + TB * LS;     // A_jk -> W_j
   double* sv = sY + TB * LS;     // b_k
   double* su = sv + TB;          // u_k = Linv b_k
-  __shared__ int fail;
+  // LDS ints live in the dynamic region too: a static __shared__ variable would shift the
+  // dynamic base off 16 B and every 16-B LDS access would be replayed (Guideline 17)
+  int& fail = *reinterpret_cast<int*>(su + TB);
   const int t = threadIdx.x;
   const int wg = blockIdx.x;
   int i = -1, j = -1;
@@ -402,7 +447,7 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
                                                      double* __restrict__ x, int T,
                                                      const int* skip) {
   if (skip && *skip) return;
-  extern __shared__ double sx[];   // 64 T: solved blocks of x
+  extern __shared__ __attribute__((aligned(16))) double sx[];   // 64 T: solved blocks of x
   __shared__ double part[16][TB];
   __shared__ double rk[TB];
   const int t = threadIdx.x, c = t & 63, g = t >> 6;
@@ -442,6 +487,370 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pipelined factorisation: ONE launch for the whole LDL^T (instead of one k_panel launch per
+// step, each of whose workgroups re-factors A_kk).  Same arithmetic as the k_panel steps, so
+// the results are bitwise those of the launch-per-step path:
+//   * workgroup "diag" (the holder of ticket 0) walks k = 0 .. T-1: applies the last product
+//     (k, k, k-1) to A_kk and b_k, factors A_kk ONCE (L_kk, D_k, Linv_kk, u_k = Linv b_k,
+//     z_k = u_k / D_k), publishes Linv_kk / D_k / u_k, then forms the next panel tile
+//     L_{k+1,k} = A_{k+1,k} Linv^T D^-1 and W_{k+1,k} = A_{k+1,k} Linv^T itself (look-ahead:
+//     the diagonal chain never waits for another workgroup's hand-off of its own outputs);
+//   * every other workgroup takes tasks from a queue in step-major order:
+//       TRSM (i, k), i >= k + 2:  L_ik, W_ik from A_ik (after products 0..k-1) and Linv_kk;
+//       UPDATE (i, j, k):         A_ij -= L_ik W_jk^T (and b_i -= L_ik u_k when i == j), in k
+//                                 order per tile (a per-tile product counter), except
+//                                 (k+1, k+1, k), which the diag workgroup applies itself.
+// Deadlock freedom does not depend on residency or dispatch order: tickets are taken from one
+// device-scope counter; the diag workgroup at step k waits only on tasks of steps <= k - 1, and
+// every task waits only on earlier tickets or on diag steps <= its own step.  Every wait is
+// bounded (kWaitTicks): a timeout sets the error word and the solve's failure flag, and
+// every workgroup then drains out.
+// Hand-offs (MI355X_MICROARCH.md, visibility; cdna_hip_programming.md Guideline 16, R1):
+// payload stored write-through (sc1: 16-B buffer stores from LDS, 8-B stores from registers),
+// every storing wave drains vmcnt, a workgroup barrier, ONE lane stores the flag / counter
+// (relaxed, agent scope); the consumer's lane 0 polls relaxed with s_sleep, then ONE agent-scope
+// acquire + vmcnt drain before the workgroup barrier, then plain loads.  Flag words are zeroed
+// by a memset on the stream before every launch.
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// a wait gives up after this many ticks of the 100 MHz real-time counter (0.25 s)
+constexpr long long kWaitTicks = 25000000;
+
+__device__ __forceinline__ unsigned pl_load(const unsigned* p) {
+  return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pl_store(unsigned* p, unsigned v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 64x64 tile from LDS (stride LS) to global (row-major), write-through, 16 B per store
+__device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, TB * TB * 8, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = 2 * (threadIdx.x + 256 * i);
+    const d2 v = *reinterpret_cast<const d2*>(&s[(e >> 6) * LS + (e & 63)]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, e * 8, 0, 16);
+  }
+}
+
+// Lane 0 waits until *w_i >= v_i for every non-null word (bounded in time), then acquires; all threads get the
+// outcome (false: timed out here or elsewhere).
+__device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const unsigned* w1, unsigned v1,
+                                     const unsigned* w2, unsigned v2, unsigned* err, int* sh_ok) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      if ((!w0 || pl_load(w0) >= v0) && (!w1 || pl_load(w1) >= v1) && (!w2 || pl_load(w2) >= v2)) break;
+      if (pl_load(err) != 0u) { ok = 0; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { pl_store(err, 1u); ok = 0; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (ok) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *sh_ok = ok;
+  }
+  __syncthreads();
+  // wave-uniform by construction; readfirstlane makes that visible to the compiler, so every
+  // branch on it is a scalar branch (no exec-mask structurisation around the barriers)
+  const bool ok = __builtin_amdgcn_readfirstlane(*sh_ok) != 0;
+  __syncthreads();
+  return ok;
+}
+
+// every storing wave drains its write-through stores, then ONE lane raises the word
+__device__ __forceinline__ void wg_publish(unsigned* word, unsigned v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) pl_store(word, v);
+}
+
+struct PipeArgs {
+  double* A;            // tiles (destroyed)
+  double* b;            // 64 T (destroyed)
+  double* L;            // off-diagonal L tiles (out)
+  double* W;            // off-diagonal W = L D tiles (scratch)
+  double* Linv;         // T x 64 x 64 (out)
+  double* du;           // T x 128: D_k, u_k
+  double* z;            // 64 T (out)
+  unsigned* sync;       // [0] ticket, [1] error, [4..] product counters, panel flags, diag flags
+  const int4* tasks;    // (type 0 TRSM / 1 UPDATE, i, j, k)
+  int ntasks, T, ntile;
+  int* flag;
+  const int* skip;
+};
+
+__device__ __forceinline__ int tix(int I, int J, int T) { return (int)band_tiles(I - J, T) + J; }
+
+#ifdef MCS_LDLT_PROBE
+// probe builds only: diag step stamps [k][8] and task stamps [ticket][4] (s_memrealtime, 100 MHz)
+__device__ long long g_diag_stamps[128 * 8];
+__device__ long long g_task_stamps[65536 * 4];
+#define DSTAMP(k, i) do { if (threadIdx.x == 0 && (k) < 128) g_diag_stamps[(k) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TSTAMP(tk, i) do { if (threadIdx.x == 0 && (tk) < 65536) g_task_stamps[(tk) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define DSTAMP(k, i) do { } while (0)
+#define TSTAMP(tk, i) do { } while (0)
+#endif
+
+#ifdef MCS_PIPE_TRACE
+// debug builds only (tools/bench/pipe_debug.hip): events {wg, code, a, b} into host memory
+__device__ unsigned* g_pipe_trace;
+__device__ unsigned g_pipe_trace_n;
+__device__ __forceinline__ void ptrace(unsigned code, unsigned a, unsigned b) {
+  if (threadIdx.x == 0 && g_pipe_trace) {
+    const unsigned i = atomicAdd(&g_pipe_trace_n, 1u);
+    if (i < 65536) {
+      unsigned* e = g_pipe_trace + 4 * (size_t)i;
+      __hip_atomic_store(e + 1, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(e + 2, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(e + 3, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(e + 0, blockIdx.x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+#define PTRACE(c, a, b) ptrace((c), (unsigned)(a), (unsigned)(b))
+#else
+#define PTRACE(c, a, b) do { } while (0)
+#endif
+
+// W = X Linv^T (registers, wave-row layout), then sX <- W D^-1 (= L), sY <- W, as k_panel does
+__device__ __forceinline__ void trsm_to_lds(double* sX, double* sY, const double* sI, const double* dvec) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = l & 15, k4 = l >> 4;
+  d4 wi[4];
+  gemm_xlt(sX, sI, wi);
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int col = 16 * c + r16;
+    const double invd = 1.0 / dvec[col];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = 16 * w + k4 + 4 * r;
+      sX[row * LS + col] = wi[c][r] * invd;
+      sY[row * LS + col] = wi[c][r];
+    }
+  }
+  __syncthreads();
+}
+
+// A_kk's entries in the accumulator layout (rows 16q + k4 + 4r, column 16w + r16)
+__device__ __forceinline__ void load_acc(double (&a)[4][4], const double* Aij) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = l & 15, k4 = l >> 4;
+  const int col = 16 * w + r16;
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) a[q][r] = Aij[(16 * q + k4 + 4 * r) * TB + col];
+}
+
+__device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) {
+  double* sK = sm;
+  double* sI = sK + TB * LS;
+  double* sX = sI + TB * LS;
+  double* sY = sX + TB * LS;
+  double* sv = sY + TB * LS;
+  double* su = sv + TB;
+  const int T = g.T, t = threadIdx.x, l = t & 63, w = t >> 6, r16 = l & 15, k4 = l >> 4;
+  unsigned* err = g.sync + 1;
+  unsigned* cnt = g.sync + 4;
+  unsigned* pan = cnt + g.ntile;
+  unsigned* dg = pan + g.ntile;
+  for (int k = 0; k < T; k++) {
+    PTRACE(10, k, 0);
+    DSTAMP(k, 0);
+    // A_kk after products 0 .. k-2 (UPDATE tasks), then product k-1 from the tiles this
+    // workgroup formed at step k-1 (still in sX / sY, u_{k-1} in su)
+    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok)) break;
+    DSTAMP(k, 1);
+    double a[4][4];
+    load_acc(a, g.A + toff(k, k, T));
+    double bv = g.b[k * TB + (t >> 2)];
+    if (k >= 1) {
+      d4 p[4];
+      gemm_xyt(sX, sY, p);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) a[q][r] = a[q][r] - p[q][r];
+      bv -= gemv_row(sX, su);
+    }
+    __syncthreads();
+    {
+      const int col = 16 * w + r16;
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = 16 * q + k4 + 4 * r;
+          sK[row * LS + col] = (col > row) ? 0.0 : a[q][r];
+        }
+    }
+    if ((t & 3) == 0) sv[t >> 2] = bv;
+    if (t == 0) *fail = 0;
+    __syncthreads();
+    DSTAMP(k, 2);
+    factor_tile(sK, sI, fail);
+    {
+      const double u = gemv_row(sI, sv);
+      if ((t & 3) == 0) su[t >> 2] = u;
+    }
+    __syncthreads();
+    store_tile_sc1(g.Linv + (size_t)k * TB * TB, sI);
+    if (t < TB) {
+      const double dk = sK[t * LS + t];
+      st_sc1(g.du + (size_t)k * 128 + t, dk);
+      st_sc1(g.du + (size_t)k * 128 + TB + t, su[t]);
+      g.z[k * TB + t] = su[t] / dk;
+    }
+    if (t == 0 && *fail) *g.flag = 1;
+    DSTAMP(k, 3);
+    wg_publish(dg + k, 1u);
+    PTRACE(11, k, 0);
+    DSTAMP(k, 4);
+    if (k + 1 < T) {
+      // the next panel tile: A_{k+1,k} after products 0 .. k-1
+      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok)) break;
+      DSTAMP(k, 5);
+      {
+        d2 v[8];
+        fetch_tile(v, g.A + toff(k + 1, k, T));
+        put_tile(sX, v);
+      }
+      if (t < TB) sv[t] = sK[t * LS + t];
+      __syncthreads();
+      trsm_to_lds(sX, sY, sI, sv);
+      store_tile_sc1(g.L + toff(k + 1, k, T), sX);
+      store_tile_sc1(g.W + toff(k + 1, k, T), sY);
+      wg_publish(pan + tix(k + 1, k, T), 1u);
+      PTRACE(12, k, 0);
+      DSTAMP(k, 6);
+    }
+  }
+  if (t == 0 && pl_load(err) != 0u) *g.flag = 1;
+}
+
+__device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_ok, int tk) {
+  double* sI = sm + TB * LS;
+  double* sX = sI + TB * LS;
+  double* sY = sX + TB * LS;
+  double* sv = sY + TB * LS;
+  const int T = g.T, t = threadIdx.x;
+  unsigned* err = g.sync + 1;
+  unsigned* cnt = g.sync + 4;
+  unsigned* pan = cnt + g.ntile;
+  unsigned* dg = pan + g.ntile;
+  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok)) return false;
+  TSTAMP(tk, 1);
+  {
+    d2 vx[8], vi[8];
+    fetch_tile(vx, g.A + toff(i, k, T));
+    fetch_tile(vi, g.Linv + (size_t)k * TB * TB);
+    if (t < TB) sv[t] = g.du[(size_t)k * 128 + t];
+    put_tile(sX, vx);
+    put_tile(sI, vi);
+  }
+  __syncthreads();
+  TSTAMP(tk, 2);
+  trsm_to_lds(sX, sY, sI, sv);
+  store_tile_sc1(g.L + toff(i, k, T), sX);
+  store_tile_sc1(g.W + toff(i, k, T), sY);
+  wg_publish(pan + tix(i, k, T), 1u);
+  return true;
+}
+
+__device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, int* sh_ok, int tk) {
+  double* sX = sm + 2 * TB * LS;
+  double* sY = sX + TB * LS;
+  double* su = sY + TB * LS + TB;
+  const int T = g.T, t = threadIdx.x, l = t & 63, w = t >> 6, r16 = l & 15, k4 = l >> 4;
+  unsigned* err = g.sync + 1;
+  unsigned* cnt = g.sync + 4;
+  unsigned* pan = cnt + g.ntile;
+  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok))
+    return false;
+  TSTAMP(tk, 1);
+  double a[4][4];
+  double bv = 0.0;
+  {
+    d2 vx[8], vy[8];
+    fetch_tile(vx, g.L + toff(i, k, T));
+    fetch_tile(vy, g.W + toff(j, k, T));
+    load_acc(a, g.A + toff(i, j, T));
+    if (i == j) {
+      bv = g.b[i * TB + (t >> 2)];
+      if (t < TB) su[t] = g.du[(size_t)k * 128 + TB + t];
+    }
+    put_tile(sX, vx);
+    put_tile(sY, vy);
+  }
+  __syncthreads();
+  TSTAMP(tk, 2);
+  d4 p[4];
+  gemm_xyt(sX, sY, p);
+  {
+    double* Aij = g.A + toff(i, j, T);
+    const int col = 16 * w + r16;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) st_sc1(&Aij[(16 * q + k4 + 4 * r) * TB + col], a[q][r] - p[q][r]);
+  }
+  if (i == j) {
+    const double s = gemv_row(sX, su);
+    if ((t & 3) == 0) st_sc1(&g.b[i * TB + (t >> 2)], bv - s);
+  }
+  wg_publish(cnt + tix(i, j, T), (unsigned)(k + 1));
+  __syncthreads();   // LDS tiles are rewritten by the next task
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
+  if (g.skip && *g.skip) return;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  int* ish = reinterpret_cast<int*>(sm + 4 * TB * LS + 2 * TB);   // dynamic region (Guideline 17)
+  int& sh_tk = ish[0];
+  int& sh_ok = ish[1];
+  int& fail = ish[2];
+  for (;;) {
+    if (threadIdx.x == 0) sh_tk = (int)atomicAdd(g.sync, 1u);
+    __syncthreads();
+    const int tk = __builtin_amdgcn_readfirstlane(sh_tk);
+    __syncthreads();
+    PTRACE(1, tk, 0);
+    if (tk == 0) {
+      diag_role(g, sm, &sh_ok, &fail);
+      break;
+    }
+    if (tk > g.ntasks) break;
+    const int4 tq = g.tasks[tk - 1];
+    const int ty = __builtin_amdgcn_readfirstlane(tq.x), ti = __builtin_amdgcn_readfirstlane(tq.y);
+    const int tj = __builtin_amdgcn_readfirstlane(tq.z), tkk = __builtin_amdgcn_readfirstlane(tq.w);
+    PTRACE(2, ty, (ti << 16) | (tj << 8) | tkk);
+    TSTAMP(tk, 0);
+    const bool ok = ty == 0 ? trsm_task(g, ti, tkk, sm, &sh_ok, tk) : update_task(g, ti, tj, tkk, sm, &sh_ok, tk);
+    TSTAMP(tk, 3);
+    PTRACE(3, ok, 0);
+    if (!ok) {
+      if (threadIdx.x == 0) *g.flag = 1;
+      break;
+    }
+  }
+}
+
+}  // namespace
+
 __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int T, double dv,
                       const int* skip) {
   if (skip && *skip) return;
@@ -464,13 +873,13 @@ __global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, co
                                                 double* __restrict__ x, int n, double dv, int* flag,
                                                 const int* skip) {
   if (skip && *skip) return;
-  extern __shared__ double sm[];
+  extern __shared__ __attribute__((aligned(16))) double sm[];
   double* sK = sm;               // A -> L (strict lower) + D (diagonal)
   double* sI = sK + TB * LS;     // Linv
   double* sv = sI + TB * LS;     // b, then z
   double* su = sv + TB;          // u
   double* part = su + TB;        // [16][TB]
-  __shared__ int fail;
+  int& fail = *reinterpret_cast<int*>(part + 16 * TB);
   const int t = threadIdx.x;
   if (t == 0) fail = 0;
   d2 vK[8];
@@ -512,7 +921,7 @@ __global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, co
 
 }  // namespace
 
-constexpr size_t kSolve1Lds = (2 * (size_t)TB * LS + 18 * TB) * sizeof(double);
+constexpr size_t kSolve1Lds = (2 * (size_t)TB * LS + 18 * TB) * sizeof(double) + 16;
 
 // hipFuncSetAttribute applies to the current device: set each kernel's dynamic-LDS limit once
 // per (kernel, device), under a lock (a process may drive several GPUs from several threads)
@@ -538,14 +947,89 @@ hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, do
   return hipGetLastError();
 }
 
-constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double);
+constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double) + 16;
+
+// Task table of the pipelined factorisation, step-major: for each k the TRSM tasks (i, k),
+// i = k+2 .. T-1, then the UPDATE tasks (i, j, k) by column j = k+1 .. T-1 and row i = j .. T-1,
+// except (k+1, k+1, k) (the diag workgroup's).  Every task waits only on earlier tickets or on
+// diag steps <= k, which in turn wait only on tasks of steps <= k - 1.
+static std::vector<int4> pipe_tasks(int T) {
+  std::vector<int4> v;
+  for (int k = 0; k + 1 < T; k++) {
+    for (int i = k + 2; i < T; i++) v.push_back(make_int4(0, i, k, k));
+    for (int j = k + 1; j < T; j++)
+      for (int i = j; i < T; i++)
+        if (!(i == k + 1 && j == k + 1)) v.push_back(make_int4(1, i, j, k));
+  }
+  return v;
+}
+
+size_t pipe_sync_words(int T) {
+  const size_t ntile = (size_t)T * (T + 1) / 2;
+  return (4 + 2 * ntile + (size_t)T + 3) & ~(size_t)3;   // multiple of 16 B
+}
+
+const std::vector<int4>& pipe_tasks_host(int T) {
+  static std::mutex mu;
+  static std::vector<int4> cache[kPipeMaxT + 1];
+  static bool made[kPipeMaxT + 1] = {};
+  std::lock_guard<std::mutex> g(mu);
+  if (!made[T]) { cache[T] = pipe_tasks(T); made[T] = true; }
+  return cache[T];   // never reallocated afterwards: safe as an async-copy source
+}
+
+hipError_t pipe_prepare(Work& w, int T, hipStream_t st) {
+  if (T < 1 || T > kPipeMaxT) return hipErrorInvalidValue;
+  const std::vector<int4>& tasks = pipe_tasks_host(T);
+  hipError_t e = hipMalloc(&w.W, tile_doubles(T) * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&w.du, (size_t)T * 128 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&w.sync, pipe_sync_words(T) * sizeof(unsigned));
+  if (e == hipSuccess && !tasks.empty()) e = hipMalloc(&w.tasks, tasks.size() * sizeof(int4));
+  if (e == hipSuccess && !tasks.empty())
+    e = hipMemcpyAsync(w.tasks, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  w.ntasks = (int)tasks.size();
+  w.pipe_T = T;
+  return e;
+}
+
+void pipe_release(Work& w) {
+  for (void* p : {(void*)w.W, (void*)w.du, (void*)w.sync, (void*)w.tasks})
+    if (p) (void)hipFree(p);
+  w.W = nullptr; w.du = nullptr; w.sync = nullptr; w.tasks = nullptr; w.ntasks = 0; w.pipe_T = 0;
+}
+
+static int device_cus() {
+  static std::mutex mu;
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  std::lock_guard<std::mutex> g(mu);
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
 
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st,
                  const int* skip) {
   hipError_t e = set_lds_limit((const void*)k_panel, (int)kPanelLds);
   if (e == hipSuccess) e = set_lds_limit((const void*)k_backward, 96 * 1024);
+  if (e == hipSuccess) e = set_lds_limit((const void*)k_pipe, (int)kPanelLds);
   if (e != hipSuccess) return e;
   if ((size_t)T * TB * sizeof(double) > 96 * 1024) return hipErrorInvalidValue;
+  if (w.sync && w.pipe_T == T) {
+    e = hipMemsetAsync(w.sync, 0, pipe_sync_words(T) * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, T * (T + 1) / 2, flag, skip};
+    const int grid = std::max(1, std::min(device_cus(), w.ntasks + 1));
+    hipLaunchKernelGGL(k_pipe, dim3(grid), dim3(256), kPanelLds, st, g);
+    hipLaunchKernelGGL(k_backward, dim3(1), dim3(kBwdNT), (size_t)T * TB * sizeof(double), st,
+                       (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T, skip);
+    return hipGetLastError();
+  }
   for (int k = 0; k < T; k++) {
     const int m = T - 1 - k;
     const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);

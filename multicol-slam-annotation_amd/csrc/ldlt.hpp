@@ -14,6 +14,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
+#include <vector>
 
 namespace mcs {
 namespace ldlt {
@@ -39,7 +40,23 @@ struct Work {
   double* L;      // tile_doubles(T): off-diagonal L blocks (I > J)
   double* Linv;   // T * 64 * 64: inverse of each unit-lower diagonal L block
   double* z;      // 64 T: D^-1 L^-1 b
+  // pipelined factorisation (one launch, see ldlt.hip), set up by pipe_prepare for one T;
+  // without it solve() runs one k_panel launch per step
+  double* W = nullptr;        // tile_doubles(T): W_ik = L_ik D_k
+  double* du = nullptr;       // T * 128: D_k, u_k
+  unsigned* sync = nullptr;   // pipe_sync_words(T): ticket, error, product counters, flags
+  int4* tasks = nullptr;      // task table
+  int ntasks = 0;
+  int pipe_T = 0;
 };
+
+// largest tile count the pipelined path is set up for (task table ~T^3/6 entries)
+constexpr int kPipeMaxT = 96;
+size_t pipe_sync_words(int T);
+hipError_t pipe_prepare(Work& w, int T, hipStream_t st);   // allocates W, du, sync, tasks
+// the task table for T tiles (host copy, cached for the process: a valid async-copy source)
+const std::vector<int4>& pipe_tasks_host(int T);
+void pipe_release(Work& w);
 
 // A: tiles (destroyed), b: 64 T (destroyed), x: 64 T (out).  *flag (device) = 1 on an
 // exact zero pivot, else left untouched (callers clear it).  All launches on st.

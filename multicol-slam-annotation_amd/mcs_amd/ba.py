@@ -747,17 +747,20 @@ Solver.global_ba = _solver_global_ba
 Solver.optimize_sharded = _solver_optimize_sharded
 
 
-def dense_ldlt_solve(S, b, device=0, tiled=False):
+def dense_ldlt_solve(S, b, device=0, tiled=False, path=None):
     """Device LDL^T solve of the reduced camera system (test hook) -> (x, zero_pivot).
-    tiled=True forces the pad + panel + backward kernels even for n <= 64."""
+    tiled=True forces the pad + per-step panel + backward kernels even for n <= 64 (path 1);
+    path=2 forces the pipelined factorisation (one launch); default path 0 = what BA uses."""
     from . import lib, _check
     S = np.ascontiguousarray(S, np.float64)
     b = np.ascontiguousarray(b, np.float64)
     n = S.shape[0]
     x = np.zeros(n)
     zp = ctypes.c_int32()
+    if path is None:
+        path = 1 if tiled else 0
     _check(lib().mcs_dense_ldlt_solve_ex(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp),
-                                         1 if tiled else 0))
+                                         int(path)))
     return x, zp.value
 
 

@@ -177,6 +177,33 @@ def test_gpu_one_tile_solve_matches_tiled(gpu, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [65, 128, 129, 300, 700, 1194])
+def test_gpu_pipelined_solve_matches_per_step(gpu, n):
+    """The pipelined factorisation (one launch: a diagonal workgroup factoring each A_kk once
+    with look-ahead, TRSM / UPDATE tasks from a device queue) is bitwise the one-launch-per-step
+    path (same operations in the same order), including a zero pivot in a later tile."""
+    from mcs_amd import ba
+    rng = np.random.default_rng(500 + n)
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    x1, z1 = ba.dense_ldlt_solve(S, b, path=1)
+    x2, z2 = ba.dense_ldlt_solve(S, b, path=2)
+    assert z1 == z2 == 0
+    assert x1.tobytes() == x2.tobytes()
+    ref = np.linalg.solve(S, b)
+    assert np.allclose(x2, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+    S2 = S.copy()
+    k = n - 3
+    S2[k, :] = 0.0
+    S2[:, k] = 0.0
+    x1, z1 = ba.dense_ldlt_solve(S2, b, path=1)
+    x2, z2 = ba.dense_ldlt_solve(S2, b, path=2)
+    assert z1 == z2 == 1
+    assert np.array_equal(x1, x2, equal_nan=True)
+
+
+@pytest.mark.gpu
 def test_gpu_dense_ldlt_zero_pivot(gpu):
     from mcs_amd import ba
     S = np.eye(70)

@@ -15,7 +15,7 @@ __global__ __launch_bounds__(256) void k_probe(const double* A, double* outL, do
   extern __shared__ double sm[];
   double* sK = sm;
   double* sI = sK + TB * LS;
-  __shared__ int fail;
+  int& fail = *reinterpret_cast<int*>(sI + TB * LS);
   long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) fail = 0;
   load_tile_lower(sK, A);
@@ -62,7 +62,7 @@ int main() {
   (void)hipMalloc(&dA, 4096 * 8); (void)hipMalloc(&dL, 4096 * 8); (void)hipMalloc(&dI, 4096 * 8);
   (void)hipMalloc(&dS, 16 * 8);
   (void)hipMemcpy(dA, h.data(), 4096 * 8, hipMemcpyHostToDevice);
-  const size_t lds = 2 * 64 * LS * 8;
+  const size_t lds = 2 * 64 * LS * 8 + 16;
   (void)hipFuncSetAttribute((const void*)k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   bool ok = true;
   for (int rep = 0; rep < 3; rep++) {
