@@ -252,6 +252,22 @@ int mcs_ba_read_host_timing(mcs_ba_ctx* c, double* ms, int32_t* n_calls, int32_t
  * negative status. */
 int mcs_ba_check_structure(mcs_ba_ctx* c, const mcs_ba_problem* p, const uint8_t* edge_level);
 
+/* Test hook: the device Levenberg-Marquardt control of the product (the function the device-
+ * driven optimisation runs after every trial: OptimizationAlgorithmLevenberg::solve's accept /
+ * reject and lambda schedule, optimization_algorithm_levenberg.cpp:99-189, Raul's nBad stop,
+ * and SparseOptimizerTerminateAction, sparse_optimizer_terminate_action.cpp:43-72) replayed on
+ * scripted trial outcomes.  in3 = {initial robust chi2, max |diag Hll|, max |diag Hpp|};
+ * trials [n][4] = {trial robust chi2, points' model decrease, poses' model decrease, solve
+ * failed (0/1)}; out [n][10] per consumed trial = {lambda used, lambda after, ni, accepted,
+ * qmax, nBad, iterations done, done, terminate flag, currentChi}; *n_out = trials consumed
+ * (the replay stops when the optimisation is done). */
+int mcs_ba_lm_replay(int32_t device, const mcs_ba_options* o, const double* in3, const double* trials,
+                     int32_t n, double* out, int32_t* n_out);
+/* Test hook: the product's robust kernel (RobustKernelHuber::robustify,
+ * robust_kernel_impl.cpp:78-91, delta^2 held as float as robust_kernel_impl.h:84 declares it) on
+ * n squared errors: rho0 = rho(e), rho1 = rho'(e). */
+int mcs_ba_huber_eval(int32_t device, const double* e, int32_t n, double delta, double* rho0, double* rho1);
+
 /* Test hook for the dense reduced-camera solve (LinearSolverEigen::solve,
  * ThirdParty/g2o/g2o/solvers/linear_solver_eigen.h:94-126): S is n x n row-major (lower
  * triangle read), b and x length n.  *zero_pivot = 1 when the LDL^T meets an exact zero. */

@@ -201,6 +201,12 @@ __device__ void edge_jac(const double* pose, const double* X, const double* mc, 
     }
 }
 
+// RobustKernelHuber keeps delta^2 in a FLOAT member (ThirdParty/g2o/g2o/core/robust_kernel_impl.h:84,
+// `float dsqr;`, set by setDelta as dsqr = delta*delta, robust_kernel_impl.cpp:65-69), so the
+// inlier test and rho(e) = 2 sqrt(e) delta - dsqr use delta^2 rounded to float.  (The culling
+// thresholds of cOptimizer, thHuber2 = thHuber*thHuber, stay double: src/cOptimizer.cpp:436.)
+static inline double huber_dsqr(double delta) { return (double)(float)(delta * delta); }
+
 __device__ __forceinline__ void huber(double e, double delta, double dsqr, double* rho0, double* rho1) {
   if (e <= dsqr) { *rho0 = e; *rho1 = 1.; }
   else { const double sq = sqrt(e); *rho0 = 2 * sq * delta - dsqr; *rho1 = delta / sq; }
@@ -421,6 +427,10 @@ __host__ __device__ inline double cube_rn(double x) {
   const double p = x * x;
   const double pe = __builtin_fma(x, x, -p);       // x^2 = p + pe exactly
   const double h = p * x;
+  // overflow: pow(x, 3) returns +-inf (the error terms would turn it into NaN, and the LM's
+  // alpha = 1 - pow(2 rho - 1, 3) must become -inf so that lambda *= 1/3; g2o_solver.npz
+  // scenario 27 has such a step)
+  if (!__builtin_isfinite(h)) return h;
   const double he = __builtin_fma(p, x, -h);       // p x = h + he exactly
   return h + (he + pe * x);
 }
@@ -510,19 +520,25 @@ __global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d, Sum3 q, LmEnd le) {
 }
 
 // chi2 of the starting point -> currentChi (the optimize() call's activeRobustChi2)
+__device__ __forceinline__ void lm_start_body(LmCtl* c, double chi) {
+  c->chi0 = chi;
+  c->currentChi = chi;
+  c->iniChi = chi;
+}
 __global__ void k_lm_start(LmCtl* c, const double* sc) {
   if (threadIdx.x != 0) return;
-  c->chi0 = sc[0];
-  c->currentChi = sc[0];
-  c->iniChi = sc[0];
+  lm_start_body(c, sc[0]);
 }
 // lambda of iteration 0: tau * max diagonal (computeLambdaInit,
-// optimization_algorithm_levenberg.cpp:166-180)
-__global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
-  if (threadIdx.x != 0 || c->done) return;
-  c->lambda = c->tau * fmax(sc[1], sc[2]);
+// optimization_algorithm_levenberg.cpp:166-180); pt / pose = max |diagonal| of Hll / Hpp
+__device__ __forceinline__ void lm_lambda0_body(LmCtl* c, double pt, double pose) {
+  c->lambda = c->tau * fmax(pt, pose);
   c->ni = 2;
   c->nBad = 0;
+}
+__global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
+  if (threadIdx.x != 0 || c->done) return;
+  lm_lambda0_body(c, sc[1], sc[2]);
 }
 // after a trial (k_edges_end's last workgroup, one thread): OptimizationAlgorithmLevenberg::solve's accept / reject
 // (optimization_algorithm_levenberg.cpp:99-163) and, when the iteration ends, the terminate
@@ -589,6 +605,36 @@ __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig) {
       }
     }
   }
+}
+
+// Test hooks (mcs_ba_lm_replay, mcs_ba_huber_eval): the production device functions replayed on
+// scripted inputs, so the LM control and the robust kernel can be checked statement for
+// statement against the reference text (tests/golden/gen_g2o_solver.py).
+// in = {chi0, maxdiag points, maxdiag poses}; trials [n][4] = {robust chi2 of the trial,
+// points' model decrease, poses' model decrease, solve failed}; out [n][10] per trial =
+// {lambda used, lambda after, ni, accepted, qmax, nBad, iterations done, done, stop_out,
+// currentChi}.  One thread.
+__global__ void k_lm_replay(LmCtl* c, LmSig* sig, const double* in, const double* trials, int n,
+                            double* out, int* n_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  lm_start_body(c, in[0]);
+  if (!c->done) lm_lambda0_body(c, in[1], in[2]);
+  int t = 0;
+  for (; t < n && !c->done; t++) {
+    const double* tr = trials + 4 * t;
+    const double sc[3] = {tr[0], tr[1], tr[2]};
+    const double lam = c->lambda;
+    lm_control(c, sc, tr[3] != 0.0 ? 1 : 0, sig);
+    double* o = out + 10 * t;
+    o[0] = lam; o[1] = c->lambda; o[2] = c->ni; o[3] = c->restore ? 0.0 : 1.0; o[4] = c->qmax;
+    o[5] = c->nBad; o[6] = c->iter; o[7] = c->done; o[8] = c->stop_out; o[9] = c->currentChi;
+  }
+  *n_out = t;
+}
+
+__global__ void k_huber_eval(const double* e, int n, double delta, double dsqr, double* rho0, double* rho1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) huber(e[i], delta, dsqr, &rho0[i], &rho1[i]);
 }
 
 // launch helper: part = kRedPartMax doubles of scratch (stream-ordered reuse is safe)
@@ -1500,7 +1546,7 @@ struct Optimizer {
       he = pk.flush(c);
     }
     d.delta = p->huber_delta;
-    d.dsqr = p->huber_delta * p->huber_delta;
+    d.dsqr = huber_dsqr(p->huber_delta);
     d.poses = d_poses; d.points = d_points; d.poses_bk = d_poses_bk; d.points_bk = d_points_bk;
     d.nae = (int)s.aedge.size();
     d.np = s.np; d.nl = s.nl;
@@ -2349,7 +2395,7 @@ int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double
   d.e_cam = up_raw(c, p->edge_cam, NE, he);
   d.e_meas = up_raw(c, p->edge_meas, 2 * (size_t)NE, he);
   d.e_info = up_raw(c, p->edge_info, NE, he);
-  d.delta = p->huber_delta; d.dsqr = p->huber_delta * p->huber_delta;
+  d.delta = p->huber_delta; d.dsqr = huber_dsqr(p->huber_delta);
   d.poses = up_raw(c, p->poses, 6 * (size_t)p->n_poses, he);
   d.points = up_raw(c, p->points, 3 * (size_t)p->n_points, he);
   std::vector<int32_t> all(NE);
@@ -2365,6 +2411,80 @@ int mcs_ba_linearize(mcs_ba_ctx* c, const mcs_ba_problem* p, double* err, double
   MCS_HIP_CHECK(hipMemcpyAsync(jac_point, d.jl, 48 * (size_t)NE, hipMemcpyDeviceToHost, c->st));
   MCS_HIP_CHECK(hipStreamSynchronize(c->st));
   return MCS_OK;
+}
+
+int mcs_ba_lm_replay(int32_t device, const mcs_ba_options* o, const double* in3, const double* trials,
+                     int32_t n, double* out, int32_t* n_out) {
+  if (!o || !in3 || (n > 0 && (!trials || !out)) || !n_out || n < 0) {
+    set_error("lm_replay: null argument or n < 0");
+    return MCS_ERR_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device visible (no CPU fallback)");
+    return MCS_ERR_NO_DEVICE;
+  }
+  MCS_HIP_CHECK(hipSetDevice(device));
+  LmCtl h0;
+  std::memset(&h0, 0, sizeof(h0));
+  h0.tau = o->tau; h0.gain_threshold = o->gain_threshold;      // as run_device sets them
+  h0.max_iterations = o->max_iterations; h0.max_trials = o->max_trials;
+  h0.terminate_max_iter = o->terminate_max_iter;
+  h0.lin = 1; h0.ni = 2;
+  h0.done = o->max_iterations <= 0 ? 1 : 0;
+  LmCtl* dc = nullptr; LmSig* ds = nullptr; double *din = nullptr, *dtr = nullptr, *dout = nullptr; int* dn = nullptr;
+  int rc = MCS_OK;
+  auto chk = [&](hipError_t e, const char* w) { if (e != hipSuccess && rc == MCS_OK) { set_hip_error(e, w, __FILE__, __LINE__); rc = MCS_ERR_HIP; } };
+  chk(hipMalloc(&dc, sizeof(LmCtl)), "malloc"); chk(hipMalloc(&ds, sizeof(LmSig)), "malloc");
+  chk(hipMalloc(&din, 3 * 8), "malloc"); chk(hipMalloc(&dtr, std::max(1, n) * 32), "malloc");
+  chk(hipMalloc(&dout, std::max(1, n) * 80), "malloc"); chk(hipMalloc(&dn, 4), "malloc");
+  if (rc == MCS_OK) {
+    chk(hipMemcpy(dc, &h0, sizeof(h0), hipMemcpyHostToDevice), "h2d");
+    chk(hipMemset(ds, 0, sizeof(LmSig)), "memset");
+    chk(hipMemcpy(din, in3, 3 * 8, hipMemcpyHostToDevice), "h2d");
+    if (n) chk(hipMemcpy(dtr, trials, (size_t)n * 32, hipMemcpyHostToDevice), "h2d");
+    chk(hipMemset(dn, 0, 4), "memset");
+    hipLaunchKernelGGL(k_lm_replay, dim3(1), dim3(64), 0, 0, dc, ds, (const double*)din, (const double*)dtr, n, dout, dn);
+    chk(hipGetLastError(), "launch");
+    chk(hipDeviceSynchronize(), "sync");
+    int32_t m = 0;
+    chk(hipMemcpy(&m, dn, 4, hipMemcpyDeviceToHost), "d2h");
+    if (rc == MCS_OK && m) chk(hipMemcpy(out, dout, (size_t)m * 80, hipMemcpyDeviceToHost), "d2h");
+    *n_out = m;
+  }
+  for (void* q : {(void*)dc, (void*)ds, (void*)din, (void*)dtr, (void*)dout, (void*)dn})
+    if (q) (void)hipFree(q);
+  return rc;
+}
+
+int mcs_ba_huber_eval(int32_t device, const double* e, int32_t n, double delta, double* rho0, double* rho1) {
+  if (n < 0 || (n > 0 && (!e || !rho0 || !rho1))) {
+    set_error("huber_eval: null argument or n < 0");
+    return MCS_ERR_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device visible (no CPU fallback)");
+    return MCS_ERR_NO_DEVICE;
+  }
+  if (n == 0) return MCS_OK;
+  MCS_HIP_CHECK(hipSetDevice(device));
+  double *de = nullptr, *d0 = nullptr, *d1 = nullptr;
+  int rc = MCS_OK;
+  auto chk = [&](hipError_t x, const char* w) { if (x != hipSuccess && rc == MCS_OK) { set_hip_error(x, w, __FILE__, __LINE__); rc = MCS_ERR_HIP; } };
+  chk(hipMalloc(&de, (size_t)n * 8), "malloc"); chk(hipMalloc(&d0, (size_t)n * 8), "malloc");
+  chk(hipMalloc(&d1, (size_t)n * 8), "malloc");
+  if (rc == MCS_OK) {
+    chk(hipMemcpy(de, e, (size_t)n * 8, hipMemcpyHostToDevice), "h2d");
+    hipLaunchKernelGGL(k_huber_eval, dim3((n + 255) / 256), dim3(256), 0, 0, (const double*)de, n, delta,
+                       huber_dsqr(delta), d0, d1);
+    chk(hipGetLastError(), "launch");
+    chk(hipMemcpy(rho0, d0, (size_t)n * 8, hipMemcpyDeviceToHost), "d2h");
+    chk(hipMemcpy(rho1, d1, (size_t)n * 8, hipMemcpyDeviceToHost), "d2h");
+  }
+  for (void* q : {(void*)de, (void*)d0, (void*)d1})
+    if (q) (void)hipFree(q);
+  return rc;
 }
 
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
@@ -2409,14 +2529,13 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
     } else {
       chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
       ldlt::Work w{dL, dI, dz};
-      // path 0 and 2: the pipelined factorisation (one launch); path 1: one launch per step
-      const bool pipe = path == 2 || (path == 0 && T >= 2);
-      if (pipe && rc == MCS_OK) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
+      // path 0 and 2: the pipelined factorisation (one launch); path 1: one launch per step;
+      // both with the multi-workgroup backward substitution
+      if (rc == MCS_OK) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
+      w.per_step = (path == 1);
       chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
-      if (pipe) {
-        chk(hipStreamSynchronize(st), "sync");
-        ldlt::pipe_release(w);
-      }
+      chk(hipStreamSynchronize(st), "sync");
+      ldlt::pipe_release(w);
     }
     std::vector<double> hx(Np);
     int32_t fl = 0;

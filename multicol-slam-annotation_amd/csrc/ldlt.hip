@@ -141,43 +141,247 @@ __device__ __forceinline__ void offdiag_block(const double* sA, double* sI, int 
 // Outputs: L (strict lower) and D (diagonal) of the panel's columns in sA, C^T of the rows
 // below the panel in sA's strict upper triangle (row J, column l >= P + 16).  sx: 128
 // doubles of wave-private LDS scratch.
+__device__ __forceinline__ void panel_bulk(double (&a)[16], const double (&cm)[16], double lj, int m0, int m1) {
+#pragma unroll
+  for (int m = m0; m < m1; m++)
+    if (m < 16) a[m] = __builtin_fma(-lj, cm[m], a[m]);
+}
+
 __device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double (&a)[16], int* fail) {
   const int l = threadIdx.x & 63;
-  double lv[16];
+  double lv[16], cm[16], cn[16];
   double dsel = 0.0;
-  bool zero = false;
+  // software pipelined: iteration j finishes column j, publishes column j+1 to LDS and issues
+  // the reads of its entries at once (they are consumed an iteration later), and computes the
+  // reciprocal of the next pivot in between its own bulk updates; sched_barriers pin that
+  // interleaving (the compiler otherwise issues bulk updates ahead of the chain and stalls the
+  // in-order wave on them)
+  sx[l] = a[0];
+#pragma unroll
+  for (int m = 2; m < 16; m++) cn[m] = sx[P + m];
+  double dn = readlane_d(a[0], P), c1 = readlane_d(a[0], P + 1);
+  double r = __builtin_amdgcn_rcp(dn);
+  r = __builtin_fma(r, __builtin_fma(-dn, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-dn, r, 1.0), r);
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const int J = P + j;
+#pragma unroll
+    for (int m = j + 2; m < 16; m++) cm[m] = cn[m];
     const double cj = a[j];
-    double* buf = sx + (j & 1) * 64;
-    if (j < 14) buf[l] = cj;
-    const double dj = readlane_d(cj, J);
-    zero = zero || (dj == 0.0);
-    if (l == J) dsel = cj;
-    double r = __builtin_amdgcn_rcp(dj);
-    r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
-    r = __builtin_fma(r, __builtin_fma(-dj, r, 1.0), r);
     const double lj = cj * r;
     lv[j] = lj;
-    if (j < 15) {
-      a[j + 1] = __builtin_fma(-lj, readlane_d(cj, J + 1), a[j + 1]);
-#pragma unroll
-      for (int m = j + 2; m < 16; m++) a[m] = __builtin_fma(-lj, buf[P + m], a[m]);
+    if (j == 15) {
+      if (l == J) dsel = cj;
+      break;
     }
+    a[j + 1] = __builtin_fma(-lj, c1, a[j + 1]);
+    double c1n = 0.0;
+    if (j + 1 <= 13) {
+      double* bn = sx + ((j + 1) & 1) * 64;
+      bn[l] = a[j + 1];
+#ifdef MCS_LDLT_PIVOT_RL
+      dn = readlane_d(a[j + 1], J + 1);
+      c1n = readlane_d(a[j + 1], J + 2);
+#else
+      dn = bn[J + 1];
+      c1n = bn[J + 2];
+#endif
+#pragma unroll
+      for (int m = j + 3; m < 16; m++) cn[m] = bn[P + m];
+    } else {
+      dn = readlane_d(a[j + 1], J + 1);
+      if (j + 1 <= 14) c1n = readlane_d(a[j + 1], J + 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 2, j + 5);
+    if (l == J) dsel = cj;
+    __builtin_amdgcn_sched_barrier(0);
+    double rn = __builtin_amdgcn_rcp(dn);
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 5, j + 7);
+    __builtin_amdgcn_sched_barrier(0);
+    double e = __builtin_fma(-dn, rn, 1.0);
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 7, j + 8);
+    __builtin_amdgcn_sched_barrier(0);
+    rn = __builtin_fma(rn, e, rn);
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 8, j + 9);
+    __builtin_amdgcn_sched_barrier(0);
+    e = __builtin_fma(-dn, rn, 1.0);
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 9, j + 10);
+    __builtin_amdgcn_sched_barrier(0);
+    rn = __builtin_fma(rn, e, rn);
+    __builtin_amdgcn_sched_barrier(0);
+    panel_bulk(a, cm, lj, j + 10, 16);
+    r = rn;
+    c1 = c1n;
   }
   // L on and above the diagonal too (scratch of the strict upper triangle; the diagonal is
   // overwritten by D next, in-order LDS within the wave)
 #pragma unroll
   for (int k = 0; k < 16; k++) sA[l * LS + P + k] = lv[k];
-  if (l >= P && l < P + 16) sA[l * LS + l] = dsel;
+  const bool diag = (l >= P && l < P + 16);
+  if (diag) sA[l * LS + l] = dsel;
   if (l >= P + 16) {
 #pragma unroll
     for (int k = 0; k < 16; k++) sA[(P + k) * LS + l] = a[k];
   }
-  if (zero && l == 0) *fail = 1;
+  if (__any(diag && dsel == 0.0) && l == 0) *fail = 1;
 }
 
+// Partial sum of an off-diagonal block of L^-1: s += L_ik X_kj (one wave, MFMA), the k-th term
+// of S_ij = sum_{k=j}^{i-1} L_ik X_kj in offdiag_block's order (callers add k ascending).
+__device__ __forceinline__ void xsum_add(const double* sA, const double* sI, d4& s, int i, int k, int j) {
+  const int l = threadIdx.x & 63, r16 = l & 15, k4 = l >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    const double av = sA[(16 * i + r16) * LS + 16 * k + k0 + k4];   // L_ik[m][kk]
+    const double bv = sI[(16 * k + k0 + k4) * LS + 16 * j + r16];   // X_kj[kk][n]
+    s = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, s, 0, 0, 0);
+  }
+}
+// X_ij = -X_ii S_ij (one wave, MFMA), S in accumulator (= B-operand) layout, as offdiag_block
+__device__ __forceinline__ void xfinish(double* sI, const d4& s, int i, int j) {
+  const int l = threadIdx.x & 63, r16 = l & 15, k4 = l >> 4;
+  d4 xo = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const double av = sI[(16 * i + r16) * LS + 16 * i + 4 * r + k4];  // X_ii[m][4r + kk]
+    xo = __builtin_amdgcn_mfma_f64_16x16x4f64(av, s[r], xo, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) sI[(16 * i + k4 + 4 * r) * LS + 16 * j + r16] = -xo[r];
+}
+// Trailing update of the 16x16 block (bi, bj) by panel p: A_{bi,bj} -= C_{bi,p} L_{bj,p}^T
+// (C^T from sA's upper triangle), one wave, four MFMAs.
+__device__ __forceinline__ void upd_block(double* sA, int p, int bi, int bj) {
+  const int l = threadIdx.x & 63, r16 = l & 15, k4 = l >> 4, P = 16 * p;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    const double av = sA[(P + k0 + k4) * LS + 16 * bi + r16];   // C[16 bi + m][P + k]
+    const double bv = sA[(16 * bj + r16) * LS + P + k0 + k4];   // L[16 bj + n][P + k]
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) sA[(16 * bi + k4 + 4 * r) * LS + 16 * bj + r16] -= acc[r];
+}
+
+// LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, blocked by 16-column panels,
+// with every block operation that is off the column-to-column chain moved beside the next
+// panel's elimination (which occupies one wave; the other three were idle):
+//   panel p        : wave p eliminates columns 16p..16p+15 (panel_elim);
+//   urgent update  : the block column p+1 of the trailing matrix (the next panel's input), one
+//                    16x16 block per wave (upd_block), between two barriers;
+//   beside panel p : the deferred trailing blocks of panel p-1 (not needed before panel p+1),
+//                    X_{p-1,p-1} = inverse of the previous diagonal block (inv_diag16) and the
+//                    partial sums S_ij = sum_k L_ik X_kj of the off-diagonal L^-1 blocks whose
+//                    inputs are final;
+//   tail           : X_33, then X_3j = -X_33 S_3j.
+// Every block is updated by its panels in panel order and every S_ij accumulates k ascending
+// in one wave's registers, so the arithmetic is the same as a panel-at-a-time factorisation
+// followed by offdiag_block (same operations in the same order per element).  7 barriers.
+// On return sA holds L (strict lower) and D (diagonal), sI holds L^-1 (0 above the diagonal).
+__device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  double* sx = sI + 62 * LS;   // panel scratch (block row 3 of sI is written last)
+  d4 s0 = {0.0, 0.0, 0.0, 0.0}, s1 = {0.0, 0.0, 0.0, 0.0};
+  // ---- panel 0; the other waves clear the strict upper blocks of L^-1
+  if (w == 0) {
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = sA[l * LS + c];
+    panel_elim(sA, sx, 0, a, fail);
+  } else {
+    for (int e = t - 64; e < TB * TB; e += 192) {
+      const int rr = e >> 6, cc = e & 63;
+      if ((cc >> 4) > (rr >> 4)) sI[rr * LS + cc] = 0.0;
+    }
+  }
+  __syncthreads();
+  LDLT_STAMP(0);
+  if (w >= 1) upd_block(sA, 0, w, 1);               // urgent: block column 1
+  __syncthreads();
+  // ---- panel 1 | X00 | panel-0 blocks (2,2), (3,2), (3,3)
+  if (w == 1) {
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = sA[l * LS + 16 + c];
+    panel_elim(sA, sx, 16, a, fail);
+  } else if (w == 0) {
+    inv_diag16(sA, sI, 0);
+  } else if (w == 2) {
+    upd_block(sA, 0, 2, 2);
+    upd_block(sA, 0, 3, 2);
+  } else {
+    upd_block(sA, 0, 3, 3);
+  }
+  __syncthreads();
+  LDLT_STAMP(1);
+  if (w >= 2) upd_block(sA, 1, w, 2);               // urgent: block column 2
+  __syncthreads();
+  // ---- panel 2 | X11 | S20, S30 (k = 0) | panel-1 block (3,3)
+  if (w == 2) {
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = sA[l * LS + 32 + c];
+    panel_elim(sA, sx, 32, a, fail);
+  } else if (w == 1) {
+    inv_diag16(sA, sI, 16);
+  } else if (w == 0) {
+    xsum_add(sA, sI, s0, 2, 0, 0);                  // S20
+    xsum_add(sA, sI, s1, 3, 0, 0);                  // S30
+  } else {
+    upd_block(sA, 1, 3, 3);
+  }
+  __syncthreads();
+  LDLT_STAMP(2);
+  if (w == 3) upd_block(sA, 2, 3, 3);               // urgent: block column 3
+  __syncthreads();
+  // ---- panel 3 | X22 | X10, S21, S31 (k = 1)
+  if (w == 3) {
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) a[c] = sA[l * LS + 48 + c];
+    panel_elim(sA, sx, 48, a, fail);
+  } else if (w == 2) {
+    inv_diag16(sA, sI, 32);
+  } else if (w == 1) {
+    d4 s10 = {0.0, 0.0, 0.0, 0.0};
+    xsum_add(sA, sI, s10, 1, 0, 0);
+    xfinish(sI, s10, 1, 0);                         // X10
+    xsum_add(sA, sI, s0, 2, 1, 1);                  // S21
+    xsum_add(sA, sI, s1, 3, 1, 1);                  // S31 (k = 1)
+  }
+  __syncthreads();
+  LDLT_STAMP(3);
+  // ---- X33 | S20, S30 (k = 1), X20, S30 (k = 2) | X21, then S31 (k = 2) | S32
+  if (w == 3) {
+    inv_diag16(sA, sI, 48);
+  } else if (w == 0) {
+    xsum_add(sA, sI, s0, 2, 1, 0);                  // S20 (k = 1)
+    xsum_add(sA, sI, s1, 3, 1, 0);                  // S30 (k = 1)
+    xfinish(sI, s0, 2, 0);
+    __builtin_amdgcn_wave_barrier();
+    xsum_add(sA, sI, s1, 3, 2, 0);
+  } else if (w == 1) {
+    xfinish(sI, s0, 2, 1);
+    __builtin_amdgcn_wave_barrier();
+    xsum_add(sA, sI, s1, 3, 2, 1);
+  } else {
+    xsum_add(sA, sI, s1, 3, 2, 2);                  // S32
+  }
+  __syncthreads();
+  LDLT_STAMP(4);
+  if (w < 3) xfinish(sI, s1, 3, w);                 // X30, X31, X32
+  __syncthreads();
+  LDLT_STAMP(8);
+}
+
+#ifdef MCS_LDLT_FACTOR_V0
 // LDL^T of the 64x64 tile in sA (lower triangle read) and L^-1, blocked by 16-column panels.
 //   panel p (wave p, lane = row): columns 16p..16p+15 are eliminated in registers; the value of
 //     column j at another row comes from v_readlane (one wave: no barrier, no LDS).  The wave
@@ -193,7 +397,7 @@ __device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double
 // The column-at-a-time version this replaces needed one barrier and a 64-row exchange per
 // column (~138k cycles per tile); here 8 barriers remain.
 // On return sA holds L (strict lower) and D (diagonal), sI holds L^-1 (0 above the diagonal).
-__device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
+__device__ __forceinline__ void factor_tile_v0(double* sA, double* sI, int* fail) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int r16 = l & 15, k4 = l >> 4;
   for (int p = 0; p < 4; p++) {
@@ -273,6 +477,8 @@ __device__ __forceinline__ void factor_tile(double* sA, double* sI, int* fail) {
     __syncthreads();
   }
 }
+
+#endif
 
 // acc = X Y^T (64x64x64), wave w owns output columns [16w, 16w+16), acc[q] rows [16q, 16q+16)
 // v_mfma_f64_16x16x4_f64: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15];
@@ -849,6 +1055,109 @@ __global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
   }
 }
 
+// Backward substitution L^T x = z across workgroups (one launch): the workgroup holding
+// ticket t owns block column k = T - 1 - t and forms
+//   r_k = z_k - sum_{i > k} L_ik^T x_i,   x_k = Linv_kk^T r_k,
+// accumulating L_ik^T x_i as each x_i is published (i descending, the next tile prefetched
+// into registers while it waits), so only the x_{k+1} term and the Linv product follow the
+// hand-off of x_{k+1}.  Tickets make it deadlock-free without co-residency (a column waits only
+// on columns with earlier tickets).  x_k is published write-through (8-B sc1 stores, every
+// storing wave drained, then one flag), read with sc1 loads (MICROARCH visibility table, row 1).
+// Thread (c = t & 63, q = t >> 6) sums rows q + 4m of each tile; x_k = Linv^T r_k uses
+// k_solve1's partial layout and order (16 row groups), so a one-tile system gives the bits of
+// the fused one-tile solve.  sync: [0] ticket, [1] error, [4 .. 4+T) column flags.
+__global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const double* __restrict__ Linv,
+                                             const double* __restrict__ z, double* x, unsigned* sync,
+                                             int T, int* flag, const int* skip) {
+  if (skip && *skip) return;
+  extern __shared__ __attribute__((aligned(16))) double bsm[];
+  double* part = bsm;              // [16][64]
+  double* rk = part + 16 * TB;     // [64]
+  int* ish = reinterpret_cast<int*>(rk + TB);
+  const int t = threadIdx.x, c = t & 63, q = t >> 6;
+  unsigned* err = sync + 1;
+  unsigned* xf = sync + 4;
+  if (t == 0) ish[0] = (int)atomicAdd(sync, 1u);
+  __syncthreads();
+  const int tk = __builtin_amdgcn_readfirstlane(ish[0]);
+  if (tk >= T) return;
+  const int k = T - 1 - tk;
+  // Linv_kk in registers: rows g + 16 h (h = 0..3) of the row groups g = q + 4 m (m = 0..3)
+  double iv[4][4];
+  {
+    const double* I = Linv + (size_t)k * TB * TB;
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+      for (int h = 0; h < 4; h++) iv[m][h] = I[(q + 4 * m + 16 * h) * TB + c];
+  }
+  double acc = 0.0;
+  double lt[16];
+  if (k + 1 < T) {
+    const double* Lt = L + toff(T - 1, k, T);
+#pragma unroll
+    for (int m = 0; m < 16; m++) lt[m] = Lt[(q + 4 * m) * TB + c];
+  }
+  bool ok = true;
+  for (int i = T - 1; i > k; i--) {
+    // wait for x_i
+    if (t == 0) {
+      int good = 1;
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (pl_load(xf + i) == 0u) {
+        if (pl_load(err) != 0u) { good = 0; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { pl_store(err, 1u); good = 0; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      ish[1] = good;
+    }
+    __syncthreads();
+    ok = __builtin_amdgcn_readfirstlane(ish[1]) != 0;
+    __syncthreads();
+    if (!ok) break;
+    double xv[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      xv[m] = __longlong_as_double((long long)__hip_atomic_load((const gu64*)(x + (size_t)i * TB + q + 4 * m),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    double cur[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++) cur[m] = lt[m];
+    if (i - 1 > k) {   // prefetch the next tile while this one is summed
+      const double* Lt = L + toff(i - 1, k, T);
+#pragma unroll
+      for (int m = 0; m < 16; m++) lt[m] = Lt[(q + 4 * m) * TB + c];
+    }
+#pragma unroll
+    for (int m = 0; m < 16; m++) acc = __builtin_fma(cur[m], xv[m], acc);
+  }
+  if (ok) {
+    part[q * TB + c] = acc;
+    __syncthreads();
+    if (t < TB) rk[t] = z[(size_t)k * TB + t] - (((part[t] + part[TB + t]) + part[2 * TB + t]) + part[3 * TB + t]);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int g = q + 4 * m;
+      double u = iv[m][0] * rk[g] + iv[m][1] * rk[g + 16];
+      u += iv[m][2] * rk[g + 32] + iv[m][3] * rk[g + 48];
+      part[g * TB + c] = u;
+    }
+    __syncthreads();
+    if (t < TB) {
+      double a = 0.0;
+#pragma unroll
+      for (int g = 0; g < 16; g++) a += part[g * TB + t];
+      st_sc1(x + (size_t)k * TB + t, a);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) pl_store(xf + k, 1u);
+  } else if (t == 0) {
+    *flag = 1;
+  }
+}
+
 }  // namespace
 
 __global__ void k_pad(double* __restrict__ A, double* __restrict__ b, int n, int T, double dv,
@@ -964,10 +1273,15 @@ static std::vector<int4> pipe_tasks(int T) {
   return v;
 }
 
+static size_t bwd_sync_words(int T) { return (4 + (size_t)T + 3) & ~(size_t)3; }
+
 size_t pipe_sync_words(int T) {
+  // factorisation words, then the backward's (ticket, error, column flags); multiple of 16 B
   const size_t ntile = (size_t)T * (T + 1) / 2;
-  return (4 + 2 * ntile + (size_t)T + 3) & ~(size_t)3;   // multiple of 16 B
+  return ((4 + 2 * ntile + (size_t)T + 3) & ~(size_t)3) + bwd_sync_words(T);
 }
+
+constexpr size_t kBwdLds = (17 * (size_t)TB) * sizeof(double) + 16;
 
 const std::vector<int4>& pipe_tasks_host(int T) {
   static std::mutex mu;
@@ -1024,10 +1338,18 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
     e = hipMemsetAsync(w.sync, 0, pipe_sync_words(T) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, T * (T + 1) / 2, flag, skip};
-    const int grid = std::max(1, std::min(device_cus(), w.ntasks + 1));
-    hipLaunchKernelGGL(k_pipe, dim3(grid), dim3(256), kPanelLds, st, g);
-    hipLaunchKernelGGL(k_backward, dim3(1), dim3(kBwdNT), (size_t)T * TB * sizeof(double), st,
-                       (const double*)w.L, (const double*)w.Linv, (const double*)w.z, x, T, skip);
+    if (w.per_step) {
+      for (int k = 0; k < T; k++) {
+        const int m = T - 1 - k;
+        const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);
+        hipLaunchKernelGGL(k_panel, dim3(grid), dim3(256), kPanelLds, st, A, b, w.L, w.Linv, w.z, k, T, flag, skip);
+      }
+    } else {
+      const int grid = std::max(1, std::min(device_cus(), w.ntasks + 1));
+      hipLaunchKernelGGL(k_pipe, dim3(grid), dim3(256), kPanelLds, st, g);
+    }
+    hipLaunchKernelGGL(k_bwd, dim3(T), dim3(256), kBwdLds, st, (const double*)w.L, (const double*)w.Linv,
+                       (const double*)w.z, x, w.sync + pipe_sync_words(T) - bwd_sync_words(T), T, flag, skip);
     return hipGetLastError();
   }
   for (int k = 0; k < T; k++) {

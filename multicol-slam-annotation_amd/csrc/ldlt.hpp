@@ -48,6 +48,7 @@ struct Work {
   int4* tasks = nullptr;      // task table
   int ntasks = 0;
   int pipe_T = 0;
+  bool per_step = false;      // with the pipeline's sync words: one k_panel launch per step
 };
 
 // largest tile count the pipelined path is set up for (task table ~T^3/6 entries)

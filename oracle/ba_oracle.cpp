@@ -221,6 +221,10 @@ void edge_jac(const double* pose, const double* X, const double* mc, const doubl
     }
 }
 
+// RobustKernelHuber::dsqr is a float member (ThirdParty/g2o/g2o/core/robust_kernel_impl.h:84),
+// setDelta stores delta*delta into it (robust_kernel_impl.cpp:65-69)
+static inline double huber_dsqr(double delta) { return (double)(float)(delta * delta); }
+
 struct Huber {
   double delta, dsqr;
   void robustify(double e, double* rho) const {
@@ -630,7 +634,7 @@ int oracle_ba_optimize(const mcs_ba_problem* p, const mcs_ba_options* o, double*
   g.level.assign(p->n_edges, 0);
   if (edge_level) g.level.assign(edge_level, edge_level + p->n_edges);
   g.hk.delta = p->huber_delta;
-  g.hk.dsqr = p->huber_delta * p->huber_delta;
+  g.hk.dsqr = huber_dsqr(p->huber_delta);
   optimize(g, *o, stop_flag, rep);
   std::memcpy(poses, g.poses.data(), sizeof(double) * 6 * p->n_poses);
   std::memcpy(points, g.points.data(), sizeof(double) * 3 * p->n_points);
@@ -661,7 +665,7 @@ int oracle_global_ba(const mcs_ba_problem* p, int32_t pose_only, double* poses, 
   g.level.assign(p->n_edges, 0);
   g.points_fixed = pose_only != 0;
   g.hk.delta = p->huber_delta;
-  g.hk.dsqr = p->huber_delta * p->huber_delta;
+  g.hk.dsqr = huber_dsqr(p->huber_delta);
   optimize(g, o, stop_flag, rep);
   std::memcpy(poses, g.poses.data(), sizeof(double) * 6 * p->n_poses);
   std::memcpy(points, g.points.data(), sizeof(double) * 3 * p->n_points);
@@ -682,7 +686,7 @@ int oracle_ba_partial_schur(const mcs_ba_problem* p, const double* pose_cnt, dou
   g.level.assign(p->n_edges, 0);
   g.pose_cnt = pose_cnt;
   g.hk.delta = p->huber_delta;
-  g.hk.dsqr = p->huber_delta * p->huber_delta;
+  g.hk.dsqr = huber_dsqr(p->huber_delta);
   g.initialize();
   g.err.assign(2 * p->n_edges, 0.0);
   g.compute_errors();
@@ -869,7 +873,7 @@ int oracle_pose_optimization(const mcs_ba_problem* p, double* pose, uint8_t* out
     g.level = level;
     g.points_fixed = true;
     g.hk.delta = p->huber_delta;
-    g.hk.dsqr = th2;
+    g.hk.dsqr = huber_dsqr(p->huber_delta);
     optimize(g, o, &aux, rep);
     std::memcpy(pose, g.poses.data(), sizeof(double) * 6);
     std::vector<double> chi(N);

@@ -4,7 +4,7 @@ The generators (gen_refmath.py, gen_mcsjacs1.py, gen_g2o_solver.py) cut function
 the reference checkout -- untrusted input -- and rewrite them into Python.  Before anything
 runs, the translated source is parsed with `ast` and rejected unless every node is on a small
 whitelist: numbers / strings / None / bools, names (no dunder names), arithmetic, comparison
-and boolean operators, subscripts, tuples / dicts, assignments, `if`, `for ... in range(...)`,
+and boolean operators, subscripts, tuples / dicts, assignments, `if`, `while` / `break`, `for ... in range(...)`,
 `def` / `return`, and calls whose target is a plain name or one of a few whitelisted attributes
 (`Matx.make`, `.t()`, `math.sqrt`, ...).  The code then runs with an empty `__builtins__`, so
 a name resolves only to what the generator put in the environment.  A crafted statement such
@@ -15,7 +15,7 @@ import ast
 
 _NODES = (
     ast.Module, ast.Expression, ast.FunctionDef, ast.arguments, ast.arg, ast.Return,
-    ast.Assign, ast.AugAssign, ast.If, ast.For, ast.Pass, ast.Expr,
+    ast.Assign, ast.AugAssign, ast.If, ast.For, ast.While, ast.Break, ast.Pass, ast.Expr,
     ast.Name, ast.Load, ast.Store, ast.Constant, ast.Tuple, ast.List, ast.Dict,
     ast.Subscript, ast.Slice,
     ast.Call, ast.Attribute,
@@ -42,8 +42,8 @@ def check(src, mode="exec"):
             raise UnsafeSource("attribute %r not allowed in translated reference code" % node.attr)
         if isinstance(node, ast.Constant) and not isinstance(node.value, (int, float, bool, str, type(None))):
             raise UnsafeSource("constant %r not allowed" % (node.value,))
-        if isinstance(node, ast.Call) and not isinstance(node.func, (ast.Name, ast.Attribute)):
-            raise UnsafeSource("call target must be a name or a whitelisted attribute")
+        if isinstance(node, ast.Call) and not isinstance(node.func, (ast.Name, ast.Attribute, ast.Subscript)):
+            raise UnsafeSource("call target must be a name, a whitelisted attribute or a subscript")
         if isinstance(node, ast.For):
             it = node.iter
             if not (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"):

@@ -21,7 +21,11 @@ __global__ __launch_bounds__(256) void k_probe(const double* A, double* outL, do
   load_tile_lower(sK, A);
   __syncthreads();
   long long t1 = __builtin_amdgcn_s_memtime();
+#ifdef MCS_LDLT_FACTOR_V0
+  factor_tile_v0(sK, sI, &fail);
+#else
   factor_tile(sK, sI, &fail);
+#endif
   long long t2 = __builtin_amdgcn_s_memtime(), r2 = __builtin_amdgcn_s_memrealtime();
   for (int e = threadIdx.x; e < 4096; e += 256) {
     const int r = e >> 6, c = e & 63;
@@ -35,7 +39,7 @@ __global__ __launch_bounds__(256) void k_probe(const double* A, double* outL, do
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
   std::vector<double> h(4096);
   for (int i = 0; i < 64; i++)
     for (int j = 0; j < 64; j++) h[i * 64 + j] = (i == j) ? 70.0 : 1.0 / (1 + i + j);
@@ -90,6 +94,13 @@ int main() {
                 "\"clock_mhz\": %.0f, \"fail\": %lld, \"err_L\": %.3e, \"err_D\": %.3e, "
                 "\"err_Linv\": %.3e, \"upper_Linv\": %.3e}\n",
                 s[0], s[1], s[2], s[3] / 100.0, s[2] / (s[3] / 100.0), s[4], eL, eD, eI, eU);
+  }
+  if (argc > 1) {   // dump L (with D) and L^-1 of the last rep for a bitwise comparison
+    std::vector<double> oL(4096), oI(4096);
+    (void)hipMemcpy(oL.data(), dL, 4096 * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(oI.data(), dI, 4096 * 8, hipMemcpyDeviceToHost);
+    FILE* f = std::fopen(argv[1], "wb");
+    if (f) { std::fwrite(oL.data(), 8, 4096, f); std::fwrite(oI.data(), 8, 4096, f); std::fclose(f); }
   }
   std::printf(ok ? "LDLT PROBE OK\n" : "LDLT PROBE MISMATCH\n");
   return ok ? 0 : 1;

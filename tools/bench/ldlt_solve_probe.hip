@@ -36,10 +36,14 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&dL, tiles.size() * 8); (void)hipMalloc(&dLi, (size_t)T * TB * TB * 8);
   (void)hipMalloc(&dz, Np * 8); (void)hipMalloc(&dflag, 4);
   Work w{dL, dLi, dz};
+  if (mode != 3) {   // mode 3: the legacy path (no sync words: single-workgroup k_backward)
+    if (pipe_prepare(w, T, 0) != hipSuccess) { std::printf("pipe_prepare (per-step) failed\n"); return 2; }
+    w.per_step = true;
+  }
   std::vector<double> x(Np), xp(Np);
   // pipelined path first (its own Work), then the launch-per-step path below; x must agree
   // bitwise
-  if (mode != 1) {
+  if (mode != 1 && mode != 3) {
     double *pA, *pb, *px, *pL, *pLi, *pz;
     (void)hipMalloc(&pA, tiles.size() * 8); (void)hipMalloc(&pb, Np * 8); (void)hipMalloc(&px, Np * 8);
     (void)hipMalloc(&pL, tiles.size() * 8); (void)hipMalloc(&pLi, (size_t)T * TB * TB * 8);
@@ -151,8 +155,10 @@ int main(int argc, char** argv) {
   std::printf("residual %.3e\n", rmax);
   size_t ndiff = 0;
   for (int r = 0; r < Np; r++) ndiff += (x[r] != xp[r]);
-  std::printf("pipelined vs launch-per-step: %zu of %d entries differ\n", ndiff, Np);
-  if (ndiff) return 1;
+  if (mode == 0) {
+    std::printf("pipelined vs launch-per-step: %zu of %d entries differ\n", ndiff, Np);
+    if (ndiff) return 1;
+  }
   std::printf("step  wgs  load(med/max)  factor(med/max)  W-gemms(med/max)  upd-gemm(med/max)  tail(med/max)  total(max) [cycles]\n");
   for (int k = 0; k < T && k < 32; k++) {
     const int m = T - 1 - k, nwg = std::min(256, 1 + m * (m + 1) / 2);
