@@ -20,6 +20,7 @@ all-gather of the per-camera blocks).
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -140,6 +141,8 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     lock = threading.Lock()
     cpus = baseline_cpus(ncams)
 
+    match_s = [0.0] * ncams
+
     def work(c):
         nonlocal nkp
         if len(cpus) == ncams:   # fresh thread: pinned for its whole life
@@ -150,10 +153,13 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
             descs[t][c] = d
             with lock:
                 nkp += len(k)
+        tm = time.perf_counter()
         for t in range(1, n_multiframes):
             q, tr = descs[t - 1][c], descs[t][c]
             top2[t - 1][c] = ob.hamming_top2(q, tr)
+        match_s[c] = time.perf_counter() - tm
 
+    ob.stage_ns(reset=True)
     t0 = time.perf_counter()
     ths = [threading.Thread(target=work, args=(c,)) for c in range(ncams)]
     for th in ths:
@@ -163,7 +169,12 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     dt = time.perf_counter() - t0
     sample = "%d multi-frames x %d cams (extract+match), oracle restatement; %s" % (
         n_multiframes, ncams, pin_note(cpus if len(cpus) == ncams else []))
-    return nkp / dt / 1e3, sample, ncams, (kpss, descs, top2)
+    ns = ob.stage_ns(reset=True)
+    nf = n_multiframes * ncams
+    stages = {k: round(float(v) / 1e6 / nf, 3) for k, v in
+              zip(("pyramid", "fast", "octree", "ic_angle", "blur_desc"), ns)}
+    stages["match_per_pair"] = round(1e3 * sum(match_s) / max(1, (n_multiframes - 1) * ncams), 3)
+    return nkp / dt / 1e3, sample, ncams, (kpss, descs, top2), stages
 
 
 def check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, ncams):
@@ -405,6 +416,133 @@ def run_config_d(args, rank, world, local_rank, dev, stream):
             "problem": "config D: 8 cams 1024x1024, 4000 feat/cam, %d multi-frames per step" % MD}
 
 
+def run_triangulation(args, rank, world, dev, stream, d_kps, d_cnt, d_desc, cap, ncams, U):
+    """SearchForTriangulationRaw as CreateNewMapPoints drives it (src/cLocalMapping.cpp:223-266
+    -> src/cORBmatcher.cpp:968-1156): the current keyframe against its 5 best covisible
+    neighbours, one device call per neighbour, on the keyframes the timed extraction produced
+    (multi-frame 5 against multi-frames 0..4: 3 cameras x up to 2000 keypoints each), with
+    keypoint rays from the Lafida omni model (ImgToWorld) and E from mcs_compute_e_rig.  Timed
+    with events on the launch stream over `tri_reps` keyframes; untimed afterwards, every
+    neighbour's match list is checked against the oracle.  Reported beside the headline."""
+    if args.tri_reps <= 0 or U < 6:
+        return None, None
+    import torch
+    import mcs_amd
+    from mcs_amd import synth
+    L = mcs_amd.lib()
+    cams = [synth.LAFIDA_CAMS[c % len(synth.LAFIDA_CAMS)] for c in range(ncams)]
+    cnt = d_cnt.cpu().numpy()
+    kps = d_kps.view(-1, cap, 7)
+    rng = np.random.default_rng(31 + rank)
+    kf = []
+    for t in range(6):
+        fr = [t * ncams + c for c in range(ncams)]
+        desc = torch.cat([d_desc[f, :cnt[f]] for f in fr]).contiguous()
+        xy = torch.cat([kps[f, :cnt[f], :2] for f in fr]).cpu().numpy().view(np.float32).astype(np.float64)
+        cam = np.concatenate([np.full(cnt[f], c, np.int32) for c, f in enumerate(fr)])
+        rays = np.zeros((len(cam), 3))
+        for c in range(ncams):
+            sel = cam == c
+            x, y, z = synth.img_to_world(cams[c], xy[sel, 0], xy[sel, 1])
+            rays[sel] = np.stack([x, y, z], 1)
+        has = (rng.random(len(cam)) < 0.3).astype(np.uint8)   # keypoints already tracked
+        kf.append(dict(desc=desc, cam=cam, rays=rays, has=has, n=len(cam),
+                       d_cam=torch.from_numpy(cam).to(dev), d_rays=torch.from_numpy(rays).to(dev),
+                       d_has=torch.from_numpy(has).to(dev)))
+    mc = np.array(synth.LAFIDA_MC[:ncams], np.float64)
+    Es = []
+    for j in range(5):
+        mt1 = np.array([0.0, 0.0, 0.0, 0.0, 0.0, 0.0])
+        mt2 = np.array([0.01 * (j + 1), -0.005 * j, 0.002, 0.05 * (j + 1), 0.01, -0.02 * j])
+        E = np.zeros((ncams, ncams, 9))
+        assert L.mcs_compute_e_rig(mt1.ctypes.data, mt2.ctypes.data, mc.ctypes.data, ncams,
+                                   E.ctypes.data) == 0
+        Es.append(E)
+    d_E = [torch.from_numpy(E).to(dev) for E in Es]
+    th_low, thresh = 64, 1e-2   # TH_LOW (32 B, unmasked) and CheckDistEpipolarLine's 1e-2
+    n1 = kf[5]["n"]
+    n2max = max(k["n"] for k in kf[:5])
+    ws = ctypes.c_void_p()
+    if L.mcs_tri_workspace_create(dev.index, n1, n2max, ctypes.byref(ws)) != 0:
+        raise RuntimeError("tri workspace: " + L.mcs_last_error().decode())
+    out = [torch.empty(n1, dtype=torch.int32, device=dev) for _ in range(5)]
+    nm = torch.empty(5, dtype=torch.int32, device=dev)
+    k1 = kf[5]
+
+    def one_kf():
+        for j in range(5):
+            k2 = kf[j]
+            rc = L.mcs_search_for_triangulation_raw_device(
+                ws, k1["desc"].data_ptr(), None, k1["d_cam"].data_ptr(), k1["d_has"].data_ptr(),
+                k1["d_rays"].data_ptr(), n1, k2["desc"].data_ptr(), None, k2["d_cam"].data_ptr(),
+                k2["d_has"].data_ptr(), k2["d_rays"].data_ptr(), k2["n"], ncams, d_E[j].data_ptr(),
+                32, th_low, thresh, out[j].data_ptr(), nm[j:].data_ptr(), stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError("triangulation: " + L.mcs_last_error().decode())
+
+    for _ in range(3):
+        one_kf()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(args.tri_reps):
+        one_kf()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.tri_reps
+    # host entry (host buffers in and out, one synchronisation per neighbour), for comparison
+    hd1 = k1["desc"].cpu().numpy()
+    hd2 = [k["desc"].cpu().numpy() for k in kf[:5]]
+    t0 = time.perf_counter()
+    reps_h = max(1, min(5, args.tri_reps))
+    for _ in range(reps_h):
+        for j in range(5):
+            got = np.zeros(n1, np.int32)
+            n = ctypes.c_int32()
+            rc = L.mcs_search_for_triangulation_raw(
+                hd1.ctypes.data, k1["cam"].ctypes.data, k1["has"].ctypes.data, k1["rays"].ctypes.data,
+                n1, hd2[j].ctypes.data, kf[j]["cam"].ctypes.data, kf[j]["has"].ctypes.data,
+                kf[j]["rays"].ctypes.data, kf[j]["n"], ncams, Es[j].ctypes.data, 32, th_low, thresh,
+                got.ctypes.data, ctypes.byref(n))
+            if rc != 0:
+                raise RuntimeError("triangulation host entry failed")
+    ms_host = (time.perf_counter() - t0) / reps_h * 1e3
+    L.mcs_tri_workspace_destroy(ws)
+    same_cam = sum(int(sum(int((k1["cam"] == c).sum()) * int((kf[j]["cam"] == c).sum())
+                           for c in range(ncams))) for j in range(5))
+    res = {"ms_per_keyframe": round(ms, 4), "neighbours": 5,
+           "host_entry_ms_per_keyframe": round(ms_host, 3),
+           "distances_per_s": round(same_cam / (ms / 1e3), 1),
+           "matches_per_neighbour": [int(v) for v in nm.cpu().numpy()],
+           "keypoints": {"kf1": n1, "neighbours": [k["n"] for k in kf[:5]]},
+           "th_low": th_low, "epi_thresh": thresh,
+           "path": "mcs_search_for_triangulation_raw_device: k_tri_radius + k_tri_private + k_tri_shared"}
+    cpu = None
+    if rank == 0 and world == 1:
+        from tests import oracle_bind as ob
+        t0 = time.perf_counter()
+        refs = []
+        for j in range(5):
+            ref = np.zeros(n1, np.int32)
+            ob.lib().oracle_search_for_triangulation_raw_ex(
+                hd1.ctypes.data, None, n1, hd2[j].ctypes.data, None, kf[j]["n"], 32,
+                k1["cam"].ctypes.data, kf[j]["cam"].ctypes.data, k1["has"].ctypes.data,
+                kf[j]["has"].ctypes.data, np.ascontiguousarray(k1["rays"]).ctypes.data,
+                np.ascontiguousarray(kf[j]["rays"]).ctypes.data, Es[j].ctypes.data, thresh, ncams,
+                ref.ctypes.data)
+            refs.append(ref)
+        tc = time.perf_counter() - t0
+        for j in range(5):
+            if not np.array_equal(out[j].cpu().numpy(), refs[j]):
+                raise RuntimeError("bench parity: triangulation neighbour %d differs from the oracle" % j)
+        res["oracle_check"] = "5 of 5 neighbour match lists bit-exact"
+        if not args.no_cpu_baseline:
+            cpu = {"value": round(1e3 * tc, 2), "unit": "ms per keyframe (5 neighbours)", "cores": 1,
+                   "kind": "port", "sample": "the same 5 neighbour searches, oracle restatement, "
+                   "single thread (unpinned)"}
+    return res, cpu
+
+
 def run_bow(args, rank, world, dev, stream, d_desc, n_valid):
     """DBoW2 transform: every descriptor slot of one step's extraction
     output through the reference's own vocabulary (small_orb_omni_voc_9_6, k=9, L=6),
@@ -532,6 +670,8 @@ def main():
     ap.add_argument("--d-multiframes", type=int, default=16,
                     help="config D multi-frames per step (8 cams 1024^2, camera per GPU); 0 = off")
     ap.add_argument("--bow-reps", type=int, default=10, help="timed DBoW2 transform launches; 0 = off")
+    ap.add_argument("--tri-reps", type=int, default=20,
+                    help="timed SearchForTriangulationRaw keyframes (5 neighbours each); 0 = off")
     ap.add_argument("--d-unique", type=int, default=2, help="distinct rendered config D multi-frames")
     ap.add_argument("--latency-reps", type=int, default=20,
                     help="single multi-frame extraction latency samples; 0 = off")
@@ -688,6 +828,7 @@ def main():
                                 pin_note(cpus)}
 
     bow, cpu_bow = run_bow(args, rank, world, dev, stream, d_desc, kp_per_step)
+    tri, cpu_tri = run_triangulation(args, rank, world, dev, stream, d_kps, d_cnt, d_desc, cap, NC, U)
     gba, cpu_gba = run_global_ba(args, rank, world, local_rank, dev)
     cfg_d = run_config_d(args, rank, world, local_rank, dev, stream)
 
@@ -695,9 +836,13 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         S = min(args.cpu_sample, U)
-        v, sample, cores, ref = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
+        v, sample, cores, ref, stages = cpu_baseline(uimgs, masks, NC, args.nfeatures, S)
         cpu = {"value": round(v, 3), "unit": "kfeatures/s", "cores": cores, "kind": "port",
-               "sample": sample}
+               "sample": sample,
+               "stage_ms_per_camera_frame": stages,
+               "note": "upper bound on the GPU/CPU ratio: a scalar portable-x86-64 restatement "
+                       "(no -march, no SIMD intrinsics, -ffp-contract=off), not the reference's "
+                       "OpenCV SSE/AVX build"}
         cpu.update(host_cpu_info())
         parity = check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, NC)
 
@@ -731,6 +876,8 @@ def main():
             "config_d": cfg_d,
             "bow": bow,
             "cpu_baseline_bow": cpu_bow,
+            "triangulation": tri,
+            "cpu_baseline_triangulation": cpu_tri,
             "latency": latency,
             "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
             "match_ms_per_step": round(match_ms_last, 4),

@@ -79,6 +79,29 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
                                             double epi_thresh, int32_t* matches12,
                                             int32_t* n_matches);
 
+/* Device-resident SearchForTriangulationRaw for CreateNewMapPoints' neighbour loop
+ * (src/cLocalMapping.cpp:223-266 -> src/cORBmatcher.cpp:968-1156): the same match list as
+ * the two host entries above, on device buffers and stream-ordered (no host synchronisation),
+ * so a caller keeps KF descriptors, rays and has-map-point flags resident and runs one call per
+ * neighbour keyframe, updating d_has_mp1 between calls as the reference's triangulation does.
+ * d_mask1 / d_mask2: both null (ORB, DescriptorDistance64) or both set (mdBRIEF, ...Masked).
+ * d_E [ncams][ncams][9] (mcs_compute_e_rig).  Out: d_matches12[n1] (-1 = none), *d_n_matches.
+ * Keypoints whose camera lies outside [0, ncams) never match (the host entries reject them).
+ * The workspace holds per-query candidate slots; n1 <= max_n1, n2 <= max_n2 < 2^20. */
+typedef struct mcs_tri_workspace mcs_tri_workspace;
+int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs_tri_workspace** out);
+void mcs_tri_workspace_destroy(mcs_tri_workspace* ws);
+int mcs_search_for_triangulation_raw_device(mcs_tri_workspace* ws, const uint8_t* d_desc1,
+                                            const uint8_t* d_mask1, const int32_t* d_cam1,
+                                            const uint8_t* d_has_mp1, const double* d_rays1,
+                                            int32_t n1, const uint8_t* d_desc2,
+                                            const uint8_t* d_mask2, const int32_t* d_cam2,
+                                            const uint8_t* d_has_mp2, const double* d_rays2,
+                                            int32_t n2, int32_t ncams, const double* d_E,
+                                            int32_t bytes, int32_t th_low, double epi_thresh,
+                                            int32_t* d_matches12, int32_t* d_n_matches,
+                                            void* stream);
+
 /* The essential matrices SearchForTriangulationRaw precomputes per camera pair
  * (src/cORBmatcher.cpp:985-998): E[i][j] = ComputeE(KF1.Get_MtMc_inv(i), KF2.Get_MtMc(j))
  * (src/misc.cpp:72-86), the rig poses given as the Cayley 6-vectors the keyframes hold

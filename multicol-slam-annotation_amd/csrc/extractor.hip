@@ -15,6 +15,7 @@
 #include "extractor_plan.hpp"
 #include "extractor_kernels.hpp"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -53,6 +54,7 @@ struct mcs_extractor {
   int32_t* d_sel_count = nullptr;  // [F][nlevels]
   // masks: registered set + single-call slot, each with per-cell window bitmaps
   uint8_t* d_mask_pyr = nullptr; int n_masks = 0;
+  mcs::FastUnit* d_munits = nullptr; int64_t munit_stride = 0;   // per-mask FAST units
   uint8_t* d_mask_single = nullptr;
   // single-frame staging
   uint8_t* d_in = nullptr;
@@ -60,6 +62,8 @@ struct mcs_extractor {
   uint8_t* d_dmask = nullptr;
   // camera models (dBRIEF / mdBRIEF)
   mcs_cam_model* d_cams = nullptr; int n_cams = 0;
+  // side stream for the level-0 blur (overlaps the resize chain; see run_batch)
+  hipStream_t side = nullptr; hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // last call (for read_stage)
   const uint8_t* last_img0 = nullptr;
   int last_frames = 0;
@@ -124,6 +128,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   fa.pyr = h->d_pyr; fa.pyr_fstride = pl.pyr_frame_bytes;
   fa.mask_pyr = mask_pyr; fa.mask_fstride = pl.mask_frame_bytes;
   fa.mask_index = d_mask_index;
+  fa.nmasks = (mask_pyr && mask_pyr == h->d_mask_pyr) ? h->n_masks : 1;
   fa.cells = h->d_cells; fa.ncells = (int)pl.cells.size();
   fa.slots = h->d_slots; fa.slots_fstride = pl.slots_per_frame;
   fa.cell_counts = h->d_cell_counts;
@@ -136,15 +141,37 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   // of every level in one launch.  (FAST per level on a second stream beside the chain was
   // measured slower: 1.85 -> 2.0-2.1 ms per step; the chain then loses its Infinity-Cache
   // reuse of level l-1 and its CU slots.)
+  // The level-0 blur depends on the input only: on the side stream it runs beside the chain
+  // (sharing the chain's level-0 reads while level 1 streams them, and filling the CUs the
+  // small levels 4..7 leave idle); FAST joins both.  MCS_BLUR0_SIDE=0 restores the serial order.
+  static const bool side_blur = [] {
+    const char* e = std::getenv("MCS_BLUR0_SIDE");
+    return !(e && e[0] == '0');
+  }();
+  const bool use_side = side_blur && !h->timing;
+  if (use_side && !h->side) {
+    MCS_HIP_CHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    MCS_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    MCS_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  }
   stage_mark(h, 0, st);
+  if (use_side) {
+    MCS_HIP_CHECK(hipEventRecord(h->ev_fork, st));
+    MCS_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    launch_pyr_blur(pyr_args(0), false, false, h->side);   // blur of level 0 (the input frames)
+    MCS_HIP_CHECK(hipEventRecord(h->ev_join, h->side));
+  }
   for (int l = 1; l < nl; l++) launch_pyr_blur(pyr_args(l), true, wide, st);
   stage_mark(h, 1, st);
-  launch_pyr_blur(pyr_args(0), false, false, st);  // blur of level 0 (the input frames)
+  if (use_side) MCS_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
+  else launch_pyr_blur(pyr_args(0), false, false, st);  // blur of level 0 (the input frames)
   stage_mark(h, 2, st);
   {
     FastRowArgs fl = fa;
-    fl.units = h->d_units;
-    fl.nunits = (int)pl.fast_units.size();
+    const bool per_mask = mask_pyr && mask_pyr == h->d_mask_pyr && h->d_munits;
+    fl.units = per_mask ? h->d_munits : h->d_units;
+    fl.nunits = per_mask ? (int)h->munit_stride : (int)pl.fast_units.size();
+    fl.unit_mstride = per_mask ? h->munit_stride : 0;
     launch_fast_rows(fl, st);
   }
   MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));
@@ -288,10 +315,13 @@ void mcs_extractor_destroy(mcs_extractor* h) {
   (void)hipSetDevice(h->device);
   void* ptrs[] = {h->d_xofs, h->d_alpha, h->d_yofs, h->d_beta, h->d_cells, h->d_units, h->d_pyr, h->d_blur,
                   h->d_slots, h->d_cell_counts, h->d_cand, h->d_cnode, h->d_sel, h->d_sel_count,
-                  h->d_mask_pyr, h->d_mask_single, h->d_in,
+                  h->d_mask_pyr, h->d_munits, h->d_mask_single, h->d_in,
                   h->d_kps, h->d_desc, h->d_count, h->d_dmask, h->d_cams};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (h->side) (void)hipStreamDestroy(h->side);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev) {
     for (int i = 0; i < mcs_extractor::kRing * (MCS_EXTRACTOR_NSTAGES + 1); i++)
       (void)hipEventDestroy(h->ev[i]);
@@ -349,12 +379,35 @@ int mcs_extractor_set_masks_device(mcs_extractor* h, const uint8_t* d_masks, int
   if (!h || n_masks < 0 || (n_masks > 0 && !d_masks)) return MCS_ERR_ARG;
   MCS_HIP_CHECK(hipSetDevice(h->device));
   if (h->d_mask_pyr) { MCS_HIP_CHECK(hipFree(h->d_mask_pyr)); h->d_mask_pyr = nullptr; }
+  if (h->d_munits) { MCS_HIP_CHECK(hipFree(h->d_munits)); h->d_munits = nullptr; }
   h->n_masks = 0;
+  h->munit_stride = 0;
   if (n_masks == 0) return MCS_OK;
-  int rc = dalloc(&h->d_mask_pyr, (size_t)n_masks * h->plan.mask_frame_bytes);
+  const Plan& pl = h->plan;
+  int rc = dalloc(&h->d_mask_pyr, (size_t)n_masks * pl.mask_frame_bytes);
   if (rc) return rc;
-  launch_mask_pyramids(h->plan, d_masks, n_masks, h->d_mask_pyr, (hipStream_t)stream);
+  launch_mask_pyramids(pl, d_masks, n_masks, h->d_mask_pyr, (hipStream_t)stream);
   MCS_HIP_CHECK(hipGetLastError());
+  // FAST units per mask (registration time, once per camera): cells without a mask pixel only
+  // zero their count, and every wave of the batch kernel covers live cells
+  std::vector<uint8_t> hm((size_t)n_masks * pl.mask_frame_bytes);
+  MCS_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  MCS_HIP_CHECK(hipMemcpy(hm.data(), h->d_mask_pyr, hm.size(), hipMemcpyDeviceToHost));
+  std::vector<std::vector<FastUnit>> lists(n_masks);
+  size_t stride = 0;
+  for (int m = 0; m < n_masks; m++) {
+    std::vector<FastUnit> dead;
+    build_masked_units(pl, hm.data() + (size_t)m * pl.mask_frame_bytes, lists[m], dead);
+    lists[m].insert(lists[m].end(), dead.begin(), dead.end());   // heavy units first
+    stride = std::max(stride, lists[m].size());
+  }
+  stride = std::max<size_t>(stride, 1);
+  FastUnit pad{};   // no cells, no rows: the wave exits without a store
+  std::vector<FastUnit> all((size_t)n_masks * stride, pad);
+  for (int m = 0; m < n_masks; m++) std::copy(lists[m].begin(), lists[m].end(), all.begin() + (size_t)m * stride);
+  if ((rc = dalloc(&h->d_munits, all.size())) != MCS_OK) return rc;
+  MCS_HIP_CHECK(hipMemcpy(h->d_munits, all.data(), all.size() * sizeof(FastUnit), hipMemcpyHostToDevice));
+  h->munit_stride = (int64_t)stride;
   h->n_masks = n_masks;
   return MCS_OK;
 }

@@ -70,8 +70,10 @@ struct FastRowArgs {
   const uint8_t* img0; int64_t img0_fstride;
   const uint8_t* pyr; int64_t pyr_fstride;
   const uint8_t* mask_pyr; int64_t mask_fstride;  // mask pyramids (nullable = no mask)
-  const int32_t* mask_index;
+  const int32_t* mask_index; int nmasks;           // index clamped to [0, nmasks)
   const FastUnit* units; int nunits;
+  int64_t unit_mstride;   // per-mask unit lists (build_masked_units): units of mask m at
+                          // units + m * unit_mstride; 0 = one list for every frame
   const CellDesc* cells; int ncells;
   uint32_t* slots; int64_t slots_fstride;
   int32_t* cell_counts;

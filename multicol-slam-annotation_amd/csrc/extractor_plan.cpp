@@ -38,6 +38,51 @@ void linear_tables(int sw, int sh, int dw, int dh, Plan& pl) {
   }
 }
 
+// Cells [c, e) of one cell row as k_fast_rows units: the fewest equal runs whose detection span
+// (+3 px halo each side) fits one wave's lanes 0..62.
+void split_runs(const std::vector<CellDesc>& cells, int c, int e, int level, int wcell,
+                std::vector<FastUnit>& out) {
+  const int n = e - c;
+  auto fits = [&](int a, int b) {
+    const int xa = (cells[a].wx0 - 3) & ~3;
+    return cells[b - 1].wx1 + 3 <= xa + kFastUnitSpan;
+  };
+  for (int runs = 1; runs <= n; runs++) {
+    const int per = (n + runs - 1) / runs;
+    bool ok = true;
+    for (int a = c; a < e && ok; a += per) ok = fits(a, std::min(e, a + per));
+    if (!ok) continue;
+    for (int a = c; a < e; a += per) {
+      const int b = std::min(e, a + per);
+      FastUnit u;
+      u.level = (int16_t)level; u.ncells = (int16_t)(b - a);
+      u.wy0 = cells[a].wy0; u.wy1 = cells[a].wy1;
+      u.ux0 = cells[a].wx0; u.ux1 = cells[b - 1].wx1;
+      u.xa = (int16_t)((u.ux0 - 3) & ~3);
+      u.wcell = (int16_t)wcell;
+      u.cell0 = a;
+      out.push_back(u);
+    }
+    return;
+  }
+}
+
+// Cells [c, e) as count-zeroing units (no rows: the wave writes 0 to each cell's count)
+void zero_runs(const std::vector<CellDesc>& cells, int c, int e, int level, int wcell,
+               std::vector<FastUnit>& out) {
+  for (int a = c; a < e; a += 64) {
+    const int b = std::min(e, a + 64);
+    FastUnit u;
+    u.level = (int16_t)level; u.ncells = (int16_t)(b - a);
+    u.wy0 = u.wy1 = cells[a].wy0;
+    u.ux0 = cells[a].wx0; u.ux1 = cells[b - 1].wx1;
+    u.xa = (int16_t)((u.ux0 - 3) & ~3);
+    u.wcell = (int16_t)wcell;
+    u.cell0 = a;
+    out.push_back(u);
+  }
+}
+
 }  // namespace
 
 int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
@@ -163,32 +208,11 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
     pl.unit_begin[l] = (int32_t)pl.fast_units.size();
     // k_fast_rows work units: every cell row split into the fewest equal runs of cells whose
     // detection span (+3 px halo each side) fits one wave's lanes 0..62
+    L.wcell = wCell;
     for (int c = L.cell_begin; c < L.cell_end;) {
       int e = c;
       while (e < L.cell_end && pl.cells[e].wy0 == pl.cells[c].wy0) e++;
-      const int n = e - c;
-      auto fits = [&](int a, int b) {
-        const int xa = (pl.cells[a].wx0 - 3) & ~3;
-        return pl.cells[b - 1].wx1 + 3 <= xa + kFastUnitSpan;
-      };
-      for (int runs = 1; runs <= n; runs++) {
-        const int per = (n + runs - 1) / runs;
-        bool ok = true;
-        for (int a = c; a < e && ok; a += per) ok = fits(a, std::min(e, a + per));
-        if (!ok) continue;
-        for (int a = c; a < e; a += per) {
-          const int b = std::min(e, a + per);
-          FastUnit u;
-          u.level = (int16_t)l; u.ncells = (int16_t)(b - a);
-          u.wy0 = pl.cells[a].wy0; u.wy1 = pl.cells[a].wy1;
-          u.ux0 = pl.cells[a].wx0; u.ux1 = pl.cells[b - 1].wx1;
-          u.xa = (int16_t)((u.ux0 - 3) & ~3);
-          u.wcell = (int16_t)wCell;
-          u.cell0 = a;
-          pl.fast_units.push_back(u);
-        }
-        break;
-      }
+      split_runs(pl.cells, c, e, l, wCell, pl.fast_units);
       c = e;
     }
     pl.max_cells_level = std::max(pl.max_cells_level, L.cell_end - L.cell_begin);
@@ -225,6 +249,35 @@ int build_plan(const mcs_extractor_params& p, int W, int H, Plan& pl) {
   pl.cand_per_frame = slot;
   pl.sel_per_frame = sel;
   return MCS_OK;
+}
+
+void build_masked_units(const Plan& pl, const uint8_t* mask_pyr, std::vector<FastUnit>& live,
+                        std::vector<FastUnit>& dead) {
+  for (int l = 0; l < pl.nlevels; l++) {
+    const LevelPlan& L = pl.lv[l];
+    const uint8_t* m = mask_pyr + L.mask_off;
+    auto cell_live = [&](const CellDesc& cd) {
+      for (int y = cd.wy0; y < cd.wy1; y++)
+        for (int x = cd.wx0; x < cd.wx1; x++)
+          if (m[(int64_t)y * L.bpitch + x]) return true;
+      return false;
+    };
+    for (int c = L.cell_begin; c < L.cell_end;) {
+      int e = c;
+      while (e < L.cell_end && pl.cells[e].wy0 == pl.cells[c].wy0) e++;
+      int a0 = -1, a1 = -1;
+      for (int k = c; k < e; k++)
+        if (cell_live(pl.cells[k])) { if (a0 < 0) a0 = k; a1 = k + 1; }
+      if (a0 < 0) {
+        zero_runs(pl.cells, c, e, l, L.wcell, dead);
+      } else {
+        zero_runs(pl.cells, c, a0, l, L.wcell, dead);
+        split_runs(pl.cells, a0, a1, l, L.wcell, live);
+        zero_runs(pl.cells, a1, e, l, L.wcell, dead);
+      }
+      c = e;
+    }
+  }
 }
 
 }  // namespace mcs

@@ -58,6 +58,7 @@ struct LevelPlan {
   double hx;                  // (maxX-minX)/nIni (:643)
   int32_t width_rel, height_rel;  // maxX-minX, maxY-minY of the octree domain
   int32_t simd_end;           // first dx computed by the scalar vertical resize form
+  int32_t wcell;              // FAST cell width (every cell but a clamped last one)
   int32_t patch_size_scaled;  // (int)(PATCH_SIZE * scaleFactor^l)  (:959)
   float scale;                // (float)mvScaleFactor[l]  (:1305)
 };
@@ -86,5 +87,13 @@ struct Plan {
 
 // Returns MCS_OK or an error (unsupported geometry / parameters).
 int build_plan(const mcs_extractor_params& p, int W, int H, Plan& plan);
+
+// k_fast_rows units for frames of one registered mask (its host copy of the mask pyramid,
+// plan layout).  A cell whose detection window holds no mask pixel emits nothing (runByPixels-
+// Mask drops every keypoint; NMS never looks across a cell): such cells become `dead` units
+// that only zero the cell's count, and each cell row's live range is re-split into the fewest
+// runs (`live`), so a wave covers live cells only.
+void build_masked_units(const Plan& pl, const uint8_t* mask_pyr, std::vector<FastUnit>& live,
+                        std::vector<FastUnit>& dead);
 
 }  // namespace mcs

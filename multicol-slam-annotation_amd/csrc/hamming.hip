@@ -6,7 +6,9 @@
 //            best/second-best scans             src/cORBmatcher.cpp:67-163, 326-475
 #include "common.hpp"
 #include "../../include/mcs_matcher.h"
+#include "ldlt.hpp"
 #include <algorithm>
+#include <new>
 #include <vector>
 
 namespace mcs {
@@ -385,59 +387,6 @@ __device__ __forceinline__ void load_desc_row(uint32_t (&q)[W], const uint8_t* r
   }
 }
 
-// radius search for SearchForTriangulationRaw: candidates with dist <= th among trains of
-// the same camera without a map point.  pass 0 counts, pass 1 writes (dist<<20 | idx2).
-// MASKED: mdBRIEF descriptor masks (havingMasks), DescriptorDistance64Masked.
-template <int W, bool MASKED>
-__global__ __launch_bounds__(kHamThreads) void k_radius(
-    const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA,
-    const int32_t* __restrict__ camA, const uint8_t* __restrict__ hasA, int na,
-    const uint8_t* __restrict__ B, const uint8_t* __restrict__ MB,
-    const int32_t* __restrict__ camB, const uint8_t* __restrict__ hasB, int nb, int th,
-    int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
-    uint32_t* __restrict__ out) {
-  __shared__ uint4 tile[kHamTile * (W / 4)];
-  __shared__ uint4 mtile[MASKED ? kHamTile * (W / 4) : 1];
-  __shared__ int tcam[kHamTile];
-  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
-  uint32_t q[W], qm[W];
-  int qc = -1;
-  bool active = qi < na && !hasA[qi];
-#pragma unroll
-  for (int w = 0; w < W; w++) { q[w] = 0; qm[w] = 0; }
-  if (qi < na) {
-    qc = camA[qi];
-    load_desc_row<W>(q, A + (int64_t)qi * W * 4);
-    if (MASKED) load_desc_row<W>(qm, MA + (int64_t)qi * W * 4);
-  }
-  int cnt = 0;
-  int pos = (offsets && qi < na) ? offsets[qi] : 0;
-  for (int t0 = 0; t0 < nb; t0 += kHamTile) {
-    const int nt_tile = min(kHamTile, nb - t0);
-    __syncthreads();
-    const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
-    for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
-    if (MASKED) {
-      const uint4* msrc = reinterpret_cast<const uint4*>(MB + (int64_t)t0 * W * 4);
-      for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) mtile[i] = msrc[i];
-    }
-    for (int i = threadIdx.x; i < nt_tile; i += kHamThreads)
-      tcam[i] = hasB[t0 + i] ? -2 : camB[t0 + i];
-    __syncthreads();
-    if (!active) continue;
-    for (int j = 0; j < nt_tile; j++) {
-      if (tcam[j] != qc) continue;
-      const int d = MASKED ? ham_dist_masked_v<W>(q, qm, &tile[j * (W / 4)], &mtile[j * (W / 4)])
-                           : ham_dist_v<W>(q, &tile[j * (W / 4)]);
-      if (d <= th) {
-        if (out) out[pos++] = ((uint32_t)d << 20) | (uint32_t)(t0 + j);
-        cnt++;
-      }
-    }
-  }
-  if (!out && qi < na) counts[qi] = active ? cnt : 0;
-}
-
 static int check_bytes(int bytes) {
   if (bytes != 16 && bytes != 32 && bytes != 64) {
     set_error("descriptor bytes must be 16, 32 or 64");
@@ -540,26 +489,12 @@ int mcs_hamming_top2_batch_device(const uint8_t* d_desc, const int32_t* d_counts
 
 namespace mcs {
 
-template <bool MASKED>
-static void launch_radius(int bytes, dim3 g, const uint8_t* dA, const uint8_t* dmA,
-                          const int32_t* dcA, const uint8_t* dhA, int n1, const uint8_t* dB,
-                          const uint8_t* dmB, const int32_t* dcB, const uint8_t* dhB, int n2,
-                          int th, int32_t* dcnt, const int32_t* doff, uint32_t* dout) {
-  if (bytes == 16)
-    hipLaunchKernelGGL((k_radius<4, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
-                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
-  else if (bytes == 32)
-    hipLaunchKernelGGL((k_radius<8, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
-                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
-  else
-    hipLaunchKernelGGL((k_radius<16, MASKED>), g, dim3(kHamThreads), 0, (hipStream_t)0, dA, dmA,
-                       dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th, dcnt, doff, dout);
-}
-
 // CheckDistEpipolarLine (src/misc.cpp:54-70).  nom = (ray2^T E12) ray1 evaluated left to right
 // as cv::Matx does; (ray2^T E12)_c = sum_r ray2_r E_rc is exactly Etx2_c, so nom = Etx2 . ray1.
-static bool check_dist_epipolar_line(const double* r1, const double* r2, const double* Em,
-                                     double thresh) {
+// One definition for the host entry and the device search (same operation order, no FMA
+// contraction on either side: -ffp-contract=off), so both give the same verdict bit for bit.
+__host__ __device__ __forceinline__ bool epi_check(const double* r1, const double* r2,
+                                                   const double* Em, double thresh) {
   double Ex1[3], Etx2[3];
   for (int r = 0; r < 3; r++) {
     Ex1[r] = Em[3 * r] * r1[0] + Em[3 * r + 1] * r1[1] + Em[3 * r + 2] * r1[2];
@@ -570,6 +505,226 @@ static bool check_dist_epipolar_line(const double* r1, const double* r2, const d
                      Etx2[1] * Etx2[1] + Etx2[2] * Etx2[2];
   if (den == 0.0) return false;
   return (nom * nom) / den < thresh;
+}
+
+// ---- SearchForTriangulationRaw on the device (src/cORBmatcher.cpp:1016-1089)
+// The reference walks KF1's keypoints in index order; for each it sorts the (dist, idx2) list of
+// unmatched same-camera KF2 keypoints with dist <= TH_LOW, takes best = the first list entry,
+// and accepts the first entry with dist <= cvRound(2 best) that passes CheckDistEpipolarLine,
+// marking it in vbMatched2.  With keys (dist << 20 | idx2) the sorted order is key order, so a
+// query's decision is: best = min key among unmatched candidates, winner = min key among
+// unmatched candidates with dist <= 2 best that pass the check.  The only state between
+// queries is vbMatched2, and a query can only be affected by earlier queries that list one of
+// its candidates.  Three stream-ordered kernels:
+//   k_tri_radius  (one thread per query): candidate keys (+ epipolar verdict in bit 30) into a
+//                 fixed kTriCap slot per query, full count, and per-KF2-keypoint reference counts
+//   k_tri_private (one thread per query): a query whose candidates nobody else lists decides
+//                 alone (nothing can be matched before it); the others are marked -2
+//   k_tri_shared  (one wave): the marked queries in index order against an LDS vbMatched2
+//                 bitmap (private winners are never listed by a marked query); a query with more
+//                 than kTriCap candidates rescans KF2 on the fly (exact, rare).
+constexpr int kTriCap = 64;
+constexpr uint32_t kTriPass = 1u << 30, kTriKey = kTriPass - 1;
+
+template <int W, bool MASKED>
+__global__ __launch_bounds__(kHamThreads) void k_tri_radius(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA, const int32_t* __restrict__ camA,
+    const uint8_t* __restrict__ hasA, const double* __restrict__ raysA, int na,
+    const uint8_t* __restrict__ B, const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
+    const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int nb, int ncams,
+    const double* __restrict__ E, int th, double thresh, uint32_t* __restrict__ cand,
+    int32_t* __restrict__ cnt_out, int32_t* __restrict__ ref2) {
+  __shared__ uint4 tile[kHamTile * (W / 4)];
+  __shared__ uint4 mtile[MASKED ? kHamTile * (W / 4) : 1];
+  __shared__ int tcam[kHamTile];
+  const int qi = blockIdx.x * kHamThreads + threadIdx.x;
+  uint32_t q[W], qm[W];
+  double r1[3] = {0, 0, 0}, Em[9];
+  int qc = -1;
+#pragma unroll
+  for (int w = 0; w < W; w++) { q[w] = 0; qm[w] = 0; }
+  if (qi < na) {
+    qc = camA[qi];
+    if (hasA[qi] || qc < 0 || qc >= ncams) qc = -1;   // inactive: no candidates
+  }
+  if (qc >= 0) {
+    load_desc_row<W>(q, A + (int64_t)qi * W * 4);
+    if (MASKED) load_desc_row<W>(qm, MA + (int64_t)qi * W * 4);
+    for (int k = 0; k < 3; k++) r1[k] = raysA[3 * (int64_t)qi + k];
+    // same camera only (:1040-1041): E[cam1][cam2] with cam2 == cam1
+    for (int k = 0; k < 9; k++) Em[k] = E[9 * ((int64_t)qc * ncams + qc) + k];
+  } else {
+    for (int k = 0; k < 9; k++) Em[k] = 0.0;
+  }
+  int cnt = 0;
+  uint32_t* const out = cand + (int64_t)(qi < na ? qi : 0) * kTriCap;
+  for (int t0 = 0; t0 < nb; t0 += kHamTile) {
+    const int nt_tile = min(kHamTile, nb - t0);
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
+    for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
+    if (MASKED) {
+      const uint4* msrc = reinterpret_cast<const uint4*>(MB + (int64_t)t0 * W * 4);
+      for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) mtile[i] = msrc[i];
+    }
+    for (int i = threadIdx.x; i < nt_tile; i += kHamThreads)
+      tcam[i] = hasB[t0 + i] ? -2 : camB[t0 + i];
+    __syncthreads();
+    if (qc < 0) continue;
+    for (int j = 0; j < nt_tile; j++) {
+      if (tcam[j] != qc) continue;
+      const int d = MASKED ? ham_dist_masked_v<W>(q, qm, &tile[j * (W / 4)], &mtile[j * (W / 4)])
+                           : ham_dist_v<W>(q, &tile[j * (W / 4)]);
+      if (d <= th) {
+        const int i2 = t0 + j;
+        if (cnt < kTriCap) {
+          const bool pass = epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh);
+          out[cnt] = ((uint32_t)d << 20) | (uint32_t)i2 | (pass ? kTriPass : 0u);
+        }
+        cnt++;
+        atomicAdd(ref2 + i2, 1);
+      }
+    }
+  }
+  if (qi < na) cnt_out[qi] = cnt;
+}
+
+__global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict__ cand,
+                                                     const int32_t* __restrict__ cnt_in,
+                                                     const int32_t* __restrict__ ref2, int na,
+                                                     int32_t* __restrict__ m12,
+                                                     int32_t* __restrict__ n_matches) {
+  const int qi = blockIdx.x * 256 + threadIdx.x;
+  int won = 0;
+  if (qi < na) {
+    const int c = cnt_in[qi];
+    int r = -1;
+    if (c > kTriCap) {
+      r = -2;
+    } else if (c > 0) {
+      const uint32_t* k = cand + (int64_t)qi * kTriCap;
+      uint32_t best = 0xFFFFFFFFu;
+      bool alone = true;
+      for (int i = 0; i < c; i++) {
+        const uint32_t key = k[i];
+        best = min(best, key & kTriKey);
+        alone = alone && ref2[key & 0xFFFFFu] == 1;
+      }
+      if (!alone) {
+        r = -2;
+      } else {
+        const uint32_t th = 2u * (best >> 20);   // cvRound(2 * bestDist), integer distance
+        uint32_t win = 0xFFFFFFFFu;
+        for (int i = 0; i < c; i++) {
+          const uint32_t key = k[i];
+          if ((key & kTriPass) && ((key & kTriKey) >> 20) <= th) win = min(win, key & kTriKey);
+        }
+        if (win != 0xFFFFFFFFu) { r = (int)(win & 0xFFFFFu); won = 1; }
+      }
+    }
+    m12[qi] = r;
+  }
+  const int s = dev::wave_sum(won);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_matches, s);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+template <int W, bool MASKED>
+__global__ __launch_bounds__(64) void k_tri_shared(
+    const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA, const int32_t* __restrict__ camA,
+    const double* __restrict__ raysA, int na, const uint8_t* __restrict__ B,
+    const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
+    const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int nb, int ncams,
+    const double* __restrict__ E, int th_low, double thresh, const uint32_t* __restrict__ cand,
+    const int32_t* __restrict__ cnt_in, int32_t* __restrict__ m12, int32_t* __restrict__ n_matches) {
+  extern __shared__ uint32_t matched2[];   // vbMatched2 bitmap, nb bits
+  const int lane = threadIdx.x;
+  const int nwords = (nb + 31) >> 5;
+  for (int i = lane; i < nwords; i += 64) matched2[i] = 0u;
+  dev::wave_sync();
+  auto is_matched = [&](uint32_t i2) { return (matched2[i2 >> 5] >> (i2 & 31)) & 1u; };
+  int nm = 0;
+  for (int base = 0; base < na; base += 64) {
+    const int qi = base + lane;
+    const int mine = qi < na ? m12[qi] : -1;
+    const int mycnt = qi < na ? cnt_in[qi] : 0;
+    uint64_t todo = __ballot(mine == -2);
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int q = base + j;
+      const int c = __builtin_amdgcn_readlane(mycnt, j);
+      uint32_t win = 0xFFFFFFFFu;
+      if (c <= kTriCap) {
+        const uint32_t key = lane < c ? cand[(int64_t)q * kTriCap + lane] : 0u;
+        const bool unm = lane < c && !is_matched(key & 0xFFFFFu);
+        const uint32_t best = wave_min_u32(unm ? (key & kTriKey) : 0xFFFFFFFFu);
+        if (best != 0xFFFFFFFFu) {
+          const uint32_t th = 2u * (best >> 20);
+          const bool ok = unm && (key & kTriPass) && ((key & kTriKey) >> 20) <= th;
+          win = wave_min_u32(ok ? (key & kTriKey) : 0xFFFFFFFFu);
+        }
+      } else {
+        // more candidates than the slot holds: rescan KF2 for this query (same filters)
+        const int qc = camA[q];
+        uint32_t qd[W], qmk[W];
+        load_desc_row<W>(qd, A + (int64_t)q * W * 4);
+        if (MASKED) load_desc_row<W>(qmk, MA + (int64_t)q * W * 4);
+        else
+          for (int w = 0; w < W; w++) qmk[w] = 0;
+        auto dist_to = [&](int i2) {
+          uint32_t t[W], tm[W];
+          load_desc_row<W>(t, B + (int64_t)i2 * W * 4);
+          int d = 0;
+          if (MASKED) {
+            load_desc_row<W>(tm, MB + (int64_t)i2 * W * 4);
+            for (int w = 0; w < W; w++) {
+              const uint32_t x = qd[w] ^ t[w];
+              d += __popc(x & qmk[w]) + __popc(x & tm[w]);
+            }
+            d /= 2;
+          } else {
+            for (int w = 0; w < W; w++) d += __popc(qd[w] ^ t[w]);
+          }
+          return d;
+        };
+        uint32_t lbest = 0xFFFFFFFFu;
+        for (int i2 = lane; i2 < nb; i2 += 64) {
+          if (camB[i2] != qc || hasB[i2] || is_matched((uint32_t)i2)) continue;
+          const int d = dist_to(i2);
+          if (d <= th_low) lbest = min(lbest, ((uint32_t)d << 20) | (uint32_t)i2);
+        }
+        const uint32_t best = wave_min_u32(lbest);
+        if (best != 0xFFFFFFFFu) {
+          const int th = 2 * (int)(best >> 20);
+          double r1[3], Em[9];
+          for (int k = 0; k < 3; k++) r1[k] = raysA[3 * (int64_t)q + k];
+          for (int k = 0; k < 9; k++) Em[k] = E[9 * ((int64_t)qc * ncams + qc) + k];
+          uint32_t lw = 0xFFFFFFFFu;
+          for (int i2 = lane; i2 < nb; i2 += 64) {
+            if (camB[i2] != qc || hasB[i2] || is_matched((uint32_t)i2)) continue;
+            const int d = dist_to(i2);
+            if (d <= th_low && d <= th && epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh))
+              lw = min(lw, ((uint32_t)d << 20) | (uint32_t)i2);
+          }
+          win = wave_min_u32(lw);
+        }
+      }
+      const int r = win != 0xFFFFFFFFu ? (int)(win & 0xFFFFFu) : -1;
+      if (lane == 0) {
+        m12[q] = r;
+        if (r >= 0) matched2[r >> 5] |= 1u << (r & 31);
+      }
+      dev::wave_sync();
+      nm += r >= 0;
+    }
+  }
+  if (lane == 0 && nm) atomicAdd(n_matches, nm);
 }
 
 // ---- ComputeE per camera pair (src/misc.cpp:72-86) as SearchForTriangulationRaw builds its
@@ -644,6 +799,44 @@ static void host_compute_e(const double* T1, const double* T2, double* E) {  // 
   host_matmul(S, R12, E, 3, 3, 3);        // t12x * R12
 }
 
+// Device pipeline on device buffers (stream-ordered; no host synchronisation).
+static hipError_t tri_run(const uint8_t* dA, const uint8_t* dmA, const int32_t* dcA, const uint8_t* dhA,
+                          const double* drA, int n1, const uint8_t* dB, const uint8_t* dmB,
+                          const int32_t* dcB, const uint8_t* dhB, const double* drB, int n2, int ncams,
+                          const double* dE, int bytes, int th_low, double thresh, uint32_t* cand,
+                          int32_t* cnt, int32_t* ref2, int32_t* m12, int32_t* nmatch, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(nmatch, 0, sizeof(int32_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(ref2, 0, sizeof(int32_t) * (size_t)n2, st);
+  if (e != hipSuccess) return e;
+  const bool masked = dmA != nullptr;
+  const dim3 g((n1 + kHamThreads - 1) / kHamThreads);
+#define MCS_TRI_RADIUS(WW, MM)                                                                   \
+  hipLaunchKernelGGL((k_tri_radius<WW, MM>), g, dim3(kHamThreads), 0, st, dA, dmA, dcA, dhA, drA, \
+                     n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, cand, cnt, ref2)
+  if (bytes == 16) { if (masked) MCS_TRI_RADIUS(4, true); else MCS_TRI_RADIUS(4, false); }
+  else if (bytes == 32) { if (masked) MCS_TRI_RADIUS(8, true); else MCS_TRI_RADIUS(8, false); }
+  else { if (masked) MCS_TRI_RADIUS(16, true); else MCS_TRI_RADIUS(16, false); }
+#undef MCS_TRI_RADIUS
+  hipLaunchKernelGGL(k_tri_private, dim3((n1 + 255) / 256), dim3(256), 0, st, cand, cnt, ref2, n1, m12,
+                     nmatch);
+  const int lds = ((n2 + 31) / 32) * 4;
+  const void* fn = nullptr;
+#define MCS_TRI_SHARED_FN(WW, MM) fn = (const void*)&k_tri_shared<WW, MM>
+  if (bytes == 16) { if (masked) MCS_TRI_SHARED_FN(4, true); else MCS_TRI_SHARED_FN(4, false); }
+  else if (bytes == 32) { if (masked) MCS_TRI_SHARED_FN(8, true); else MCS_TRI_SHARED_FN(8, false); }
+  else { if (masked) MCS_TRI_SHARED_FN(16, true); else MCS_TRI_SHARED_FN(16, false); }
+#undef MCS_TRI_SHARED_FN
+  if (lds > 64 * 1024 && (e = ldlt::set_lds_limit(fn, lds)) != hipSuccess) return e;
+#define MCS_TRI_SHARED(WW, MM)                                                                    \
+  hipLaunchKernelGGL((k_tri_shared<WW, MM>), dim3(1), dim3(64), lds, st, dA, dmA, dcA, drA, n1, dB, \
+                     dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, cand, cnt, m12, nmatch)
+  if (bytes == 16) { if (masked) MCS_TRI_SHARED(4, true); else MCS_TRI_SHARED(4, false); }
+  else if (bytes == 32) { if (masked) MCS_TRI_SHARED(8, true); else MCS_TRI_SHARED(8, false); }
+  else { if (masked) MCS_TRI_SHARED(16, true); else MCS_TRI_SHARED(16, false); }
+#undef MCS_TRI_SHARED
+  return hipGetLastError();
+}
+
 static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
                                     const int32_t* cam1, const uint8_t* has_mp1,
                                     const double* rays1, int32_t n1, const uint8_t* desc2,
@@ -673,13 +866,13 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
     set_error("no HIP device visible (no CPU fallback)");
     return MCS_ERR_NO_DEVICE;
   }
-  // ---- GPU: per-query candidate lists (same camera, no map point, dist <= th_low)
+  // host entry: upload, run the device search, download (one synchronisation)
   uint8_t *dA = nullptr, *dB = nullptr, *dmA = nullptr, *dmB = nullptr, *dhA = nullptr,
           *dhB = nullptr;
-  int32_t *dcA = nullptr, *dcB = nullptr, *dcnt = nullptr, *doff = nullptr;
-  uint32_t* dout = nullptr;
-  std::vector<int32_t> cnt(n1), off(n1 + 1, 0);
-  std::vector<uint32_t> cand;
+  int32_t *dcA = nullptr, *dcB = nullptr, *dcnt = nullptr, *dref = nullptr, *dm12 = nullptr,
+          *dn = nullptr;
+  double *drA = nullptr, *drB = nullptr, *dE = nullptr;
+  uint32_t* dcand = nullptr;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
   chk(hipMalloc((void**)&dA, (size_t)n1 * bytes));
@@ -694,71 +887,37 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   chk(hipMalloc((void**)&dhB, n2));
   chk(hipMalloc((void**)&dcA, 4 * (size_t)n1));
   chk(hipMalloc((void**)&dcB, 4 * (size_t)n2));
+  chk(hipMalloc((void**)&drA, 24 * (size_t)n1));
+  chk(hipMalloc((void**)&drB, 24 * (size_t)n2));
+  chk(hipMalloc((void**)&dE, 72 * (size_t)ncams * ncams));
+  chk(hipMalloc((void**)&dcand, 4 * (size_t)n1 * kTriCap));
   chk(hipMalloc((void**)&dcnt, 4 * (size_t)n1));
-  chk(hipMalloc((void**)&doff, 4 * (size_t)n1));
+  chk(hipMalloc((void**)&dref, 4 * (size_t)n2));
+  chk(hipMalloc((void**)&dm12, 4 * (size_t)n1));
+  chk(hipMalloc((void**)&dn, 4));
   chk(hipMemcpy(dA, desc1, (size_t)n1 * bytes, hipMemcpyHostToDevice));
   chk(hipMemcpy(dB, desc2, (size_t)n2 * bytes, hipMemcpyHostToDevice));
   chk(hipMemcpy(dhA, has_mp1, n1, hipMemcpyHostToDevice));
   chk(hipMemcpy(dhB, has_mp2, n2, hipMemcpyHostToDevice));
   chk(hipMemcpy(dcA, cam1, 4 * (size_t)n1, hipMemcpyHostToDevice));
   chk(hipMemcpy(dcB, cam2, 4 * (size_t)n2, hipMemcpyHostToDevice));
-  dim3 g((n1 + kHamThreads - 1) / kHamThreads);
-  auto launch = [&](const int32_t* o, uint32_t* out) {
-    if (masked)
-      launch_radius<true>(bytes, g, dA, dmA, dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th_low, dcnt, o, out);
-    else
-      launch_radius<false>(bytes, g, dA, dmA, dcA, dhA, n1, dB, dmB, dcB, dhB, n2, th_low, dcnt, o, out);
-    chk(hipGetLastError());
-  };
-  if (e == hipSuccess) {
-    launch(nullptr, nullptr);
-    chk(hipMemcpy(cnt.data(), dcnt, 4 * (size_t)n1, hipMemcpyDeviceToHost));
-  }
-  if (e == hipSuccess) {
-    for (int i = 0; i < n1; i++) off[i + 1] = off[i] + cnt[i];
-    cand.resize(std::max(1, off[n1]));
-    chk(hipMalloc((void**)&dout, 4 * cand.size()));
-    chk(hipMemcpy(doff, off.data(), 4 * (size_t)n1, hipMemcpyHostToDevice));
-    if (e == hipSuccess) {
-      launch(doff, dout);
-      chk(hipMemcpy(cand.data(), dout, 4 * (size_t)off[n1], hipMemcpyDeviceToHost));
-    }
-  }
-  void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, dcnt, doff, dout};
+  chk(hipMemcpy(drA, rays1, 24 * (size_t)n1, hipMemcpyHostToDevice));
+  chk(hipMemcpy(drB, rays2, 24 * (size_t)n2, hipMemcpyHostToDevice));
+  chk(hipMemcpy(dE, E, 72 * (size_t)ncams * ncams, hipMemcpyHostToDevice));
+  if (e == hipSuccess)
+    e = tri_run(dA, dmA, dcA, dhA, drA, n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, bytes, th_low,
+                epi_thresh, dcand, dcnt, dref, dm12, dn, nullptr);
+  chk(hipMemcpy(matches12, dm12, 4 * (size_t)n1, hipMemcpyDeviceToHost));
+  chk(hipMemcpy(n_matches, dn, 4, hipMemcpyDeviceToHost));
+  void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, drA, drB, dE, dcand, dcnt, dref, dm12, dn};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  if (e != hipSuccess) { set_hip_error(e, "triangulation radius search", __FILE__, __LINE__); return MCS_ERR_HIP; }
-
-  // ---- host: the order-dependent greedy of :1016-1089 (vbMatched2 state)
-  std::vector<uint8_t> matched2(n2, 0);
-  int nm = 0;
-  for (int i1 = 0; i1 < n1; i1++) {
-    if (has_mp1[i1]) continue;
-    uint32_t* c = cand.data() + off[i1];
-    const int nc = off[i1 + 1] - off[i1];
-    if (nc == 0) continue;
-    std::sort(c, c + nc);  // (dist, idx2) ascending == sort(vDistIndex)
-    int best = -1;
-    for (int k = 0; k < nc; k++)
-      if (!matched2[c[k] & 0xFFFFF]) { best = (int)(c[k] >> 20); break; }
-    if (best < 0) continue;
-    const int th = (int)std::lrint(2.0 * best);
-    const int c1 = cam1[i1];
-    const double* r1 = rays1 + 3 * (size_t)i1;
-    for (int k = 0; k < nc; k++) {
-      const int d = (int)(c[k] >> 20), i2 = (int)(c[k] & 0xFFFFF);
-      if (matched2[i2]) continue;
-      if (d > th) break;
-      const double* Em = E + 9 * ((size_t)c1 * ncams + cam2[i2]);
-      if (check_dist_epipolar_line(r1, rays2 + 3 * (size_t)i2, Em, epi_thresh)) {
-        matched2[i2] = 1;
-        matches12[i1] = i2;
-        nm++;
-        break;
-      }
-    }
+  if (e != hipSuccess) {
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    *n_matches = 0;
+    set_hip_error(e, "triangulation search", __FILE__, __LINE__);
+    return MCS_ERR_HIP;
   }
-  *n_matches = nm;
   return MCS_OK;
 }
 
@@ -793,6 +952,81 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
                                   matches12, n_matches);
 }
 
+struct mcs_tri_workspace {
+  int device = 0, max_n1 = 0, max_n2 = 0;
+  uint32_t* cand = nullptr;   // [max_n1][kTriCap]
+  int32_t* cnt = nullptr;     // [max_n1]
+  int32_t* ref2 = nullptr;    // [max_n2]
+};
+
+int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs_tri_workspace** out) {
+  if (!out || max_n1 < 1 || max_n2 < 1 || max_n2 >= (1 << 20)) {
+    set_error("tri workspace: need max_n1 >= 1 and 1 <= max_n2 < 2^20");
+    return MCS_ERR_ARG;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { set_error("no HIP device visible (no CPU fallback)"); return MCS_ERR_NO_DEVICE; }
+  if (device < 0 || device >= ndev) { set_error("bad device ordinal"); return MCS_ERR_ARG; }
+  MCS_HIP_CHECK(hipSetDevice(device));
+  auto* w = new (std::nothrow) mcs_tri_workspace();
+  if (!w) return MCS_ERR_ARG;
+  w->device = device; w->max_n1 = max_n1; w->max_n2 = max_n2;
+  hipError_t e = hipMalloc((void**)&w->cand, 4 * (size_t)max_n1 * kTriCap);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, 4 * (size_t)max_n1);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->ref2, 4 * (size_t)max_n2);
+  if (e != hipSuccess) {
+    mcs_tri_workspace_destroy(w);
+    set_hip_error(e, "tri workspace", __FILE__, __LINE__);
+    return MCS_ERR_HIP;
+  }
+  *out = w;
+  return MCS_OK;
+}
+
+void mcs_tri_workspace_destroy(mcs_tri_workspace* w) {
+  if (!w) return;
+  (void)hipSetDevice(w->device);
+  if (w->cand) (void)hipFree(w->cand);
+  if (w->cnt) (void)hipFree(w->cnt);
+  if (w->ref2) (void)hipFree(w->ref2);
+  delete w;
+}
+
+int mcs_search_for_triangulation_raw_device(mcs_tri_workspace* ws, const uint8_t* d_desc1,
+                                            const uint8_t* d_mask1, const int32_t* d_cam1,
+                                            const uint8_t* d_has_mp1, const double* d_rays1,
+                                            int32_t n1, const uint8_t* d_desc2,
+                                            const uint8_t* d_mask2, const int32_t* d_cam2,
+                                            const uint8_t* d_has_mp2, const double* d_rays2,
+                                            int32_t n2, int32_t ncams, const double* d_E,
+                                            int32_t bytes, int32_t th_low, double epi_thresh,
+                                            int32_t* d_matches12, int32_t* d_n_matches,
+                                            void* stream) {
+  int rc = check_bytes(bytes);
+  if (rc) return rc;
+  if (!ws || !d_n_matches || n1 < 0 || n2 < 0 || ncams <= 0) { set_error("triangulation: bad arguments"); return MCS_ERR_ARG; }
+  if (n1 > ws->max_n1 || n2 > ws->max_n2) { set_error("triangulation: n1 / n2 above the workspace capacity"); return MCS_ERR_CAPACITY; }
+  if ((d_mask1 != nullptr) != (d_mask2 != nullptr)) { set_error("triangulation: masks for both keyframes or none"); return MCS_ERR_ARG; }
+  MCS_HIP_CHECK(hipSetDevice(ws->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (n1 == 0 || n2 == 0) {
+    if (n1 > 0) MCS_HIP_CHECK(hipMemsetAsync(d_matches12, 0xFF, 4 * (size_t)n1, st));   // -1
+    MCS_HIP_CHECK(hipMemsetAsync(d_n_matches, 0, 4, st));
+    return MCS_OK;
+  }
+  if (!d_desc1 || !d_desc2 || !d_cam1 || !d_cam2 || !d_has_mp1 || !d_has_mp2 || !d_rays1 ||
+      !d_rays2 || !d_E || !d_matches12) {
+    set_error("triangulation: null device buffer");
+    return MCS_ERR_ARG;
+  }
+  const hipError_t e = tri_run(d_desc1, d_mask1, d_cam1, d_has_mp1, d_rays1, n1, d_desc2, d_mask2, d_cam2,
+                               d_has_mp2, d_rays2, n2, ncams, d_E, bytes, th_low, epi_thresh, ws->cand,
+                               ws->cnt, ws->ref2, d_matches12, d_n_matches, st);
+  if (e != hipSuccess) { set_hip_error(e, "triangulation search", __FILE__, __LINE__); return MCS_ERR_HIP; }
+  return MCS_OK;
+}
+
 int mcs_compute_e_rig(const double* mt1, const double* mt2, const double* mc, int32_t ncams,
                       double* E) {
   if (!mt1 || !mt2 || !mc || !E || ncams <= 0) { set_error("compute_e_rig: bad arguments"); return MCS_ERR_ARG; }
@@ -815,7 +1049,7 @@ int mcs_compute_e_rig(const double* mt1, const double* mt2, const double* mc, in
 int mcs_check_dist_epipolar_line(const double* ray1, const double* ray2, const double* E12,
                                  double thresh) {
   if (!ray1 || !ray2 || !E12) { set_error("check_dist_epipolar_line: null argument"); return MCS_ERR_ARG; }
-  return check_dist_epipolar_line(ray1, ray2, E12, thresh) ? 1 : 0;
+  return epi_check(ray1, ray2, E12, thresh) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -133,7 +133,8 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   if (!xcd_frame_map(blockIdx.x, a.nframes, (a.nunits + 3) / 4, &f, &item)) return;
   const int ui = item * 4 + wv;
   if (ui >= a.nunits) return;
-  const FastUnit u = a.units[ui];
+  const int mi = a.mask_index ? min(max(a.mask_index[f], 0), a.nmasks - 1) : 0;
+  const FastUnit u = a.units[(int64_t)mi * a.unit_mstride + ui];
 #ifdef MCS_FAST_PROBE
   unsigned long long acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long long t_begin_ = __builtin_amdgcn_s_memtime();
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   }
   // mask rows of the run (the level of the frame's mask pyramid, pitch bpitch: aligned dwords)
   const uint8_t* const mrow0 =
-      a.mask_pyr ? a.mask_pyr + (int64_t)(a.mask_index ? a.mask_index[f] : 0) * a.mask_fstride +
+      a.mask_pyr ? a.mask_pyr + (int64_t)mi * a.mask_fstride +
                        a.lp.mask_off[level] + (int64_t)(u.wy0 - 3) * a.lp.bpitch[level] + u.xa
                  : nullptr;
   const int mpitch = a.lp.bpitch[level];

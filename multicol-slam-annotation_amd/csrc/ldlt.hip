@@ -861,6 +861,22 @@ __device__ __forceinline__ void load_acc(double (&a)[4][4], const double* Aij) {
     for (int r = 0; r < 4; r++) a[q][r] = Aij[(16 * q + k4 + 4 * r) * TB + col];
 }
 
+// the 10 lower and 6 strict-upper 16x16 blocks of a diagonal tile
+__constant__ int kLowBi[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+__constant__ int kLowBj[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+__constant__ int kUpBi[6] = {0, 0, 0, 1, 1, 2};
+__constant__ int kUpBj[6] = {1, 2, 3, 2, 3, 3};
+// one lane's four accumulator-layout values of block (bi, bj) into the LDS tile, the strict
+// upper part of a diagonal block as 0
+__device__ __forceinline__ void a3_store(double* sK, const double (&v)[4], int bi, int bj) {
+  const int l = threadIdx.x & 63, r16 = l & 15, k4 = l >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = 16 * bi + k4 + 4 * r, col = 16 * bj + r16;
+    sK[row * LS + col] = (col > row) ? 0.0 : v[r];
+  }
+}
+
 __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) {
   double* sK = sm;
   double* sI = sK + TB * LS;
@@ -880,29 +896,49 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     // workgroup formed at step k-1 (still in sX / sY, u_{k-1} in su)
     if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok)) break;
     DSTAMP(k, 1);
-    double a[4][4];
-    load_acc(a, g.A + toff(k, k, T));
+    // A_kk -= L_{k,k-1} W_{k,k-1}^T on the 10 lower 16x16 blocks only (the upper ones are
+    // not read by the factorisation), 3 / 3 / 2 / 2 blocks per wave; each block is the same
+    // MFMA chain (k ascending) as the full gemm_xyt, so the bits are the full product's
     double bv = g.b[k * TB + (t >> 2)];
-    if (k >= 1) {
-      d4 p[4];
-      gemm_xyt(sX, sY, p);
+    {
+      const double* Akk = g.A + toff(k, k, T);
+      const int nb = w < 2 ? 3 : 2, b0 = w < 2 ? 3 * w : 6 + 2 * (w - 2);
+      double a[3][4];
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+      for (int q = 0; q < 3; q++) {
+        if (q < nb) {
+          const int bi = kLowBi[b0 + q], bj = kLowBj[b0 + q];
 #pragma unroll
-        for (int r = 0; r < 4; r++) a[q][r] = a[q][r] - p[q][r];
-      bv -= gemv_row(sX, su);
+          for (int r = 0; r < 4; r++) a[q][r] = Akk[(16 * bi + k4 + 4 * r) * TB + 16 * bj + r16];
+        }
+      }
+      if (k >= 1) bv -= gemv_row(sX, su);
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        if (q < nb) {
+          const int bi = kLowBi[b0 + q], bj = kLowBj[b0 + q];
+          if (k >= 1) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k0 = 0; k0 < TB; k0 += 4)
+              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sX[(16 * bi + r16) * LS + k0 + k4],
+                                                          sY[(16 * bj + r16) * LS + k0 + k4], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; r++) a[q][r] = a[q][r] - acc[r];
+          }
+          a3_store(sK, a[q], bi, bj);
+        }
+      }
+      // the strict upper blocks are zero (the factorisation reads the lower triangle only, but
+      // put_tile_lower's convention keeps the upper part defined)
+      const int nz = w < 2 ? 2 : 1, z0 = w < 2 ? 2 * w : 4 + (w - 2);
+      for (int q = 0; q < nz; q++) {
+        const int bi = kUpBi[z0 + q], bj = kUpBj[z0 + q];
+#pragma unroll
+        for (int r = 0; r < 4; r++) sK[(16 * bi + k4 + 4 * r) * LS + 16 * bj + r16] = 0.0;
+      }
     }
     __syncthreads();
-    {
-      const int col = 16 * w + r16;
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = 16 * q + k4 + 4 * r;
-          sK[row * LS + col] = (col > row) ? 0.0 : a[q][r];
-        }
-    }
     if ((t & 3) == 0) sv[t >> 2] = bv;
     if (t == 0) *fail = 0;
     __syncthreads();

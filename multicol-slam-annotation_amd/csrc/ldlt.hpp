@@ -71,6 +71,9 @@ hipError_t pad(double* A, double* b, int n, int T, double diag_value, hipStream_
                const int* skip = nullptr);
 // pad + solve of a one-tile system (n <= 64) in one launch, bitwise equal to pad + solve
 // (diag_value: the padding diagonal after any exchange, i.e. 1)
+// dynamic-LDS limit of a kernel above 64 KB, once per (kernel, device)
+hipError_t set_lds_limit(const void* fn, int bytes);
+
 hipError_t solve_one_tile(const double* A, const double* b, double* x, int n, double diag_value, int* flag,
                           hipStream_t st, const int* skip = nullptr);
 

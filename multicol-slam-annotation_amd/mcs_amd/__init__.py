@@ -140,6 +140,9 @@ SIGNATURES = {
     "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
     "mcs_search_for_triangulation_raw_masked": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
     "mcs_compute_e_rig": (ctypes.c_int, [_P, _P, _P, _I32, _P]),
+    "mcs_tri_workspace_create": (ctypes.c_int, [_I32, _I32, _I32, _P]),
+    "mcs_tri_workspace_destroy": (None, [_P]),
+    "mcs_search_for_triangulation_raw_device": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P, _P]),
     "mcs_check_dist_epipolar_line": (ctypes.c_int, [_P, _P, _P, ctypes.c_double]),
     "mcs_frame_grid_build": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P, _P]),
     "mcs_window_search_device": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P]),

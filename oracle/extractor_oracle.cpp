@@ -26,6 +26,8 @@
 // created == "higher address"), identically in oracle and GPU path.
 // Build: g++ -O2 -ffp-contract=off -fPIC -shared (see __graft_entry__.build()).
 // ============================================================================
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -825,6 +827,24 @@ float oracle_ic_angle(const uint8_t* img, int w, int h, int cx, int cy, int* m01
   return ic_angle(im, cx, cy, umax, m01, m10);
 }
 
+// Per-stage time of oracle_extract_ex2, summed over calling threads (bench.py's cpu_baseline
+// reports it per camera-frame): [0] pyramid, [1] FAST + NMS + mask, [2] octree, [3] IC angle,
+// [4] blur + descriptor.  Nanoseconds, steady clock.
+static std::atomic<long long> g_stage_ns[5];
+struct StageClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(int k) {
+    const auto n = std::chrono::steady_clock::now();
+    g_stage_ns[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count();
+    t = n;
+  }
+};
+
+int oracle_stage_ns(long long* out5, int reset) {
+  for (int k = 0; k < 5; k++) out5[k] = reset ? g_stage_ns[k].exchange(0) : g_stage_ns[k].load();
+  return 0;
+}
+
 // Full extractor: mdBRIEFextractorOct::operator() (:1244-1337).  ORB when cam == nullptr
 // (do_dbrief = learn_masks = 0); dBRIEF / mdBRIEF otherwise.  kps/desc/desc_masks
 // caller-allocated (cap keypoints; desc_masks nullable).  Returns 0, or -1 if cap too small.
@@ -840,6 +860,7 @@ int oracle_extract_ex2(const uint8_t* image, int W, int H, const uint8_t* mask, 
   auto nPerLevel = features_per_level(p);
   auto umax = make_umax();
   if ((do_dbrief || learn_masks) && !cam) return -2;
+  StageClock clk;
   // ComputePyramid (:1158-1201)
   std::vector<Img> pyr(nlevels), mpyr(nlevels);
   pyr[0].create(W, H); std::memcpy(pyr[0].d.data(), image, (size_t)W * H);
@@ -848,15 +869,18 @@ int oracle_extract_ex2(const uint8_t* image, int W, int H, const uint8_t* mask, 
     resize_linear(pyr[l - 1], pyr[l], lv[l].w, lv[l].h, vresize_mode);
     if (mask) resize_nearest(mpyr[l - 1], mpyr[l], lv[l].w, lv[l].h);
   }
+  clk.lap(0);
   // ComputeKeyPointsOctTree (:863-976)
   std::vector<std::vector<KP>> all(nlevels);
   const int minBorder = EDGE_THRESHOLD - 3;
   for (int l = 0; l < nlevels; l++) {
     std::vector<KP> cands;
     level_candidates(pyr[l], mask ? &mpyr[l] : nullptr, fast_threshold, cands, fast_type);
+    clk.lap(1);
     all[l] = distribute_octree(cands, minBorder, pyr[l].w - EDGE_THRESHOLD + 3, minBorder,
                                pyr[l].h - EDGE_THRESHOLD + 3, nPerLevel[l]);
     for (auto& k : all[l]) { k.x += minBorder; k.y += minBorder; }
+    clk.lap(2);
   }
   int total = 0;
   for (int l = 0; l < nlevels; l++) total += (int)all[l].size();
@@ -869,6 +893,7 @@ int oracle_extract_ex2(const uint8_t* image, int W, int H, const uint8_t* mask, 
     std::vector<float> ang(all[l].size());
     for (size_t i = 0; i < all[l].size(); i++)
       ang[i] = ic_angle(pyr[l], cvRoundf(all[l][i].x), cvRoundf(all[l][i].y), umax);
+    clk.lap(3);
     if (all[l].empty()) continue;
     Img blurred;
     box_blur5(pyr[l], blurred);
@@ -898,6 +923,7 @@ int oracle_extract_ex2(const uint8_t* image, int W, int H, const uint8_t* mask, 
       o.octave = l; o.class_id = -1;
     }
     off += (int)all[l].size();
+    clk.lap(4);
   }
   return 0;
 }

@@ -35,6 +35,7 @@ _SIGS = {
     "oracle_extract": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _P, _P, _I, _P]),
     "oracle_extract_ex": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P]),
     "oracle_extract_ex2": (_I, [_P, _I, _I, _P, _I, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _I]),
+    "oracle_stage_ns": (_I, [_P, _I]),
     "oracle_cam_world_to_img": (_I, [_P, _D, _D, _D, _P]),
     "oracle_cam_img_to_world": (_I, [_P, _D, _D, _P]),
     # matcher oracle
@@ -406,3 +407,11 @@ def vocab_transform(voc, feats, levelsup=4):
     bow = {int(bw[i]): float(bv[i]) for i in range(int(bn[0]))}
     fv = {int(fn[j]): ff[fp[j]:fp[j + 1]].tolist() for j in range(int(fvn[0]))}
     return bow, fv
+
+
+def stage_ns(reset=True):
+    """Per-stage time of the oracle extractor summed over threads since the last reset (ns):
+    pyramid, FAST, octree, IC angle, blur + descriptor."""
+    out = np.zeros(5, np.int64)
+    lib().oracle_stage_ns(_p(out), 1 if reset else 0)
+    return out

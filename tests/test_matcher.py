@@ -59,8 +59,10 @@ def _oracle_top2(q, t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nq,nt,nbytes", [(1000, 1300, 32), (257, 5, 16), (600, 700, 64), (1, 1, 32)])
+@pytest.mark.parametrize("nq,nt,nbytes", [(1000, 1300, 32), (257, 5, 16), (600, 700, 64), (1, 1, 32),
+                                          (400, 8193, 32), (300, 20000, 32)])
 def test_top2_device(gpu, nq, nt, nbytes):
+    """nt > 8192 takes k_top2_mfma32<false> (train index beyond the 13-bit packed key)."""
     import torch
     import mcs_amd
     L = mcs_amd.lib()
@@ -269,3 +271,111 @@ def test_config_b_size_matching(gpu):
         _p(d2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), n, 3,
         _p(np.ascontiguousarray(E)), 32, 64, 0.3, _p(got), ctypes.byref(nm))
     assert rc == 0 and nm.value == nref and np.array_equal(got, ref) and nref > 100
+
+
+def _tri_problem_shared(seed, n1=900, n2=1000, ncams=2, nbytes=32):
+    """Queries that compete for the same KF2 keypoints (the order-dependent vbMatched2 greedy):
+    KF1 and KF2 hold noisy copies of a few base descriptors, and queries 0..3 have more
+    candidates than the device keeps per query (the rescan path)."""
+    rng = np.random.default_rng(seed)
+    bases = _descs(12, nbytes, seed + 100)
+    d1 = _descs(n1, nbytes, seed)
+    d2 = _descs(n2, nbytes, seed + 1)
+    pick1 = rng.integers(0, 12, 400)
+    d1[:400] = _noisy_copy(bases[pick1], rng.integers(0, 14, 400), seed + 2)
+    pick2 = rng.integers(0, 12, 500)
+    d2[:500] = _noisy_copy(bases[pick2], rng.integers(0, 14, 500), seed + 3)
+    d1[:4] = bases[0]
+    d2[500:650] = _noisy_copy(np.repeat(bases[:1], 150, 0), rng.integers(0, 10, 150), seed + 4)
+    cam1 = rng.integers(0, ncams, n1).astype(np.int32)
+    cam2 = rng.integers(0, ncams, n2).astype(np.int32)
+    cam1[:4] = 0
+    cam2[500:650] = 0
+    has1 = (rng.random(n1) < 0.05).astype(np.uint8)
+    has1[:4] = 0
+    has2 = (rng.random(n2) < 0.05).astype(np.uint8)
+    r1 = rng.normal(size=(n1, 3))
+    r1 /= np.linalg.norm(r1, axis=1, keepdims=True)
+    r2 = rng.normal(size=(n2, 3))
+    r2 /= np.linalg.norm(r2, axis=1, keepdims=True)
+    E = rng.normal(size=(ncams, ncams, 3, 3))
+    return d1, d2, cam1, cam2, has1, has2, r1, r2, E
+
+
+def _run_tri_device(ws, d1, d2, cam1, cam2, has1, has2, r1, r2, E, nbytes, th, thresh, m1=None, m2=None):
+    import torch
+    import mcs_amd
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    bufs = [dev(x) for x in (d1, cam1, has1, r1, d2, cam2, has2, r2, E)]
+    mb = [dev(m) for m in (m1, m2)] if m1 is not None else [None, None]
+    out = torch.full((len(d1),), -9, dtype=torch.int32, device="cuda")
+    n = torch.full((1,), -9, dtype=torch.int32, device="cuda")
+    ptr = lambda t: None if t is None else t.data_ptr()
+    rc = mcs_amd.lib().mcs_search_for_triangulation_raw_device(
+        ws, ptr(bufs[0]), ptr(mb[0]), ptr(bufs[1]), ptr(bufs[2]), ptr(bufs[3]), len(d1),
+        ptr(bufs[4]), ptr(mb[1]), ptr(bufs[5]), ptr(bufs[6]), ptr(bufs[7]), len(d2), E.shape[0],
+        ptr(bufs[8]), nbytes, th, thresh, out.data_ptr(), n.data_ptr(),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    return int(n.item()), out.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,masked", [(0, False), (1, False), (2, True)])
+def test_triangulation_device_shared_candidates(gpu, seed, masked):
+    """The device-resident entry on queries that compete for KF2 keypoints (the vbMatched2
+    greedy order matters) and on queries with more candidates than a slot holds, vs the oracle;
+    the host entry on the same input agrees too."""
+    import mcs_amd
+    nbytes = 32
+    d1, d2, cam1, cam2, has1, has2, r1, r2, E = _tri_problem_shared(seed)
+    m1 = _masks(len(d1), nbytes, seed + 10, keep=0.9) if masked else None
+    m2 = _masks(len(d2), nbytes, seed + 11, keep=0.9) if masked else None
+    th = nbytes if masked else 2 * nbytes
+    thresh = 0.3
+    nref, ref = _oracle_tri(d1, d2, cam1, cam2, has1, has2, r1, r2, E, thresh, m1, m2)
+    assert nref > 50
+    # the problem really exercises both device paths: shared candidates and slot overflow
+    dist = np.unpackbits(d1[:4, None, :] ^ d2[None, :, :], axis=2).sum(2)
+    assert int(((dist <= th) & (cam2[None, :] == 0) & (has2[None, :] == 0)).sum(1).max()) > 64
+    L = mcs_amd.lib()
+    ws = ctypes.c_void_p()
+    assert L.mcs_tri_workspace_create(0, len(d1), len(d2), ctypes.byref(ws)) == 0
+    try:
+        n, got = _run_tri_device(ws, d1, d2, cam1, cam2, has1, has2, r1, r2, E, nbytes, th, thresh, m1, m2)
+        assert n == nref and np.array_equal(got, ref)
+        # a second call on the same workspace (state fully reset per call)
+        n, got = _run_tri_device(ws, d1, d2, cam1, cam2, has1, has2, r1, r2, E, nbytes, th, thresh, m1, m2)
+        assert n == nref and np.array_equal(got, ref)
+    finally:
+        L.mcs_tri_workspace_destroy(ws)
+    got = np.zeros(len(d1), np.int32)
+    nm = ctypes.c_int32()
+    if masked:
+        rc = L.mcs_search_for_triangulation_raw_masked(
+            _p(d1), _p(m1), _p(cam1), _p(has1), _p(np.ascontiguousarray(r1)), len(d1),
+            _p(d2), _p(m2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), len(d2), E.shape[0],
+            _p(np.ascontiguousarray(E)), nbytes, th, thresh, _p(got), ctypes.byref(nm))
+    else:
+        rc = L.mcs_search_for_triangulation_raw(
+            _p(d1), _p(cam1), _p(has1), _p(np.ascontiguousarray(r1)), len(d1),
+            _p(d2), _p(cam2), _p(has2), _p(np.ascontiguousarray(r2)), len(d2), E.shape[0],
+            _p(np.ascontiguousarray(E)), nbytes, th, thresh, _p(got), ctypes.byref(nm))
+    assert rc == 0 and nm.value == nref and np.array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_triangulation_device_capacity_errors(gpu):
+    import mcs_amd
+    L = mcs_amd.lib()
+    ws = ctypes.c_void_p()
+    assert L.mcs_tri_workspace_create(0, 10, 1 << 20, ctypes.byref(ws)) == -1
+    assert L.mcs_tri_workspace_create(0, 10, 20, ctypes.byref(ws)) == 0
+    try:
+        n = np.zeros(1, np.int32)
+        rc = L.mcs_search_for_triangulation_raw_device(ws, None, None, None, None, None, 11, None, None, None,
+                                                       None, None, 5, 1, None, 32, 64, 0.3, None, _p(n), None)
+        assert rc == -2 and b"capacity" in L.mcs_last_error()
+    finally:
+        L.mcs_tri_workspace_destroy(ws)
