@@ -68,7 +68,8 @@ int mcs_search_for_triangulation_raw(const uint8_t* desc1, const int32_t* cam1,
  * TH_LOW is floor(featDim), src/cORBmatcher.cpp:52-65): distances are
  * DescriptorDistance64Masked(d1, d2, m1, m2) (src/cORBmatcher.cpp:1052-1056, 2457-2477).
  * mask1 [n1][bytes], mask2 [n2][bytes] host, both required.  Both entries reject
- * n2 >= 2^20 and cameras outside [0, ncams) with MCS_ERR_ARG. */
+ * n2 >= 2^19 and cameras outside [0, ncams) with MCS_ERR_ARG (the device search keeps a
+ * vbMatched2 bitmap of KF2 in LDS). */
 int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t* mask1,
                                             const int32_t* cam1, const uint8_t* has_mp1,
                                             const double* rays1, int32_t n1,
@@ -87,7 +88,7 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
  * d_mask1 / d_mask2: both null (ORB, DescriptorDistance64) or both set (mdBRIEF, ...Masked).
  * d_E [ncams][ncams][9] (mcs_compute_e_rig).  Out: d_matches12[n1] (-1 = none), *d_n_matches.
  * Keypoints whose camera lies outside [0, ncams) never match (the host entries reject them).
- * The workspace holds per-query candidate slots; n1 <= max_n1, n2 <= max_n2 < 2^20. */
+ * The workspace holds per-query candidate slots; n1 <= max_n1, n2 <= max_n2 < 2^19. */
 typedef struct mcs_tri_workspace mcs_tri_workspace;
 int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs_tri_workspace** out);
 void mcs_tri_workspace_destroy(mcs_tri_workspace* ws);

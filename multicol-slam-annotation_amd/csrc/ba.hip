@@ -260,7 +260,6 @@ struct Dev {
   double lam, lam0;                                   // lambda; lambda on rank 0, 0 elsewhere
   const int32_t* pr_ptr; const uint2* pr;             // edge pairs (e1, e2) per block
   const int32_t* nitem;                               // k_schur items (device-built count)
-  int schur_xcd;                                      // k_schur: contiguous item ranges per XCD
   int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
   double* err; double* w; double* jp; double* jl; double* hpl; double* y; double* chi; double* rchi;
@@ -926,18 +925,7 @@ __global__ __launch_bounds__(256) void k_schur(Dev d) {
   if (lm_done(d)) return;
   const double lam0 = lam0_of(d);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  // Items are block-major and blocks row-major (pose i, then j <= i): neighbouring items read
-  // the same pose's Y rows.  Workgroups go round-robin over the 8 XCDs (blockIdx % 8), each
-  // with its own L2, so with schur_xcd every XCD takes one contiguous range of workgroups'
-  // items instead (a bijection of [0, G)) and re-reads hit its L2 instead of the MALL.
-  int wg = blockIdx.x;
-  if (d.schur_xcd) {
-    const int G = gridDim.x, x = wg & 7, r = wg >> 3;
-    int pre = 0;
-    for (int k = 0; k < x; k++) pre += (G - k + 7) >> 3;
-    wg = pre + r;
-  }
-  const int it = wg * 4 + w;
+  const int it = blockIdx.x * 4 + w;
   if (it >= *d.nitem) return;
   const int blk = d.it_blk[it], c = d.it_chunk[it], slot = d.it_slot[it];
   const int bi = d.blk_i[blk], bj = d.blk_j[blk];
@@ -1676,11 +1664,6 @@ struct Optimizer {
     d.blk_nch = nch; d.blk_slot0 = slot_off;
     it_nch_dev = it_nch;
     d.nitem = nitem;
-    static const int schur_xcd = [] {
-      const char* e = std::getenv("MCS_SCHUR_XCD");
-      return (e && e[0] == '0') ? 0 : 1;
-    }();
-    d.schur_xcd = schur_xcd;
     return MCS_OK;
   }
 

@@ -7,6 +7,8 @@
 #include "common.hpp"
 #include "../../include/mcs_matcher.h"
 #include "ldlt.hpp"
+#include <cstring>
+#include <rocprim/rocprim.hpp>
 #include <algorithm>
 #include <new>
 #include <vector>
@@ -507,23 +509,37 @@ __host__ __device__ __forceinline__ bool epi_check(const double* r1, const doubl
   return (nom * nom) / den < thresh;
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
 // ---- SearchForTriangulationRaw on the device (src/cORBmatcher.cpp:1016-1089)
 // The reference walks KF1's keypoints in index order; for each it sorts the (dist, idx2) list of
 // unmatched same-camera KF2 keypoints with dist <= TH_LOW, takes best = the first list entry,
 // and accepts the first entry with dist <= cvRound(2 best) that passes CheckDistEpipolarLine,
-// marking it in vbMatched2.  With keys (dist << 20 | idx2) the sorted order is key order, so a
-// query's decision is: best = min key among unmatched candidates, winner = min key among
-// unmatched candidates with dist <= 2 best that pass the check.  The only state between
-// queries is vbMatched2, and a query can only be affected by earlier queries that list one of
-// its candidates.  Three stream-ordered kernels:
-//   k_tri_radius  (one thread per query): candidate keys (+ epipolar verdict in bit 30) into a
-//                 fixed kTriCap slot per query, full count, and per-KF2-keypoint reference counts
-//   k_tri_private (one thread per query): a query whose candidates nobody else lists decides
-//                 alone (nothing can be matched before it); the others are marked -2
-//   k_tri_shared  (one wave): the marked queries in index order against an LDS vbMatched2
-//                 bitmap (private winners are never listed by a marked query); a query with more
+// marking it in vbMatched2.  With keys (dist << 20 | idx2) the sorted order is key order.  The
+// only state between queries is vbMatched2, and KF2 keypoint i2 can only be taken by a query
+// that lists it AND passes the epipolar check with it.  Kernels (stream-ordered):
+//   k_tri_radius  (query tiles x train segments): candidate keys (+ epipolar verdict in bit 30)
+//                 appended to a kTriCap slot per query; per KF2 keypoint, how many queries list
+//                 it and how many of them pass the check
+//   k_tri_private (one thread per query): a query none of whose candidates another query could
+//                 take, and none of whose passing candidates another query lists, decides alone
+//                 (its outcome neither depends on nor changes anyone's vbMatched2 view); the
+//                 others are marked -2 and flagged for the ordered pass
+//   two exclusive scans (rocPRIM) give each flagged query its place and key offset
+//   k_tri_gather  (one wave per flagged query): its keys sorted into one flat array, flagged
+//                 queries in index order
+//   k_tri_seq     (one wave): the flagged queries in index order against an LDS vbMatched2
+//                 bitmap, streaming the flat keys through two LDS windows with the next window
+//                 prefetched; per query a ballot finds the first unmatched key (best) and a
+//                 second the first unmatched passing key with dist <= 2 best.  A query with more
 //                 than kTriCap candidates rescans KF2 on the fly (exact, rare).
-constexpr int kTriCap = 64;
+constexpr int kTriCap = 512;
+constexpr int kTriSeg = 8;       // train segments of k_tri_radius (grid.y)
+constexpr int kTriWin = 1024;    // keys per k_tri_seq LDS window (16 per lane)
 constexpr uint32_t kTriPass = 1u << 30, kTriKey = kTriPass - 1;
 
 template <int W, bool MASKED>
@@ -533,7 +549,7 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
     const uint8_t* __restrict__ B, const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
     const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int nb, int ncams,
     const double* __restrict__ E, int th, double thresh, uint32_t* __restrict__ cand,
-    int32_t* __restrict__ cnt_out, int32_t* __restrict__ ref2) {
+    int32_t* __restrict__ cnt, int32_t* __restrict__ ref_all, int32_t* __restrict__ ref_pass) {
   __shared__ uint4 tile[kHamTile * (W / 4)];
   __shared__ uint4 mtile[MASKED ? kHamTile * (W / 4) : 1];
   __shared__ int tcam[kHamTile];
@@ -556,10 +572,11 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
   } else {
     for (int k = 0; k < 9; k++) Em[k] = 0.0;
   }
-  int cnt = 0;
   uint32_t* const out = cand + (int64_t)(qi < na ? qi : 0) * kTriCap;
-  for (int t0 = 0; t0 < nb; t0 += kHamTile) {
-    const int nt_tile = min(kHamTile, nb - t0);
+  const int per = ((nb + kTriSeg - 1) / kTriSeg + kHamTile - 1) / kHamTile * kHamTile;
+  const int tb = blockIdx.y * per, te = min(nb, tb + per);
+  for (int t0 = tb; t0 < te; t0 += kHamTile) {
+    const int nt_tile = min(kHamTile, te - t0);
     __syncthreads();
     const uint4* src = reinterpret_cast<const uint4*>(B + (int64_t)t0 * W * 4);
     for (int i = threadIdx.x; i < nt_tile * (W / 4); i += kHamThreads) tile[i] = src[i];
@@ -577,41 +594,44 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
                            : ham_dist_v<W>(q, &tile[j * (W / 4)]);
       if (d <= th) {
         const int i2 = t0 + j;
-        if (cnt < kTriCap) {
-          const bool pass = epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh);
-          out[cnt] = ((uint32_t)d << 20) | (uint32_t)i2 | (pass ? kTriPass : 0u);
-        }
-        cnt++;
-        atomicAdd(ref2 + i2, 1);
+        const bool pass = epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh);
+        const int slot = atomicAdd(cnt + qi, 1);
+        if (slot < kTriCap) out[slot] = ((uint32_t)d << 20) | (uint32_t)i2 | (pass ? kTriPass : 0u);
+        atomicAdd(ref_all + i2, 1);
+        if (pass) atomicAdd(ref_pass + i2, 1);
       }
     }
   }
-  if (qi < na) cnt_out[qi] = cnt;
 }
 
 __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict__ cand,
                                                      const int32_t* __restrict__ cnt_in,
-                                                     const int32_t* __restrict__ ref2, int na,
+                                                     const int32_t* __restrict__ ref_all,
+                                                     const int32_t* __restrict__ ref_pass, int na,
                                                      int32_t* __restrict__ m12,
-                                                     int32_t* __restrict__ n_matches) {
+                                                     int32_t* __restrict__ n_matches,
+                                                     int32_t* __restrict__ flag,
+                                                     int32_t* __restrict__ len) {
   const int qi = blockIdx.x * 256 + threadIdx.x;
   int won = 0;
   if (qi < na) {
     const int c = cnt_in[qi];
-    int r = -1;
+    int r = -1, fl = 0, ln = 0;
     if (c > kTriCap) {
-      r = -2;
+      r = -2; fl = 1;   // ln = 0: k_tri_seq rescans
     } else if (c > 0) {
       const uint32_t* k = cand + (int64_t)qi * kTriCap;
       uint32_t best = 0xFFFFFFFFu;
       bool alone = true;
       for (int i = 0; i < c; i++) {
         const uint32_t key = k[i];
+        const int i2 = (int)(key & 0xFFFFFu), own = (key & kTriPass) ? 1 : 0;
         best = min(best, key & kTriKey);
-        alone = alone && ref2[key & 0xFFFFFu] == 1;
+        if (own && ref_all[i2] > 1) alone = false;       // it could take a key another lists
+        if (ref_pass[i2] - own > 0) alone = false;      // another could take one of its keys
       }
       if (!alone) {
-        r = -2;
+        r = -2; fl = 1; ln = c;
       } else {
         const uint32_t th = 2u * (best >> 20);   // cvRound(2 * bestDist), integer distance
         uint32_t win = 0xFFFFFFFFu;
@@ -623,54 +643,125 @@ __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict_
       }
     }
     m12[qi] = r;
+    flag[qi] = fl;
+    len[qi] = ln;
+  } else if (qi == na) {   // the scans' total slot
+    flag[qi] = 0;
+    len[qi] = 0;
   }
   const int s = dev::wave_sum(won);
   if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_matches, s);
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+// one wave per flagged query: its keys, ascending by (dist, idx2), to flat[koff[q] ...); the
+// entry (q, offset, count) at its place pos[q] of the ordered list
+__global__ __launch_bounds__(256) void k_tri_gather(const uint32_t* __restrict__ cand,
+                                                    const int32_t* __restrict__ flag,
+                                                    const int32_t* __restrict__ len,
+                                                    const int32_t* __restrict__ pos,
+                                                    const int32_t* __restrict__ koff, int na,
+                                                    uint32_t* __restrict__ flat,
+                                                    int4* __restrict__ entries) {
+  __shared__ uint32_t sk[4][kTriCap];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + wv;
+  if (q >= na || !flag[q]) return;
+  const int c = len[q], o = koff[q];
+  if (lane == 0) entries[pos[q]] = make_int4(q, o, c, 0);
+  const uint32_t* src = cand + (int64_t)q * kTriCap;
+  for (int i = lane; i < c; i += 64) sk[wv][i] = src[i];
+  dev::wave_sync();
+  for (int i = lane; i < c; i += 64) {   // rank by counting (keys are distinct: idx2 differs)
+    const uint32_t key = sk[wv][i], kk = key & kTriKey;
+    int rank = 0;
+    for (int j = 0; j < c; j++) rank += (sk[wv][j] & kTriKey) < kk;
+    flat[o + rank] = key;
+  }
 }
 
+// DPP-free wave helpers on ballots: the lowest set lane of a mask, and lane l's value
+__device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
+
 template <int W, bool MASKED>
-__global__ __launch_bounds__(64) void k_tri_shared(
+__global__ __launch_bounds__(64) void k_tri_seq(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA, const int32_t* __restrict__ camA,
-    const double* __restrict__ raysA, int na, const uint8_t* __restrict__ B,
+    const double* __restrict__ raysA, const uint8_t* __restrict__ B,
     const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
-    const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int nb, int ncams,
-    const double* __restrict__ E, int th_low, double thresh, const uint32_t* __restrict__ cand,
-    const int32_t* __restrict__ cnt_in, int32_t* __restrict__ m12, int32_t* __restrict__ n_matches) {
-  extern __shared__ uint32_t matched2[];   // vbMatched2 bitmap, nb bits
+    const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int na, int nb, int ncams,
+    const double* __restrict__ E, int th_low, double thresh, const uint32_t* __restrict__ flat,
+    const int4* __restrict__ entries, const int32_t* __restrict__ pos,
+    int32_t* __restrict__ m12, int32_t* __restrict__ n_matches) {
+  extern __shared__ uint32_t smem[];
+  uint32_t* const win = smem;                    // [2][kTriWin] key windows
+  uint32_t* const matched2 = smem + 2 * kTriWin;  // vbMatched2 bitmap, nb bits
   const int lane = threadIdx.x;
   const int nwords = (nb + 31) >> 5;
   for (int i = lane; i < nwords; i += 64) matched2[i] = 0u;
-  dev::wave_sync();
+  const int ns = pos[na];                         // flagged queries
   auto is_matched = [&](uint32_t i2) { return (matched2[i2 >> 5] >> (i2 & 31)) & 1u; };
+  constexpr int R = kTriWin / 64;
+  // windows cw, cw + 1 live in LDS slots cw & 1, (cw + 1) & 1; window cw + 2 is in flight
+  uint32_t pre[R];
+  auto load_win = [&](int wj, uint32_t (&v)[R]) {
+#pragma unroll
+    for (int k = 0; k < R; k++) v[k] = flat[(int64_t)wj * kTriWin + 64 * k + lane];
+  };
+  auto store_win = [&](int wj, const uint32_t (&v)[R]) {
+#pragma unroll
+    for (int k = 0; k < R; k++) win[(wj & 1) * kTriWin + 64 * k + lane] = v[k];
+  };
+  // the flat array is padded by two windows (workspace), so whole-window loads stay inside it
+  {
+    uint32_t v0[R], v1[R];
+    load_win(0, v0);
+    load_win(1, v1);
+    store_win(0, v0);
+    store_win(1, v1);
+    load_win(2, pre);
+  }
+  int cw = 0;
+  dev::wave_sync();
   int nm = 0;
-  for (int base = 0; base < na; base += 64) {
-    const int qi = base + lane;
-    const int mine = qi < na ? m12[qi] : -1;
-    const int mycnt = qi < na ? cnt_in[qi] : 0;
-    uint64_t todo = __ballot(mine == -2);
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const int q = base + j;
-      const int c = __builtin_amdgcn_readlane(mycnt, j);
-      uint32_t win = 0xFFFFFFFFu;
-      if (c <= kTriCap) {
-        const uint32_t key = lane < c ? cand[(int64_t)q * kTriCap + lane] : 0u;
-        const bool unm = lane < c && !is_matched(key & 0xFFFFFu);
-        const uint32_t best = wave_min_u32(unm ? (key & kTriKey) : 0xFFFFFFFFu);
-        if (best != 0xFFFFFFFFu) {
+  int4 ent = lane < ns ? entries[lane] : make_int4(0, 0, 0, 0);
+  for (int base = 0; base < ns; base += 64) {
+    const int4 cur = ent;
+    if (base + 64 + lane < ns) ent = entries[base + 64 + lane];   // next chunk's entries
+    const int nin = min(64, ns - base);
+    for (int i = 0; i < nin; i++) {
+      const int q = __builtin_amdgcn_readlane(cur.x, i);
+      const int o = __builtin_amdgcn_readlane(cur.y, i);
+      const int c = __builtin_amdgcn_readlane(cur.z, i);
+      uint32_t wkey = 0xFFFFFFFFu;
+      if (c > 0) {
+        if (o / kTriWin > cw) {   // advance one window (c <= kTriCap < kTriWin)
+          store_win(cw + 2, pre);
+          cw++;
+          load_win(cw + 2, pre);
+          dev::wave_sync();
+        }
+        auto key_at = [&](int k) { const int g = o + k; return win[((g / kTriWin) & 1) * kTriWin + (g % kTriWin)]; };
+        int rb = -1;
+        uint32_t best = 0;
+        for (int r = 0; r * 64 < c; r++) {
+          const bool valid = r * 64 + lane < c;
+          const uint32_t key = valid ? key_at(r * 64 + lane) : 0u;
+          const uint64_t b = __ballot(valid && !is_matched(key & 0xFFFFFu));
+          if (b) { best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; rb = r; break; }
+        }
+        if (rb >= 0) {
           const uint32_t th = 2u * (best >> 20);
-          const bool ok = unm && (key & kTriPass) && ((key & kTriKey) >> 20) <= th;
-          win = wave_min_u32(ok ? (key & kTriKey) : 0xFFFFFFFFu);
+          for (int r = rb; r * 64 < c; r++) {
+            const bool valid = r * 64 + lane < c;
+            const uint32_t key = valid ? key_at(r * 64 + lane) : 0xFFFFFFFFu;
+            const uint32_t d = (key & kTriKey) >> 20;
+            const uint64_t b = __ballot(valid && (key & kTriPass) && d <= th && !is_matched(key & 0xFFFFFu));
+            if (b) { wkey = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; break; }
+            // keys ascend: a round whose first key is already past the threshold ends the scan
+            if ((((uint32_t)__builtin_amdgcn_readlane((int)key, 63) & kTriKey) >> 20) > th) break;
+          }
         }
       } else {
-        // more candidates than the slot holds: rescan KF2 for this query (same filters)
+        // more candidates than a slot holds: rescan KF2 for this query (same filters)
         const int qc = camA[q];
         uint32_t qd[W], qmk[W];
         load_desc_row<W>(qd, A + (int64_t)q * W * 4);
@@ -712,10 +803,10 @@ __global__ __launch_bounds__(64) void k_tri_shared(
             if (d <= th_low && d <= th && epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh))
               lw = min(lw, ((uint32_t)d << 20) | (uint32_t)i2);
           }
-          win = wave_min_u32(lw);
+          wkey = wave_min_u32(lw);
         }
       }
-      const int r = win != 0xFFFFFFFFu ? (int)(win & 0xFFFFFu) : -1;
+      const int r = wkey != 0xFFFFFFFFu ? (int)(wkey & 0xFFFFFu) : -1;
       if (lane == 0) {
         m12[q] = r;
         if (r >= 0) matched2[r >> 5] |= 1u << (r & 31);
@@ -799,41 +890,76 @@ static void host_compute_e(const double* T1, const double* T2, double* E) {  // 
   host_matmul(S, R12, E, 3, 3, 3);        // t12x * R12
 }
 
+}  // namespace mcs
+
+// Workspace of the device search (sized at creation; reused call after call on one stream).
+struct mcs_tri_workspace {
+  int device = 0, max_n1 = 0, max_n2 = 0;
+  uint32_t* cand = nullptr;     // [max_n1][kTriCap] candidate keys
+  uint32_t* flat = nullptr;     // [max_n1 * kTriCap + 3 kTriWin] sorted keys of flagged queries
+  int4* entries = nullptr;      // [max_n1] (query, key offset, count)
+  int32_t* cnt = nullptr;       // [max_n1]
+  int32_t* flag = nullptr;      // [max_n1 + 1]
+  int32_t* len = nullptr;       // [max_n1 + 1]
+  int32_t* pos = nullptr;       // [max_n1 + 1]
+  int32_t* koff = nullptr;      // [max_n1 + 1]
+  int32_t* ref_all = nullptr;   // [max_n2]
+  int32_t* ref_pass = nullptr;  // [max_n2]
+  void* scan_tmp = nullptr; size_t scan_bytes = 0;
+};
+
+namespace mcs {
+
+static size_t tri_lds_bytes(int n2) { return 2 * kTriWin * 4 + (size_t)((n2 + 31) / 32) * 4; }
+
 // Device pipeline on device buffers (stream-ordered; no host synchronisation).
-static hipError_t tri_run(const uint8_t* dA, const uint8_t* dmA, const int32_t* dcA, const uint8_t* dhA,
-                          const double* drA, int n1, const uint8_t* dB, const uint8_t* dmB,
+static hipError_t tri_run(mcs_tri_workspace* ws, const uint8_t* dA, const uint8_t* dmA, const int32_t* dcA,
+                          const uint8_t* dhA, const double* drA, int n1, const uint8_t* dB, const uint8_t* dmB,
                           const int32_t* dcB, const uint8_t* dhB, const double* drB, int n2, int ncams,
-                          const double* dE, int bytes, int th_low, double thresh, uint32_t* cand,
-                          int32_t* cnt, int32_t* ref2, int32_t* m12, int32_t* nmatch, hipStream_t st) {
+                          const double* dE, int bytes, int th_low, double thresh, int32_t* m12,
+                          int32_t* nmatch, hipStream_t st) {
   hipError_t e = hipMemsetAsync(nmatch, 0, sizeof(int32_t), st);
-  if (e == hipSuccess) e = hipMemsetAsync(ref2, 0, sizeof(int32_t) * (size_t)n2, st);
+  if (e == hipSuccess) e = hipMemsetAsync(ws->cnt, 0, sizeof(int32_t) * (size_t)n1, st);
+  if (e == hipSuccess) e = hipMemsetAsync(ws->ref_all, 0, sizeof(int32_t) * (size_t)n2, st);
+  if (e == hipSuccess) e = hipMemsetAsync(ws->ref_pass, 0, sizeof(int32_t) * (size_t)n2, st);
   if (e != hipSuccess) return e;
   const bool masked = dmA != nullptr;
-  const dim3 g((n1 + kHamThreads - 1) / kHamThreads);
+  const dim3 g((n1 + kHamThreads - 1) / kHamThreads, kTriSeg);
 #define MCS_TRI_RADIUS(WW, MM)                                                                   \
   hipLaunchKernelGGL((k_tri_radius<WW, MM>), g, dim3(kHamThreads), 0, st, dA, dmA, dcA, dhA, drA, \
-                     n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, cand, cnt, ref2)
+                     n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, ws->cand, ws->cnt, \
+                     ws->ref_all, ws->ref_pass)
   if (bytes == 16) { if (masked) MCS_TRI_RADIUS(4, true); else MCS_TRI_RADIUS(4, false); }
   else if (bytes == 32) { if (masked) MCS_TRI_RADIUS(8, true); else MCS_TRI_RADIUS(8, false); }
   else { if (masked) MCS_TRI_RADIUS(16, true); else MCS_TRI_RADIUS(16, false); }
 #undef MCS_TRI_RADIUS
-  hipLaunchKernelGGL(k_tri_private, dim3((n1 + 255) / 256), dim3(256), 0, st, cand, cnt, ref2, n1, m12,
-                     nmatch);
-  const int lds = ((n2 + 31) / 32) * 4;
+  hipLaunchKernelGGL(k_tri_private, dim3((n1 + 1 + 255) / 256), dim3(256), 0, st, ws->cand, ws->cnt, ws->ref_all,
+                     ws->ref_pass, n1, m12, nmatch, ws->flag, ws->len);
+  auto plus = rocprim::plus<int32_t>();
+  size_t b1 = ws->scan_bytes;
+  if ((e = rocprim::exclusive_scan(ws->scan_tmp, b1, ws->flag, ws->pos, 0, (size_t)n1 + 1, plus, st)) != hipSuccess)
+    return e;
+  b1 = ws->scan_bytes;
+  if ((e = rocprim::exclusive_scan(ws->scan_tmp, b1, ws->len, ws->koff, 0, (size_t)n1 + 1, plus, st)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(k_tri_gather, dim3((n1 + 3) / 4), dim3(256), 0, st, ws->cand, ws->flag, ws->len, ws->pos,
+                     ws->koff, n1, ws->flat, ws->entries);
+  const int lds = (int)tri_lds_bytes(n2);
   const void* fn = nullptr;
-#define MCS_TRI_SHARED_FN(WW, MM) fn = (const void*)&k_tri_shared<WW, MM>
-  if (bytes == 16) { if (masked) MCS_TRI_SHARED_FN(4, true); else MCS_TRI_SHARED_FN(4, false); }
-  else if (bytes == 32) { if (masked) MCS_TRI_SHARED_FN(8, true); else MCS_TRI_SHARED_FN(8, false); }
-  else { if (masked) MCS_TRI_SHARED_FN(16, true); else MCS_TRI_SHARED_FN(16, false); }
-#undef MCS_TRI_SHARED_FN
+#define MCS_TRI_SEQ_FN(WW, MM) fn = (const void*)&k_tri_seq<WW, MM>
+  if (bytes == 16) { if (masked) MCS_TRI_SEQ_FN(4, true); else MCS_TRI_SEQ_FN(4, false); }
+  else if (bytes == 32) { if (masked) MCS_TRI_SEQ_FN(8, true); else MCS_TRI_SEQ_FN(8, false); }
+  else { if (masked) MCS_TRI_SEQ_FN(16, true); else MCS_TRI_SEQ_FN(16, false); }
+#undef MCS_TRI_SEQ_FN
   if (lds > 64 * 1024 && (e = ldlt::set_lds_limit(fn, lds)) != hipSuccess) return e;
-#define MCS_TRI_SHARED(WW, MM)                                                                    \
-  hipLaunchKernelGGL((k_tri_shared<WW, MM>), dim3(1), dim3(64), lds, st, dA, dmA, dcA, drA, n1, dB, \
-                     dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, cand, cnt, m12, nmatch)
-  if (bytes == 16) { if (masked) MCS_TRI_SHARED(4, true); else MCS_TRI_SHARED(4, false); }
-  else if (bytes == 32) { if (masked) MCS_TRI_SHARED(8, true); else MCS_TRI_SHARED(8, false); }
-  else { if (masked) MCS_TRI_SHARED(16, true); else MCS_TRI_SHARED(16, false); }
-#undef MCS_TRI_SHARED
+#define MCS_TRI_SEQ(WW, MM)                                                                       \
+  hipLaunchKernelGGL((k_tri_seq<WW, MM>), dim3(1), dim3(64), lds, st, dA, dmA, dcA, drA, dB, dmB, dcB, \
+                     dhB, drB, n1, n2, ncams, dE, th_low, thresh, ws->flat, ws->entries, ws->pos, m12, \
+                     nmatch)
+  if (bytes == 16) { if (masked) MCS_TRI_SEQ(4, true); else MCS_TRI_SEQ(4, false); }
+  else if (bytes == 32) { if (masked) MCS_TRI_SEQ(8, true); else MCS_TRI_SEQ(8, false); }
+  else { if (masked) MCS_TRI_SEQ(16, true); else MCS_TRI_SEQ(16, false); }
+#undef MCS_TRI_SEQ
   return hipGetLastError();
 }
 
@@ -851,7 +977,7 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   for (int i = 0; i < n1; i++) matches12[i] = -1;
   if (n1 <= 0 || n2 <= 0) return MCS_OK;
   // candidates are packed (dist << 20 | idx2): train index must fit 20 bits
-  if (n2 >= (1 << 20)) { set_error("triangulation: at most 2^20 - 1 keypoints in KF2"); return MCS_ERR_ARG; }
+  if (n2 >= (1 << 19)) { set_error("triangulation: at most 2^19 - 1 keypoints in KF2"); return MCS_ERR_ARG; }
   if (!desc1 || !desc2 || !cam1 || !cam2 || !has_mp1 || !has_mp2 || !rays1 || !rays2 || !E ||
       ncams <= 0)
     return MCS_ERR_ARG;
@@ -869,10 +995,8 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   // host entry: upload, run the device search, download (one synchronisation)
   uint8_t *dA = nullptr, *dB = nullptr, *dmA = nullptr, *dmB = nullptr, *dhA = nullptr,
           *dhB = nullptr;
-  int32_t *dcA = nullptr, *dcB = nullptr, *dcnt = nullptr, *dref = nullptr, *dm12 = nullptr,
-          *dn = nullptr;
+  int32_t *dcA = nullptr, *dcB = nullptr, *dm12 = nullptr, *dn = nullptr;
   double *drA = nullptr, *drB = nullptr, *dE = nullptr;
-  uint32_t* dcand = nullptr;
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) { if (e == hipSuccess) e = x; };
   chk(hipMalloc((void**)&dA, (size_t)n1 * bytes));
@@ -890,9 +1014,6 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   chk(hipMalloc((void**)&drA, 24 * (size_t)n1));
   chk(hipMalloc((void**)&drB, 24 * (size_t)n2));
   chk(hipMalloc((void**)&dE, 72 * (size_t)ncams * ncams));
-  chk(hipMalloc((void**)&dcand, 4 * (size_t)n1 * kTriCap));
-  chk(hipMalloc((void**)&dcnt, 4 * (size_t)n1));
-  chk(hipMalloc((void**)&dref, 4 * (size_t)n2));
   chk(hipMalloc((void**)&dm12, 4 * (size_t)n1));
   chk(hipMalloc((void**)&dn, 4));
   chk(hipMemcpy(dA, desc1, (size_t)n1 * bytes, hipMemcpyHostToDevice));
@@ -904,12 +1025,17 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   chk(hipMemcpy(drA, rays1, 24 * (size_t)n1, hipMemcpyHostToDevice));
   chk(hipMemcpy(drB, rays2, 24 * (size_t)n2, hipMemcpyHostToDevice));
   chk(hipMemcpy(dE, E, 72 * (size_t)ncams * ncams, hipMemcpyHostToDevice));
+  int dev = 0;
+  chk(hipGetDevice(&dev));
+  mcs_tri_workspace* ws = nullptr;
+  if (e == hipSuccess && (rc = mcs_tri_workspace_create(dev, n1, n2, &ws)) != MCS_OK) e = hipErrorOutOfMemory;
   if (e == hipSuccess)
-    e = tri_run(dA, dmA, dcA, dhA, drA, n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, bytes, th_low,
-                epi_thresh, dcand, dcnt, dref, dm12, dn, nullptr);
+    e = tri_run(ws, dA, dmA, dcA, dhA, drA, n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, bytes, th_low,
+                epi_thresh, dm12, dn, nullptr);
   chk(hipMemcpy(matches12, dm12, 4 * (size_t)n1, hipMemcpyDeviceToHost));
   chk(hipMemcpy(n_matches, dn, 4, hipMemcpyDeviceToHost));
-  void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, drA, drB, dE, dcand, dcnt, dref, dm12, dn};
+  mcs_tri_workspace_destroy(ws);
+  void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, drA, drB, dE, dm12, dn};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (e != hipSuccess) {
@@ -952,16 +1078,9 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
                                   matches12, n_matches);
 }
 
-struct mcs_tri_workspace {
-  int device = 0, max_n1 = 0, max_n2 = 0;
-  uint32_t* cand = nullptr;   // [max_n1][kTriCap]
-  int32_t* cnt = nullptr;     // [max_n1]
-  int32_t* ref2 = nullptr;    // [max_n2]
-};
-
 int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs_tri_workspace** out) {
-  if (!out || max_n1 < 1 || max_n2 < 1 || max_n2 >= (1 << 20)) {
-    set_error("tri workspace: need max_n1 >= 1 and 1 <= max_n2 < 2^20");
+  if (!out || max_n1 < 1 || max_n2 < 1 || max_n2 >= (1 << 19)) {
+    set_error("tri workspace: need max_n1 >= 1 and 1 <= max_n2 < 2^19");
     return MCS_ERR_ARG;
   }
   *out = nullptr;
@@ -972,9 +1091,21 @@ int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs
   auto* w = new (std::nothrow) mcs_tri_workspace();
   if (!w) return MCS_ERR_ARG;
   w->device = device; w->max_n1 = max_n1; w->max_n2 = max_n2;
-  hipError_t e = hipMalloc((void**)&w->cand, 4 * (size_t)max_n1 * kTriCap);
-  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, 4 * (size_t)max_n1);
-  if (e == hipSuccess) e = hipMalloc((void**)&w->ref2, 4 * (size_t)max_n2);
+  const size_t n1 = (size_t)max_n1, n2 = (size_t)max_n2;
+  hipError_t e = hipMalloc((void**)&w->cand, 4 * n1 * kTriCap);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->flat, 4 * (n1 * kTriCap + 3 * kTriWin));
+  if (e == hipSuccess) e = hipMalloc((void**)&w->entries, sizeof(int4) * n1);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, 4 * n1);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->flag, 4 * (n1 + 1));
+  if (e == hipSuccess) e = hipMalloc((void**)&w->len, 4 * (n1 + 1));
+  if (e == hipSuccess) e = hipMalloc((void**)&w->pos, 4 * (n1 + 1));
+  if (e == hipSuccess) e = hipMalloc((void**)&w->koff, 4 * (n1 + 1));
+  if (e == hipSuccess) e = hipMalloc((void**)&w->ref_all, 4 * n2);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->ref_pass, 4 * n2);
+  if (e == hipSuccess)
+    e = rocprim::exclusive_scan(nullptr, w->scan_bytes, w->flag, w->pos, 0, n1 + 1, rocprim::plus<int32_t>(),
+                                (hipStream_t)0);
+  if (e == hipSuccess) e = hipMalloc(&w->scan_tmp, std::max<size_t>(16, w->scan_bytes));
   if (e != hipSuccess) {
     mcs_tri_workspace_destroy(w);
     set_hip_error(e, "tri workspace", __FILE__, __LINE__);
@@ -987,9 +1118,10 @@ int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs
 void mcs_tri_workspace_destroy(mcs_tri_workspace* w) {
   if (!w) return;
   (void)hipSetDevice(w->device);
-  if (w->cand) (void)hipFree(w->cand);
-  if (w->cnt) (void)hipFree(w->cnt);
-  if (w->ref2) (void)hipFree(w->ref2);
+  void* bufs[] = {w->cand, w->flat, w->entries, w->cnt, w->flag, w->len, w->pos, w->koff, w->ref_all,
+                  w->ref_pass, w->scan_tmp};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
   delete w;
 }
 
@@ -1020,9 +1152,9 @@ int mcs_search_for_triangulation_raw_device(mcs_tri_workspace* ws, const uint8_t
     set_error("triangulation: null device buffer");
     return MCS_ERR_ARG;
   }
-  const hipError_t e = tri_run(d_desc1, d_mask1, d_cam1, d_has_mp1, d_rays1, n1, d_desc2, d_mask2, d_cam2,
-                               d_has_mp2, d_rays2, n2, ncams, d_E, bytes, th_low, epi_thresh, ws->cand,
-                               ws->cnt, ws->ref2, d_matches12, d_n_matches, st);
+  const hipError_t e = tri_run(ws, d_desc1, d_mask1, d_cam1, d_has_mp1, d_rays1, n1, d_desc2, d_mask2, d_cam2,
+                               d_has_mp2, d_rays2, n2, ncams, d_E, bytes, th_low, epi_thresh, d_matches12,
+                               d_n_matches, st);
   if (e != hipSuccess) { set_hip_error(e, "triangulation search", __FILE__, __LINE__); return MCS_ERR_HIP; }
   return MCS_OK;
 }

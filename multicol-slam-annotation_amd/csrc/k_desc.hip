@@ -183,11 +183,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   // lane-dependent indices, from constant memory they were L2 round trips inside the compute
   // (one per test round) instead of LDS reads
   __shared__ uint32_t s_icw[2][kRawH * kRawW];
-  // per test: byte offsets ((coordinate + 16) * 16) of its four coordinates into a keypoint's
-  // rotation table (below), x0 | y0 << 16 and x1 | y1 << 16
-  __shared__ uint2 s_pat[512];
-  // per keypoint slot: (v cos, v sin) for v = -16 .. 15, the products rot_x / rot_y form
-  __shared__ __attribute__((aligned(16))) double2 s_rot[8][32];
+  __shared__ uint32_t s_pat[512];
   typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
   typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
   // wave index as a scalar: the pair, its level and counts are wave-uniform
@@ -200,11 +196,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
     s_icw[0][i] = c_icw[0][i];
     s_icw[1][i] = c_icw[1][i];
   }
-  for (int i = threadIdx.x; i < 512; i += 256) {
-    const uint32_t pw = c_pattern_i8[i];
-    auto off = [&](int sh) { return (uint32_t)(((int)(int8_t)((pw >> sh) & 0xFF) + 16) * 16); };
-    s_pat[i] = make_uint2(off(0) | (off(8) << 16), off(16) | (off(24) << 16));
-  }
+  for (int i = threadIdx.x; i < 512; i += 256) s_pat[i] = c_pattern_i8[i];
   __syncthreads();
   // even j0: both keypoints on one level (every level's sel_off is even, build_plan)
   const int j0 = 2 * (item * 4 + wv);
@@ -296,25 +288,14 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   sincos(theta, &sa, &ca);
   const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
   const uint8_t* bc = &s_blr[slot][21 * kBlrRow + 21 + mis];
-  // rotation table of this keypoint: lane hl holds v = hl - 16 (pattern coordinates lie in
-  // [-13, 12]); each entry is the same __dmul_rn(v, cos / sin) rot_x / rot_y form, so a test
-  // point costs two table reads and the two combining adds instead of four products
-  {
-    const double v = (double)(hl - 16);
-    s_rot[slot][hl] = make_double2(__dmul_rn(v, ca), __dmul_rn(v, sa));
-  }
-  dev::wave_sync();
-  const uint8_t* const rt = reinterpret_cast<const uint8_t*>(&s_rot[slot][0]);
-  auto ent = [&](uint32_t o) { return *reinterpret_cast<const double2*>(rt + o); };
   uint32_t w = 0u;   // lane hl keeps test word hl of its half's descriptor
   for (int r = 0; r < nw; r++) {
     const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
-    const uint2 po = s_pat[t];
-    const double2 ex0 = ent(po.x & 0xFFFFu), ey0 = ent(po.x >> 16);
-    const double2 ex1 = ent(po.y & 0xFFFFu), ey1 = ent(po.y >> 16);
-    // rot_y = cvRound(x sin + y cos), rot_x = cvRound(x cos - y sin)
-    const int o0 = rint_magic(__dadd_rn(ex0.y, ey0.x)) * kBlrRow + rint_magic(__dsub_rn(ex0.x, ey0.y));
-    const int o1 = rint_magic(__dadd_rn(ex1.y, ey1.x)) * kBlrRow + rint_magic(__dsub_rn(ex1.x, ey1.y));
+    const uint32_t pw = s_pat[t];
+    const double px0 = (double)(int)(int8_t)(pw & 0xFF), py0 = (double)(int)(int8_t)((pw >> 8) & 0xFF);
+    const double px1 = (double)(int)(int8_t)((pw >> 16) & 0xFF), py1 = (double)(int)(int8_t)(pw >> 24);
+    const int o0 = rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa);
+    const int o1 = rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa);
     const uint64_t b = __ballot(bc[o0] < bc[o1]);
     if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
   }

@@ -185,17 +185,17 @@ def _masks(n, nbytes, seed, keep=0.8):
 
 
 def test_triangulation_rejects_oversized_train(built):
-    """Candidates pack (dist << 20 | idx2): KF2 must hold fewer than 2^20 keypoints; the check
+    """KF2 must hold fewer than 2^19 keypoints (LDS vbMatched2 bitmap of the device search); the check
     runs before any buffer is touched or a device is needed."""
     import mcs_amd
     got = np.zeros(4, np.int32)
     nm = ctypes.c_int32()
     rc = mcs_amd.lib().mcs_search_for_triangulation_raw(
-        None, None, None, None, 4, None, None, None, None, 1 << 20, 3, None, 32, 64, 0.3, _p(got),
+        None, None, None, None, 4, None, None, None, None, 1 << 19, 3, None, 32, 64, 0.3, _p(got),
         ctypes.byref(nm))
     assert rc == -1 and np.all(got == -1) and nm.value == 0
     rc = mcs_amd.lib().mcs_search_for_triangulation_raw_masked(
-        None, None, None, None, None, 4, None, None, None, None, None, 1 << 20, 3, None, 32, 32,
+        None, None, None, None, None, 4, None, None, None, None, None, 1 << 19, 3, None, 32, 32,
         0.3, _p(got), ctypes.byref(nm))
     assert rc == -1
 
@@ -370,7 +370,7 @@ def test_triangulation_device_capacity_errors(gpu):
     import mcs_amd
     L = mcs_amd.lib()
     ws = ctypes.c_void_p()
-    assert L.mcs_tri_workspace_create(0, 10, 1 << 20, ctypes.byref(ws)) == -1
+    assert L.mcs_tri_workspace_create(0, 10, 1 << 19, ctypes.byref(ws)) == -1
     assert L.mcs_tri_workspace_create(0, 10, 20, ctypes.byref(ws)) == 0
     try:
         n = np.zeros(1, np.int32)
