@@ -88,7 +88,7 @@ int mcs_search_for_triangulation_raw_masked(const uint8_t* desc1, const uint8_t*
  * d_mask1 / d_mask2: both null (ORB, DescriptorDistance64) or both set (mdBRIEF, ...Masked).
  * d_E [ncams][ncams][9] (mcs_compute_e_rig).  Out: d_matches12[n1] (-1 = none), *d_n_matches.
  * Keypoints whose camera lies outside [0, ncams) never match (the host entries reject them).
- * The workspace holds per-query candidate slots; n1 <= max_n1, n2 <= max_n2 < 2^19. */
+ * The workspace holds per-query candidate slots; n1 <= max_n1, n2 <= max_n2 < 2^19, ncams <= 8. */
 typedef struct mcs_tri_workspace mcs_tri_workspace;
 int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs_tri_workspace** out);
 void mcs_tri_workspace_destroy(mcs_tri_workspace* ws);

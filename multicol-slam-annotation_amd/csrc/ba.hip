@@ -448,26 +448,44 @@ __device__ __forceinline__ void lm_publish(const LmCtl* c, const LmEnd& le) {
   __hip_atomic_store(&le.sig->seq, le.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
-  __shared__ double s[1024];
+  static_assert(kRedNT == 256, "the tree below folds 1024 slots onto 256 threads");
+  __shared__ double s[3][256];
   __shared__ int rej;
   LmCtl* c = d.ctl;
   const int t = threadIdx.x;
+  // slot ts = t + 256 u (u = 0..3) sums v[ts], v[ts + 1024], ... in order; the tree levels 512
+  // and 256 (s[ts] += s[ts + o]) pair slots of one thread, so they run in registers; 128 and 64
+  // cross waves (LDS); 32 .. 1 stay in wave 0 (shuffles).  Same additions in the same order.
+  double a[3];
+#pragma unroll
   for (int b = 0; b < 3; b++) {
     const double* v = q.v[b];
+    double x[4];
 #pragma unroll
-    for (int u = 0; u < 1024 / kRedNT; u++) {
-      const int ts = t + u * kRedNT;
+    for (int u = 0; u < 4; u++) {
       double acc = 0.0;
-      for (int i = ts; i < q.n[b]; i += 1024) acc = acc + v[i];
-      s[ts] = acc;
+      for (int i = t + 256 * u; i < q.n[b]; i += 1024) acc = acc + v[i];
+      x[u] = acc;
     }
-    __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-      for (int ts = t; ts < o; ts += kRedNT) s[ts] = s[ts] + s[ts + o];
-      __syncthreads();
+    x[0] = x[0] + x[2];   // o = 512
+    x[1] = x[1] + x[3];
+    a[b] = x[0] + x[1];   // o = 256
+    s[b][t] = a[b];
+  }
+  __syncthreads();
+  if (t < 128)
+    for (int b = 0; b < 3; b++) a[b] = s[b][t] + s[b][t + 128];   // o = 128
+  __syncthreads();
+  if (t < 128)
+    for (int b = 0; b < 3; b++) s[b][t] = a[b];
+  __syncthreads();
+  if (t < 64) {
+    for (int b = 0; b < 3; b++) {
+      double w = s[b][t] + s[b][t + 64];                           // o = 64
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) w = w + __shfl_down(w, o, 64);
+      if (t == 0) le.sc[b] = w;
     }
-    if (t == 0) le.sc[b] = s[0];
-    __syncthreads();
   }
   if (t == 0) {
     lm_control(c, le.sc, *le.flag, le.sig);

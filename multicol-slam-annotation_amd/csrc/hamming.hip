@@ -522,40 +522,43 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // marking it in vbMatched2.  With keys (dist << 20 | idx2) the sorted order is key order.  The
 // only state between queries is vbMatched2, and KF2 keypoint i2 can only be taken by a query
 // that lists it AND passes the epipolar check with it.  Kernels (stream-ordered):
-//   k_tri_radius  (query tiles x train segments): candidate keys (+ epipolar verdict in bit 30)
-//                 appended to a kTriCap slot per query; per KF2 keypoint, how many queries list
-//                 it and how many of them pass the check
+//   k_tri_radius  (query tiles x train segments): each (query, segment) thread appends its
+//                 candidate keys to its own kTriSub slots (no returning atomics in the loop),
+//                 counts how many queries list each KF2 keypoint, flags slot overflow
+//   k_tri_pass    (one thread per query and segment): the epipolar verdict of every stored
+//                 candidate into bit 30, and how many queries pass with each KF2 keypoint
 //   k_tri_private (one thread per query): a query none of whose candidates another query could
 //                 take, and none of whose passing candidates another query lists, decides alone
 //                 (its outcome neither depends on nor changes anyone's vbMatched2 view); the
-//                 others are marked -2 and flagged for the ordered pass
+//                 others are marked -2 and flagged for the ordered pass.  After any overflow the
+//                 pass counts are incomplete, so every query goes to the ordered pass.
 //   two exclusive scans (rocPRIM) give each flagged query its place and key offset
 //   k_tri_gather  (one wave per flagged query): its keys sorted into one flat array, flagged
 //                 queries in index order
-//   k_tri_seq     (one wave): the flagged queries in index order against an LDS vbMatched2
-//                 bitmap, streaming the flat keys through two LDS windows with the next window
-//                 prefetched; per query a ballot finds the first unmatched key (best) and a
-//                 second the first unmatched passing key with dist <= 2 best.  A query with more
-//                 than kTriCap candidates rescans KF2 on the fly (exact, rare).
-constexpr int kTriCap = 512;
-constexpr int kTriSeg = 8;       // train segments of k_tri_radius (grid.y)
+//   k_tri_seq     (one wave per camera): the flagged queries in index order against an LDS
+//                 vbMatched2 bitmap, streaming the flat keys through two LDS windows with the
+//                 next window prefetched; per query a ballot finds the first unmatched key
+//                 (best) and a second the first unmatched passing key with dist <= 2 best.  A
+//                 query whose candidates overflowed a slot rescans KF2 on the fly (exact, rare).
+constexpr int kTriSeg = 4;                  // train segments of k_tri_radius (grid.y)
+constexpr int kTriSub = 128;                // candidate slots per (query, segment)
+constexpr int kTriCap = kTriSeg * kTriSub;  // per query
 constexpr int kTriWin = 1024;    // keys per k_tri_seq LDS window (16 per lane)
 constexpr uint32_t kTriPass = 1u << 30, kTriKey = kTriPass - 1;
 
 template <int W, bool MASKED>
 __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA, const int32_t* __restrict__ camA,
-    const uint8_t* __restrict__ hasA, const double* __restrict__ raysA, int na,
-    const uint8_t* __restrict__ B, const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
-    const uint8_t* __restrict__ hasB, const double* __restrict__ raysB, int nb, int ncams,
-    const double* __restrict__ E, int th, double thresh, uint32_t* __restrict__ cand,
-    int32_t* __restrict__ cnt, int32_t* __restrict__ ref_all, int32_t* __restrict__ ref_pass) {
+    const uint8_t* __restrict__ hasA, int na, const uint8_t* __restrict__ B,
+    const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
+    const uint8_t* __restrict__ hasB, int nb, int ncams, int th, uint32_t* __restrict__ cand,
+    int32_t* __restrict__ cnt, int32_t* __restrict__ ref_all, int32_t* __restrict__ overflow) {
   __shared__ uint4 tile[kHamTile * (W / 4)];
   __shared__ uint4 mtile[MASKED ? kHamTile * (W / 4) : 1];
   __shared__ int tcam[kHamTile];
   const int qi = blockIdx.x * kHamThreads + threadIdx.x;
+  const int seg = blockIdx.y;
   uint32_t q[W], qm[W];
-  double r1[3] = {0, 0, 0}, Em[9];
   int qc = -1;
 #pragma unroll
   for (int w = 0; w < W; w++) { q[w] = 0; qm[w] = 0; }
@@ -566,15 +569,11 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
   if (qc >= 0) {
     load_desc_row<W>(q, A + (int64_t)qi * W * 4);
     if (MASKED) load_desc_row<W>(qm, MA + (int64_t)qi * W * 4);
-    for (int k = 0; k < 3; k++) r1[k] = raysA[3 * (int64_t)qi + k];
-    // same camera only (:1040-1041): E[cam1][cam2] with cam2 == cam1
-    for (int k = 0; k < 9; k++) Em[k] = E[9 * ((int64_t)qc * ncams + qc) + k];
-  } else {
-    for (int k = 0; k < 9; k++) Em[k] = 0.0;
   }
-  uint32_t* const out = cand + (int64_t)(qi < na ? qi : 0) * kTriCap;
+  uint32_t* const out = cand + ((int64_t)(qi < na ? qi : 0) * kTriSeg + seg) * kTriSub;
+  int n = 0;
   const int per = ((nb + kTriSeg - 1) / kTriSeg + kHamTile - 1) / kHamTile * kHamTile;
-  const int tb = blockIdx.y * per, te = min(nb, tb + per);
+  const int tb = seg * per, te = min(nb, tb + per);
   for (int t0 = tb; t0 < te; t0 += kHamTile) {
     const int nt_tile = min(kHamTile, te - t0);
     __syncthreads();
@@ -594,12 +593,41 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
                            : ham_dist_v<W>(q, &tile[j * (W / 4)]);
       if (d <= th) {
         const int i2 = t0 + j;
-        const bool pass = epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh);
-        const int slot = atomicAdd(cnt + qi, 1);
-        if (slot < kTriCap) out[slot] = ((uint32_t)d << 20) | (uint32_t)i2 | (pass ? kTriPass : 0u);
+        if (n < kTriSub) out[n] = ((uint32_t)d << 20) | (uint32_t)i2;
+        n++;
         atomicAdd(ref_all + i2, 1);
-        if (pass) atomicAdd(ref_pass + i2, 1);
       }
+    }
+  }
+  if (qi < na) {
+    cnt[(int64_t)qi * kTriSeg + seg] = n;
+    if (n > kTriSub) atomicOr(overflow, 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tri_pass(const int32_t* __restrict__ camA,
+                                                  const double* __restrict__ raysA, int na,
+                                                  const double* __restrict__ raysB, int ncams,
+                                                  const double* __restrict__ E, double thresh,
+                                                  uint32_t* __restrict__ cand,
+                                                  const int32_t* __restrict__ cnt,
+                                                  int32_t* __restrict__ ref_pass) {
+  const int gt = blockIdx.x * 256 + threadIdx.x;
+  if (gt >= na * kTriSeg) return;
+  const int n = min(cnt[gt], kTriSub);
+  if (n == 0) return;
+  const int qi = gt / kTriSeg, qc = camA[qi];
+  double r1[3], Em[9];
+  for (int k = 0; k < 3; k++) r1[k] = raysA[3 * (int64_t)qi + k];
+  // same camera only (:1040-1041): E[cam1][cam2] with cam2 == cam1
+  for (int k = 0; k < 9; k++) Em[k] = E[9 * ((int64_t)qc * ncams + qc) + k];
+  uint32_t* const ks = cand + (int64_t)gt * kTriSub;
+  for (int i = 0; i < n; i++) {
+    const uint32_t key = ks[i];
+    const int i2 = (int)(key & 0xFFFFFu);
+    if (epi_check(r1, raysB + 3 * (int64_t)i2, Em, thresh)) {
+      ks[i] = key | kTriPass;
+      atomicAdd(ref_pass + i2, 1);
     }
   }
 }
@@ -607,7 +635,8 @@ __global__ __launch_bounds__(kHamThreads) void k_tri_radius(
 __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict__ cand,
                                                      const int32_t* __restrict__ cnt_in,
                                                      const int32_t* __restrict__ ref_all,
-                                                     const int32_t* __restrict__ ref_pass, int na,
+                                                     const int32_t* __restrict__ ref_pass,
+                                                     const int32_t* __restrict__ overflow, int na,
                                                      int32_t* __restrict__ m12,
                                                      int32_t* __restrict__ n_matches,
                                                      int32_t* __restrict__ flag,
@@ -615,29 +644,42 @@ __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict_
   const int qi = blockIdx.x * 256 + threadIdx.x;
   int won = 0;
   if (qi < na) {
-    const int c = cnt_in[qi];
+    int c = 0;
+    bool over = false;
+    for (int sg = 0; sg < kTriSeg; sg++) {
+      const int n = cnt_in[(int64_t)qi * kTriSeg + sg];
+      over = over || n > kTriSub;
+      c += n;
+    }
     int r = -1, fl = 0, ln = 0;
-    if (c > kTriCap) {
+    if (over) {
       r = -2; fl = 1;   // ln = 0: k_tri_seq rescans
     } else if (c > 0) {
-      const uint32_t* k = cand + (int64_t)qi * kTriCap;
+      bool alone = *overflow == 0;
       uint32_t best = 0xFFFFFFFFu;
-      bool alone = true;
-      for (int i = 0; i < c; i++) {
-        const uint32_t key = k[i];
-        const int i2 = (int)(key & 0xFFFFFu), own = (key & kTriPass) ? 1 : 0;
-        best = min(best, key & kTriKey);
-        if (own && ref_all[i2] > 1) alone = false;       // it could take a key another lists
-        if (ref_pass[i2] - own > 0) alone = false;      // another could take one of its keys
+      for (int sg = 0; sg < kTriSeg; sg++) {
+        const uint32_t* k = cand + ((int64_t)qi * kTriSeg + sg) * kTriSub;
+        const int n = cnt_in[(int64_t)qi * kTriSeg + sg];
+        for (int i = 0; i < n; i++) {
+          const uint32_t key = k[i];
+          const int i2 = (int)(key & 0xFFFFFu), own = (key & kTriPass) ? 1 : 0;
+          best = min(best, key & kTriKey);
+          if (own && ref_all[i2] > 1) alone = false;       // it could take a key another lists
+          if (ref_pass[i2] - own > 0) alone = false;      // another could take one of its keys
+        }
       }
       if (!alone) {
         r = -2; fl = 1; ln = c;
       } else {
         const uint32_t th = 2u * (best >> 20);   // cvRound(2 * bestDist), integer distance
         uint32_t win = 0xFFFFFFFFu;
-        for (int i = 0; i < c; i++) {
-          const uint32_t key = k[i];
-          if ((key & kTriPass) && ((key & kTriKey) >> 20) <= th) win = min(win, key & kTriKey);
+        for (int sg = 0; sg < kTriSeg; sg++) {
+          const uint32_t* k = cand + ((int64_t)qi * kTriSeg + sg) * kTriSub;
+          const int n = cnt_in[(int64_t)qi * kTriSeg + sg];
+          for (int i = 0; i < n; i++) {
+            const uint32_t key = k[i];
+            if ((key & kTriPass) && ((key & kTriKey) >> 20) <= th) win = min(win, key & kTriKey);
+          }
         }
         if (win != 0xFFFFFFFFu) { r = (int)(win & 0xFFFFFu); won = 1; }
       }
@@ -653,9 +695,11 @@ __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict_
   if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_matches, s);
 }
 
-// one wave per flagged query: its keys, ascending by (dist, idx2), to flat[koff[q] ...); the
-// entry (q, offset, count) at its place pos[q] of the ordered list
+// one wave per flagged query: its keys (the segments' lists), ascending by (dist, idx2), to
+// flat[koff[q] ...); the entry (q, offset, count, camera) at its place pos[q] of the ordered list
 __global__ __launch_bounds__(256) void k_tri_gather(const uint32_t* __restrict__ cand,
+                                                    const int32_t* __restrict__ cnt_in,
+                                                    const int32_t* __restrict__ cam,
                                                     const int32_t* __restrict__ flag,
                                                     const int32_t* __restrict__ len,
                                                     const int32_t* __restrict__ pos,
@@ -667,9 +711,14 @@ __global__ __launch_bounds__(256) void k_tri_gather(const uint32_t* __restrict__
   const int q = blockIdx.x * 4 + wv;
   if (q >= na || !flag[q]) return;
   const int c = len[q], o = koff[q];
-  if (lane == 0) entries[pos[q]] = make_int4(q, o, c, 0);
-  const uint32_t* src = cand + (int64_t)q * kTriCap;
-  for (int i = lane; i < c; i += 64) sk[wv][i] = src[i];
+  if (lane == 0) entries[pos[q]] = make_int4(q, o, c, cam[q]);
+  int at = 0;
+  for (int sg = 0; sg < kTriSeg && c > 0; sg++) {
+    const int n = cnt_in[(int64_t)q * kTriSeg + sg];
+    const uint32_t* src = cand + ((int64_t)q * kTriSeg + sg) * kTriSub;
+    for (int i = lane; i < n; i += 64) sk[wv][at + i] = src[i];
+    at += n;
+  }
   dev::wave_sync();
   for (int i = lane; i < c; i += 64) {   // rank by counting (keys are distinct: idx2 differs)
     const uint32_t key = sk[wv][i], kk = key & kTriKey;
@@ -679,11 +728,13 @@ __global__ __launch_bounds__(256) void k_tri_gather(const uint32_t* __restrict__
   }
 }
 
-// DPP-free wave helpers on ballots: the lowest set lane of a mask, and lane l's value
 __device__ __forceinline__ int first_lane(uint64_t m) { return (int)__builtin_ctzll(m); }
 
+// One wave per camera (a query's candidates are KF2 keypoints of its own camera, so cameras
+// never share vbMatched2 bits): the wave walks the ordered flagged list, takes its camera's
+// entries, and streams their keys through two LDS windows of its own.
 template <int W, bool MASKED>
-__global__ __launch_bounds__(64) void k_tri_seq(
+__global__ __launch_bounds__(512) void k_tri_seq(
     const uint8_t* __restrict__ A, const uint8_t* __restrict__ MA, const int32_t* __restrict__ camA,
     const double* __restrict__ raysA, const uint8_t* __restrict__ B,
     const uint8_t* __restrict__ MB, const int32_t* __restrict__ camB,
@@ -692,15 +743,16 @@ __global__ __launch_bounds__(64) void k_tri_seq(
     const int4* __restrict__ entries, const int32_t* __restrict__ pos,
     int32_t* __restrict__ m12, int32_t* __restrict__ n_matches) {
   extern __shared__ uint32_t smem[];
-  uint32_t* const win = smem;                    // [2][kTriWin] key windows
-  uint32_t* const matched2 = smem + 2 * kTriWin;  // vbMatched2 bitmap, nb bits
-  const int lane = threadIdx.x;
+  const int cam = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t* const matched2 = smem;                                 // vbMatched2 bitmap, nb bits
   const int nwords = (nb + 31) >> 5;
-  for (int i = lane; i < nwords; i += 64) matched2[i] = 0u;
+  uint32_t* const win = smem + ((nwords + 3) & ~3) + cam * 2 * kTriWin;   // this wave's windows
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) matched2[i] = 0u;
+  __syncthreads();
+  if (cam >= ncams) return;
   const int ns = pos[na];                         // flagged queries
   auto is_matched = [&](uint32_t i2) { return (matched2[i2 >> 5] >> (i2 & 31)) & 1u; };
   constexpr int R = kTriWin / 64;
-  // windows cw, cw + 1 live in LDS slots cw & 1, (cw + 1) & 1; window cw + 2 is in flight
   uint32_t pre[R];
   auto load_win = [&](int wj, uint32_t (&v)[R]) {
 #pragma unroll
@@ -710,54 +762,73 @@ __global__ __launch_bounds__(64) void k_tri_seq(
 #pragma unroll
     for (int k = 0; k < R; k++) win[(wj & 1) * kTriWin + 64 * k + lane] = v[k];
   };
-  // the flat array is padded by two windows (workspace), so whole-window loads stay inside it
-  {
-    uint32_t v0[R], v1[R];
-    load_win(0, v0);
-    load_win(1, v1);
-    store_win(0, v0);
-    store_win(1, v1);
-    load_win(2, pre);
-  }
-  int cw = 0;
-  dev::wave_sync();
+  // windows cw, cw + 1 are in LDS (slots cw & 1, (cw + 1) & 1), window cw + 2 in flight; the
+  // flat array is padded by three windows (workspace), so whole-window loads stay inside it
+  int cw = -8;
+  auto ensure = [&](int o) {
+    const int w0 = o / kTriWin;
+    if (w0 == cw) return;
+    if (w0 == cw + 1) {
+      store_win(cw + 2, pre);
+      cw++;
+    } else {
+      uint32_t v0[R], v1[R];
+      load_win(w0, v0);
+      load_win(w0 + 1, v1);
+      store_win(w0, v0);
+      store_win(w0 + 1, v1);
+      cw = w0;
+    }
+    load_win(cw + 2, pre);
+    dev::wave_sync();
+  };
+  auto key_at = [&](int g) { return win[((g / kTriWin) & 1) * kTriWin + (g % kTriWin)]; };
   int nm = 0;
-  int4 ent = lane < ns ? entries[lane] : make_int4(0, 0, 0, 0);
+  int4 ent = lane < ns ? entries[lane] : make_int4(0, 0, 0, -1);
   for (int base = 0; base < ns; base += 64) {
     const int4 cur = ent;
     if (base + 64 + lane < ns) ent = entries[base + 64 + lane];   // next chunk's entries
-    const int nin = min(64, ns - base);
-    for (int i = 0; i < nin; i++) {
+    uint64_t todo = __ballot(base + lane < ns && cur.w == cam);
+    while (todo) {
+      const int i = first_lane(todo);
+      todo &= todo - 1;
       const int q = __builtin_amdgcn_readlane(cur.x, i);
       const int o = __builtin_amdgcn_readlane(cur.y, i);
       const int c = __builtin_amdgcn_readlane(cur.z, i);
       uint32_t wkey = 0xFFFFFFFFu;
       if (c > 0) {
-        if (o / kTriWin > cw) {   // advance one window (c <= kTriCap < kTriWin)
-          store_win(cw + 2, pre);
-          cw++;
-          load_win(cw + 2, pre);
-          dev::wave_sync();
-        }
-        auto key_at = [&](int k) { const int g = o + k; return win[((g / kTriWin) & 1) * kTriWin + (g % kTriWin)]; };
-        int rb = -1;
-        uint32_t best = 0;
-        for (int r = 0; r * 64 < c; r++) {
-          const bool valid = r * 64 + lane < c;
-          const uint32_t key = valid ? key_at(r * 64 + lane) : 0u;
-          const uint64_t b = __ballot(valid && !is_matched(key & 0xFFFFFu));
-          if (b) { best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; rb = r; break; }
-        }
-        if (rb >= 0) {
-          const uint32_t th = 2u * (best >> 20);
-          for (int r = rb; r * 64 < c; r++) {
+        ensure(o);
+        if (c <= 64) {   // one round: best and winner from the same reads
+          const bool valid = lane < c;
+          const uint32_t key = valid ? key_at(o + lane) : 0u;
+          const bool unm = valid && !is_matched(key & 0xFFFFFu);
+          const uint64_t bu = __ballot(unm);
+          if (bu) {
+            const uint32_t best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(bu)) & kTriKey;
+            const uint32_t th = 2u * (best >> 20);
+            const uint64_t bo = __ballot(unm && (key & kTriPass) && ((key & kTriKey) >> 20) <= th);
+            if (bo) wkey = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(bo)) & kTriKey;
+          }
+        } else {
+          int rb = -1;
+          uint32_t best = 0;
+          for (int r = 0; r * 64 < c; r++) {
             const bool valid = r * 64 + lane < c;
-            const uint32_t key = valid ? key_at(r * 64 + lane) : 0xFFFFFFFFu;
-            const uint32_t d = (key & kTriKey) >> 20;
-            const uint64_t b = __ballot(valid && (key & kTriPass) && d <= th && !is_matched(key & 0xFFFFFu));
-            if (b) { wkey = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; break; }
-            // keys ascend: a round whose first key is already past the threshold ends the scan
-            if ((((uint32_t)__builtin_amdgcn_readlane((int)key, 63) & kTriKey) >> 20) > th) break;
+            const uint32_t key = valid ? key_at(o + r * 64 + lane) : 0u;
+            const uint64_t b = __ballot(valid && !is_matched(key & 0xFFFFFu));
+            if (b) { best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; rb = r; break; }
+          }
+          if (rb >= 0) {
+            const uint32_t th = 2u * (best >> 20);
+            for (int r = rb; r * 64 < c; r++) {
+              const bool valid = r * 64 + lane < c;
+              const uint32_t key = valid ? key_at(o + r * 64 + lane) : 0xFFFFFFFFu;
+              const uint32_t d = (key & kTriKey) >> 20;
+              const uint64_t b = __ballot(valid && (key & kTriPass) && d <= th && !is_matched(key & 0xFFFFFu));
+              if (b) { wkey = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b)) & kTriKey; break; }
+              // keys ascend: once a round's last key is past the threshold, no later key qualifies
+              if ((((uint32_t)__builtin_amdgcn_readlane((int)key, 63) & kTriKey) >> 20) > th) break;
+            }
           }
         }
       } else {
@@ -809,9 +880,9 @@ __global__ __launch_bounds__(64) void k_tri_seq(
       const int r = wkey != 0xFFFFFFFFu ? (int)(wkey & 0xFFFFFu) : -1;
       if (lane == 0) {
         m12[q] = r;
-        if (r >= 0) matched2[r >> 5] |= 1u << (r & 31);
+        // LDS atomics of one wave execute in order with its later LDS reads
+        if (r >= 0) atomicOr(&matched2[r >> 5], 1u << (r & 31));
       }
-      dev::wave_sync();
       nm += r >= 0;
     }
   }
@@ -898,7 +969,8 @@ struct mcs_tri_workspace {
   uint32_t* cand = nullptr;     // [max_n1][kTriCap] candidate keys
   uint32_t* flat = nullptr;     // [max_n1 * kTriCap + 3 kTriWin] sorted keys of flagged queries
   int4* entries = nullptr;      // [max_n1] (query, key offset, count)
-  int32_t* cnt = nullptr;       // [max_n1]
+  int32_t* cnt = nullptr;       // [max_n1][kTriSeg]
+  int32_t* overflow = nullptr;  // [1] a (query, segment) overflowed its slots
   int32_t* flag = nullptr;      // [max_n1 + 1]
   int32_t* len = nullptr;       // [max_n1 + 1]
   int32_t* pos = nullptr;       // [max_n1 + 1]
@@ -910,7 +982,9 @@ struct mcs_tri_workspace {
 
 namespace mcs {
 
-static size_t tri_lds_bytes(int n2) { return 2 * kTriWin * 4 + (size_t)((n2 + 31) / 32) * 4; }
+static size_t tri_lds_bytes(int n2, int ncams) {
+  return (size_t)ncams * 2 * kTriWin * 4 + (size_t)(((n2 + 31) / 32 + 3) & ~3) * 4;
+}
 
 // Device pipeline on device buffers (stream-ordered; no host synchronisation).
 static hipError_t tri_run(mcs_tri_workspace* ws, const uint8_t* dA, const uint8_t* dmA, const int32_t* dcA,
@@ -919,22 +993,23 @@ static hipError_t tri_run(mcs_tri_workspace* ws, const uint8_t* dA, const uint8_
                           const double* dE, int bytes, int th_low, double thresh, int32_t* m12,
                           int32_t* nmatch, hipStream_t st) {
   hipError_t e = hipMemsetAsync(nmatch, 0, sizeof(int32_t), st);
-  if (e == hipSuccess) e = hipMemsetAsync(ws->cnt, 0, sizeof(int32_t) * (size_t)n1, st);
+  if (e == hipSuccess) e = hipMemsetAsync(ws->overflow, 0, sizeof(int32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(ws->ref_all, 0, sizeof(int32_t) * (size_t)n2, st);
   if (e == hipSuccess) e = hipMemsetAsync(ws->ref_pass, 0, sizeof(int32_t) * (size_t)n2, st);
   if (e != hipSuccess) return e;
   const bool masked = dmA != nullptr;
   const dim3 g((n1 + kHamThreads - 1) / kHamThreads, kTriSeg);
 #define MCS_TRI_RADIUS(WW, MM)                                                                   \
-  hipLaunchKernelGGL((k_tri_radius<WW, MM>), g, dim3(kHamThreads), 0, st, dA, dmA, dcA, dhA, drA, \
-                     n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, th_low, thresh, ws->cand, ws->cnt, \
-                     ws->ref_all, ws->ref_pass)
+  hipLaunchKernelGGL((k_tri_radius<WW, MM>), g, dim3(kHamThreads), 0, st, dA, dmA, dcA, dhA, n1, dB,  \
+                     dmB, dcB, dhB, n2, ncams, th_low, ws->cand, ws->cnt, ws->ref_all, ws->overflow)
   if (bytes == 16) { if (masked) MCS_TRI_RADIUS(4, true); else MCS_TRI_RADIUS(4, false); }
   else if (bytes == 32) { if (masked) MCS_TRI_RADIUS(8, true); else MCS_TRI_RADIUS(8, false); }
   else { if (masked) MCS_TRI_RADIUS(16, true); else MCS_TRI_RADIUS(16, false); }
 #undef MCS_TRI_RADIUS
+  hipLaunchKernelGGL(k_tri_pass, dim3((n1 * kTriSeg + 255) / 256), dim3(256), 0, st, dcA, drA, n1, drB, ncams, dE,
+                     thresh, ws->cand, ws->cnt, ws->ref_pass);
   hipLaunchKernelGGL(k_tri_private, dim3((n1 + 1 + 255) / 256), dim3(256), 0, st, ws->cand, ws->cnt, ws->ref_all,
-                     ws->ref_pass, n1, m12, nmatch, ws->flag, ws->len);
+                     ws->ref_pass, ws->overflow, n1, m12, nmatch, ws->flag, ws->len);
   auto plus = rocprim::plus<int32_t>();
   size_t b1 = ws->scan_bytes;
   if ((e = rocprim::exclusive_scan(ws->scan_tmp, b1, ws->flag, ws->pos, 0, (size_t)n1 + 1, plus, st)) != hipSuccess)
@@ -942,9 +1017,10 @@ static hipError_t tri_run(mcs_tri_workspace* ws, const uint8_t* dA, const uint8_
   b1 = ws->scan_bytes;
   if ((e = rocprim::exclusive_scan(ws->scan_tmp, b1, ws->len, ws->koff, 0, (size_t)n1 + 1, plus, st)) != hipSuccess)
     return e;
-  hipLaunchKernelGGL(k_tri_gather, dim3((n1 + 3) / 4), dim3(256), 0, st, ws->cand, ws->flag, ws->len, ws->pos,
+  hipLaunchKernelGGL(k_tri_gather, dim3((n1 + 3) / 4), dim3(256), 0, st, ws->cand, ws->cnt, dcA, ws->flag, ws->len, ws->pos,
                      ws->koff, n1, ws->flat, ws->entries);
-  const int lds = (int)tri_lds_bytes(n2);
+  const int lds = (int)tri_lds_bytes(n2, ncams);
+  if (ncams > 8 || lds > 160 * 1024) return hipErrorInvalidValue;   // entry points check first
   const void* fn = nullptr;
 #define MCS_TRI_SEQ_FN(WW, MM) fn = (const void*)&k_tri_seq<WW, MM>
   if (bytes == 16) { if (masked) MCS_TRI_SEQ_FN(4, true); else MCS_TRI_SEQ_FN(4, false); }
@@ -953,7 +1029,7 @@ static hipError_t tri_run(mcs_tri_workspace* ws, const uint8_t* dA, const uint8_
 #undef MCS_TRI_SEQ_FN
   if (lds > 64 * 1024 && (e = ldlt::set_lds_limit(fn, lds)) != hipSuccess) return e;
 #define MCS_TRI_SEQ(WW, MM)                                                                       \
-  hipLaunchKernelGGL((k_tri_seq<WW, MM>), dim3(1), dim3(64), lds, st, dA, dmA, dcA, drA, dB, dmB, dcB, \
+  hipLaunchKernelGGL((k_tri_seq<WW, MM>), dim3(1), dim3(64 * ncams), lds, st, dA, dmA, dcA, drA, dB, dmB, dcB, \
                      dhB, drB, n1, n2, ncams, dE, th_low, thresh, ws->flat, ws->entries, ws->pos, m12, \
                      nmatch)
   if (bytes == 16) { if (masked) MCS_TRI_SEQ(4, true); else MCS_TRI_SEQ(4, false); }
@@ -981,6 +1057,7 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   if (!desc1 || !desc2 || !cam1 || !cam2 || !has_mp1 || !has_mp2 || !rays1 || !rays2 || !E ||
       ncams <= 0)
     return MCS_ERR_ARG;
+  if (ncams > 8) { set_error("triangulation: at most 8 cameras (one ordered-pass wave each)"); return MCS_ERR_UNSUPPORTED; }
   const bool masked = mask1 != nullptr;
   if (masked != (mask2 != nullptr)) { set_error("triangulation: masks for both keyframes or none"); return MCS_ERR_ARG; }
   for (int i = 0; i < n1; i++)
@@ -1095,7 +1172,8 @@ int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs
   hipError_t e = hipMalloc((void**)&w->cand, 4 * n1 * kTriCap);
   if (e == hipSuccess) e = hipMalloc((void**)&w->flat, 4 * (n1 * kTriCap + 3 * kTriWin));
   if (e == hipSuccess) e = hipMalloc((void**)&w->entries, sizeof(int4) * n1);
-  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, 4 * n1);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, 4 * n1 * kTriSeg);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->overflow, 4);
   if (e == hipSuccess) e = hipMalloc((void**)&w->flag, 4 * (n1 + 1));
   if (e == hipSuccess) e = hipMalloc((void**)&w->len, 4 * (n1 + 1));
   if (e == hipSuccess) e = hipMalloc((void**)&w->pos, 4 * (n1 + 1));
@@ -1118,7 +1196,7 @@ int mcs_tri_workspace_create(int32_t device, int32_t max_n1, int32_t max_n2, mcs
 void mcs_tri_workspace_destroy(mcs_tri_workspace* w) {
   if (!w) return;
   (void)hipSetDevice(w->device);
-  void* bufs[] = {w->cand, w->flat, w->entries, w->cnt, w->flag, w->len, w->pos, w->koff, w->ref_all,
+  void* bufs[] = {w->cand, w->flat, w->entries, w->cnt, w->overflow, w->flag, w->len, w->pos, w->koff, w->ref_all,
                   w->ref_pass, w->scan_tmp};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -1139,6 +1217,7 @@ int mcs_search_for_triangulation_raw_device(mcs_tri_workspace* ws, const uint8_t
   if (rc) return rc;
   if (!ws || !d_n_matches || n1 < 0 || n2 < 0 || ncams <= 0) { set_error("triangulation: bad arguments"); return MCS_ERR_ARG; }
   if (n1 > ws->max_n1 || n2 > ws->max_n2) { set_error("triangulation: n1 / n2 above the workspace capacity"); return MCS_ERR_CAPACITY; }
+  if (ncams > 8) { set_error("triangulation: at most 8 cameras (one ordered-pass wave each)"); return MCS_ERR_UNSUPPORTED; }
   if ((d_mask1 != nullptr) != (d_mask2 != nullptr)) { set_error("triangulation: masks for both keyframes or none"); return MCS_ERR_ARG; }
   MCS_HIP_CHECK(hipSetDevice(ws->device));
   hipStream_t st = (hipStream_t)stream;
