@@ -540,8 +540,8 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 //                 next window prefetched; per query a ballot finds the first unmatched key
 //                 (best) and a second the first unmatched passing key with dist <= 2 best.  A
 //                 query whose candidates overflowed a slot rescans KF2 on the fly (exact, rare).
-constexpr int kTriSeg = 4;                  // train segments of k_tri_radius (grid.y)
-constexpr int kTriSub = 128;                // candidate slots per (query, segment)
+constexpr int kTriSeg = 16;                 // train segments of k_tri_radius (grid.y)
+constexpr int kTriSub = 96;                 // candidate slots per (query, segment)
 constexpr int kTriCap = kTriSeg * kTriSub;  // per query
 constexpr int kTriWin = 1024;    // keys per k_tri_seq LDS window (16 per lane)
 constexpr uint32_t kTriPass = 1u << 30, kTriKey = kTriPass - 1;
@@ -651,6 +651,7 @@ __global__ __launch_bounds__(256) void k_tri_private(const uint32_t* __restrict_
       over = over || n > kTriSub;
       c += n;
     }
+    over = over || c > kTriWin;   // k_tri_seq keeps a query's keys inside two LDS windows
     int r = -1, fl = 0, ln = 0;
     if (over) {
       r = -2; fl = 1;   // ln = 0: k_tri_seq rescans
