@@ -177,8 +177,12 @@ __device__ __forceinline__ float ic_angle_lds(const uint32_t* rawp, int hl) {
 // Two keypoints per wave, one per 32-lane half: the per-keypoint scalar work (level lookup,
 // fastAtan2, double sincos, keypoint record) runs once for both, the 8-32 test words of a
 // descriptor come from one 64-bit ballot per 32 tests (low half / high half).
-__global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_blr[8][kBlrH * kBlrRow];
+#ifndef MCS_DESC_WAVES
+#define MCS_DESC_WAVES 4
+#endif
+constexpr int kDescWaves = MCS_DESC_WAVES;   // waves per workgroup (the tables are staged once per workgroup)
+__global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_blr[2 * kDescWaves][kBlrH * kBlrRow];
   // the IC weight tables and the packed pattern, staged once per workgroup: read per lane at
   // lane-dependent indices, from constant memory they were L2 round trips inside the compute
   // (one per test round) instead of LDS reads
@@ -191,15 +195,15 @@ __global__ __launch_bounds__(256) void k_orient_desc(DescArgs a) {
   const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
   int f, item;
   const int pairs = (a.sel_per_frame + 1) / 2;
-  if (!xcd_frame_map(blockIdx.x, a.nframes, (pairs + 3) / 4, &f, &item)) return;
-  for (int i = threadIdx.x; i < kRawH * kRawW; i += 256) {
+  if (!xcd_frame_map(blockIdx.x, a.nframes, (pairs + kDescWaves - 1) / kDescWaves, &f, &item)) return;
+  for (int i = threadIdx.x; i < kRawH * kRawW; i += 64 * kDescWaves) {
     s_icw[0][i] = c_icw[0][i];
     s_icw[1][i] = c_icw[1][i];
   }
-  for (int i = threadIdx.x; i < 512; i += 256) s_pat[i] = c_pattern_i8[i];
+  for (int i = threadIdx.x; i < 512; i += 64 * kDescWaves) s_pat[i] = c_pattern_i8[i];
   __syncthreads();
   // even j0: both keypoints on one level (every level's sel_off is even, build_plan)
-  const int j0 = 2 * (item * 4 + wv);
+  const int j0 = 2 * (item * kDescWaves + wv);
   if (j0 >= a.sel_per_frame) return;
   int l = 0;
   while (l + 1 < a.nlevels && j0 >= a.lv[l + 1].sel_off) l++;
@@ -531,8 +535,8 @@ __global__ __launch_bounds__(256) void k_dbrief(DescArgs a, int wave_lds) {
 
 void launch_orient_desc(const DescArgs& a, hipStream_t st) {
   if (a.mode == 0) {
-    const unsigned g = xcd_grid(a.nframes, ((a.sel_per_frame + 1) / 2 + 3) / 4);
-    hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(256), 0, st, a);
+    const unsigned g = xcd_grid(a.nframes, ((a.sel_per_frame + 1) / 2 + kDescWaves - 1) / kDescWaves);
+    hipLaunchKernelGGL(k_orient_desc, dim3(g), dim3(64 * kDescWaves), 0, st, a);
     return;
   }
   const int npts = 16 * a.desc_size;
