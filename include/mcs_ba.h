@@ -263,6 +263,12 @@ int mcs_ba_check_structure(mcs_ba_ctx* c, const mcs_ba_problem* p, const uint8_t
  * (the replay stops when the optimisation is done). */
 int mcs_ba_lm_replay(int32_t device, const mcs_ba_options* o, const double* in3, const double* trials,
                      int32_t n, double* out, int32_t* n_out);
+/* Test hook: the per-landmark block of BlockSolver::solve (block_solver.hpp:381-403) through the
+ * product's device helpers -- Dinv = (H + lambda I).inverse() in Eigen 3.2.10's fixed 3x3 order,
+ * db = Dinv b, Y = Hpl Dinv -- for n independent (H[9], b[3], Hpl[18]) inputs, row-major.  Out:
+ * Dinv[n][9], db[n][3], Y[n][18].  Pinned by tests/golden/g2o_schur.npz. */
+int mcs_ba_point_block_eval(int32_t device, const double* H, double lambda, const double* b, const double* hpl,
+                            int32_t n, double* Dinv, double* db, double* Y);
 /* Test hook: the product's robust kernel (RobustKernelHuber::robustify,
  * robust_kernel_impl.cpp:78-91, delta^2 held as float as robust_kernel_impl.h:84 declares it) on
  * n squared errors: rho0 = rho(e), rho1 = rho'(e). */

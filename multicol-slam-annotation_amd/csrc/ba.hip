@@ -677,31 +677,57 @@ __device__ __forceinline__ double quad_sum(double v) {
   v += __shfl_xor(v, 2);
   return v;
 }
-// D = Hll + lambda I -> D^-1 by cofactors (k_point_trial and k_build_trial: identical bits)
-__device__ __forceinline__ void dinv_of(const double* H, double lam, double (&Di)[9]) {
-  double D[9];
-  for (int k = 0; k < 9; k++) D[k] = H[k];
-  D[0] += lam; D[4] += lam; D[8] += lam;
-  const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8], c02 = D[3] * D[7] - D[4] * D[6];
-  const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
+// D = Hll + lambda I -> Dinv = D.inverse() as the reference's Eigen 3.2.10 computes a fixed
+// 3x3 inverse (ThirdParty/Eigen/Eigen/src/LU/Inverse.h:117-159): cofactor(i, j) =
+// m(i1, j1) m(i2, j2) - m(i1, j2) m(i2, j1) with i1 = i+1, i2 = i+2, j1 = j+1, j2 = j+2 (mod 3);
+// det = the column-0 cofactors times column 0, summed by redux_novec_unroller (Redux.h:77-106:
+// a 3-vector of Matrix<double,3,1> is not packet-aligned in 3.2, so c0 + (c1 + c2)); row 0 of
+// the inverse = the column-0 cofactors, entry (r, c) otherwise = cofactor(c, r), each times
+// 1 / det.  Pinned by tests/golden/g2o_schur.npz.  (k_point_trial and k_build_trial share it.)
+__host__ __device__ __forceinline__ void dinv_of(const double* H, double lam, double (&Di)[9]) {
+  double m[9];
+  for (int k = 0; k < 9; k++) m[k] = H[k];
+  m[0] += lam; m[4] += lam; m[8] += lam;
+  auto cof = [&](int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[3 * i1 + j1] * m[3 * i2 + j2] - m[3 * i1 + j2] * m[3 * i2 + j1];
+  };
+  const double k0 = cof(0, 0), k1 = cof(1, 0), k2 = cof(2, 0);
+  const double det = k0 * m[0] + (k1 * m[3] + k2 * m[6]);
   const double id = 1.0 / det;
-  Di[0] = c00 * id; Di[3] = c01 * id; Di[6] = c02 * id;
-  Di[1] = (D[2] * D[7] - D[1] * D[8]) * id;
-  Di[4] = (D[0] * D[8] - D[2] * D[6]) * id;
-  Di[7] = (D[1] * D[6] - D[0] * D[7]) * id;
-  Di[2] = (D[1] * D[5] - D[2] * D[4]) * id;
-  Di[5] = (D[2] * D[3] - D[0] * D[5]) * id;
-  Di[8] = (D[0] * D[4] - D[1] * D[3]) * id;
+  Di[0] = k0 * id; Di[1] = k1 * id; Di[2] = k2 * id;
+  Di[3] = cof(0, 1) * id; Di[4] = cof(1, 1) * id; Di[5] = cof(2, 1) * id;
+  Di[6] = cof(0, 2) * id; Di[7] = cof(1, 2) * id; Di[8] = cof(2, 2) * id;
 }
-// Y_e = Hpl_e Dinv of one (point, edge) entry whose pose is active
-__device__ __forceinline__ void y_of(const Dev& d, int e, const double (&Di)[9]) {
-  const double* B = d.hpl + 18 * e;
+// db = Dinv * b_l (CoeffBasedProduct, CoeffBasedProduct.h:240-258: k ascending)
+__host__ __device__ __forceinline__ void db_of(const double (&Di)[9], const double* b, double* db) {
+  for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
+}
+// Y = Hpl * Dinv (BDinv = (*Bi) * Dinv, block_solver.hpp:403), same product order
+__host__ __device__ __forceinline__ void ybl_of(const double* B, const double (&Di)[9], double* Y) {
   double bb[18];
   for (int k = 0; k < 18; k++) bb[k] = B[k];
   for (int a = 0; a < 6; a++)
     for (int c = 0; c < 3; c++)
-      d.y[18 * e + 3 * a + c] = bb[3 * a] * Di[c] + bb[3 * a + 1] * Di[3 + c] + bb[3 * a + 2] * Di[6 + c];
+      Y[3 * a + c] = bb[3 * a] * Di[c] + bb[3 * a + 1] * Di[3 + c] + bb[3 * a + 2] * Di[6 + c];
 }
+// Y_e = Hpl_e Dinv of one (point, edge) entry whose pose is active
+__device__ __forceinline__ void y_of(const Dev& d, int e, const double (&Di)[9]) {
+  ybl_of(d.hpl + 18 * e, Di, d.y + 18 * e);
+}
+
+// per landmark: Dinv, db and one edge's Y from the production helpers (mcs_ba_point_block_eval)
+__global__ void k_point_block_eval(const double* H, double lam, const double* b, const double* hpl, int n,
+                                   double* Dinv, double* db, double* Y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double Di[9];
+  dinv_of(H + 9 * i, lam, Di);
+  for (int k = 0; k < 9; k++) Dinv[9 * i + k] = Di[k];
+  db_of(Di, b + 3 * i, db + 3 * i);
+  ybl_of(hpl + 18 * i, Di, Y + 18 * i);
+}
+
 
 // TRIAL (k_build_trial): the same quad then carries k_point_trial's point part -- Dinv, db and
 // the Y of the point's edges -- from the H and b it holds (LIN: just built; otherwise the
@@ -743,7 +769,7 @@ __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool 
   dinv_of(H, lam_of(d), Di);
   if (sub == 0) {
     for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
-    for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
+    db_of(Di, b, d.db + 3 * l);
   }
   for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
     const int e = d.pt_edges[q];
@@ -867,8 +893,7 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
   dinv_of(d.Hll + 9 * l, lam_of(d), Di);
   if (first) {
     for (int k = 0; k < 9; k++) d.Dinv[9 * l + k] = Di[k];
-    const double* b = d.bl + 3 * l;
-    for (int a = 0; a < 3; a++) d.db[3 * l + a] = Di[3 * a] * b[0] + Di[3 * a + 1] * b[1] + Di[3 * a + 2] * b[2];
+    db_of(Di, d.bl + 3 * l, d.db + 3 * l);
   }
   if (pose_act) y_of(d, e, Di);
 }
@@ -2502,6 +2527,41 @@ int mcs_ba_huber_eval(int32_t device, const double* e, int32_t n, double delta, 
   }
   for (void* q : {(void*)de, (void*)d0, (void*)d1})
     if (q) (void)hipFree(q);
+  return rc;
+}
+
+int mcs_ba_point_block_eval(int32_t device, const double* H, double lambda, const double* b, const double* hpl,
+                            int32_t n, double* Dinv, double* db, double* Y) {
+  if (n < 0 || (n > 0 && (!H || !b || !hpl || !Dinv || !db || !Y))) {
+    set_error("point_block_eval: null argument or n < 0");
+    return MCS_ERR_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    set_error("no HIP device visible (no CPU fallback)");
+    return MCS_ERR_NO_DEVICE;
+  }
+  if (n == 0) return MCS_OK;
+  MCS_HIP_CHECK(hipSetDevice(device));
+  double* dv = nullptr;
+  const size_t N = (size_t)n, tot = N * (9 + 3 + 18 + 9 + 3 + 18);
+  int rc = MCS_OK;
+  auto chk = [&](hipError_t x, const char* w) { if (x != hipSuccess && rc == MCS_OK) { set_hip_error(x, w, __FILE__, __LINE__); rc = MCS_ERR_HIP; } };
+  chk(hipMalloc(&dv, tot * 8), "malloc");
+  if (rc == MCS_OK) {
+    double *dH = dv, *dB = dH + 9 * N, *dP = dB + 3 * N, *dDi = dP + 18 * N, *dDb = dDi + 9 * N, *dY = dDb + 3 * N;
+    chk(hipMemcpy(dH, H, 9 * N * 8, hipMemcpyHostToDevice), "h2d");
+    chk(hipMemcpy(dB, b, 3 * N * 8, hipMemcpyHostToDevice), "h2d");
+    chk(hipMemcpy(dP, hpl, 18 * N * 8, hipMemcpyHostToDevice), "h2d");
+    if (rc == MCS_OK)
+      hipLaunchKernelGGL(k_point_block_eval, dim3((n + 255) / 256), dim3(256), 0, 0, (const double*)dH, lambda,
+                         (const double*)dB, (const double*)dP, n, dDi, dDb, dY);
+    chk(hipGetLastError(), "launch");
+    chk(hipMemcpy(Dinv, dDi, 9 * N * 8, hipMemcpyDeviceToHost), "d2h");
+    chk(hipMemcpy(db, dDb, 3 * N * 8, hipMemcpyDeviceToHost), "d2h");
+    chk(hipMemcpy(Y, dY, 18 * N * 8, hipMemcpyDeviceToHost), "d2h");
+  }
+  if (dv) (void)hipFree(dv);
   return rc;
 }
 

@@ -140,6 +140,7 @@ SIGNATURES = {
     "mcs_search_for_triangulation_raw": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
     "mcs_search_for_triangulation_raw_masked": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P]),
     "mcs_compute_e_rig": (ctypes.c_int, [_P, _P, _P, _I32, _P]),
+    "mcs_ba_point_block_eval": (ctypes.c_int, [_I32, _P, ctypes.c_double, _P, _P, _I32, _P, _P, _P]),
     "mcs_tri_workspace_create": (ctypes.c_int, [_I32, _I32, _I32, _P]),
     "mcs_tri_workspace_destroy": (None, [_P]),
     "mcs_search_for_triangulation_raw_device": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _I32, _I32, ctypes.c_double, _P, _P, _P]),

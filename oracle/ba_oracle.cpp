@@ -369,19 +369,19 @@ struct Graph {
       double D[9];
       for (int k = 0; k < 9; k++) D[k] = Hll[9 * l + k];
       D[0] += lam; D[4] += lam; D[8] += lam;
-      // Eigen 3x3 inverse via cofactors
-      const double c00 = D[4] * D[8] - D[5] * D[7], c01 = D[5] * D[6] - D[3] * D[8],
-                   c02 = D[3] * D[7] - D[4] * D[6];
-      const double det = D[0] * c00 + D[1] * c01 + D[2] * c02;
+      // Dinv = D.inverse(): Eigen 3.2.10 fixed 3x3 (ThirdParty/Eigen/Eigen/src/LU/Inverse.h:117-159),
+      // det summed c0 + (c1 + c2) (Redux.h:77-106, no packet access for 3-vectors)
+      auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return D[3 * i1 + j1] * D[3 * i2 + j2] - D[3 * i1 + j2] * D[3 * i2 + j1];
+      };
+      const double k0 = cof(0, 0), k1 = cof(1, 0), k2 = cof(2, 0);
+      const double det = k0 * D[0] + (k1 * D[3] + k2 * D[6]);
       const double id = 1.0 / det;
       double* Di = &Dinv[9 * l];
-      Di[0] = c00 * id; Di[3] = c01 * id; Di[6] = c02 * id;
-      Di[1] = (D[2] * D[7] - D[1] * D[8]) * id;
-      Di[4] = (D[0] * D[8] - D[2] * D[6]) * id;
-      Di[7] = (D[1] * D[6] - D[0] * D[7]) * id;
-      Di[2] = (D[1] * D[5] - D[2] * D[4]) * id;
-      Di[5] = (D[2] * D[3] - D[0] * D[5]) * id;
-      Di[8] = (D[0] * D[4] - D[1] * D[3]) * id;
+      Di[0] = k0 * id; Di[1] = k1 * id; Di[2] = k2 * id;
+      Di[3] = cof(0, 1) * id; Di[4] = cof(1, 1) * id; Di[5] = cof(2, 1) * id;
+      Di[6] = cof(0, 2) * id; Di[7] = cof(1, 2) * id; Di[8] = cof(2, 2) * id;
       double db[3];
       for (int a = 0; a < 3; a++) db[a] = Di[3 * a] * bl[3 * l] + Di[3 * a + 1] * bl[3 * l + 1] + Di[3 * a + 2] * bl[3 * l + 2];
       for (int e1 : pe[l]) {

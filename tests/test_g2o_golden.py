@@ -91,3 +91,47 @@ def test_gpu_huber_matches_reference(gpu, gold):
         assert L.mcs_ba_huber_eval(0, ba._p(ee), len(ee), float(delta), ba._p(r0), ba._p(r1)) == 0
         assert np.array_equal(r0, gold["huber_rho0"][sel]), delta
         assert np.array_equal(r1, gold["huber_rho1"][sel]), delta
+
+
+SCHUR = os.path.join(HERE, "golden", "g2o_schur.npz")
+
+
+def test_schur_golden_structure():
+    """g2o_schur.npz: the per-landmark block of BlockSolver::solve (block_solver.hpp:381-403)
+    in Eigen 3.2.10's order (tests/golden/gen_g2o_schur.py).  The cofactor table parsed from
+    Eigen's Inverse.h: row 0 holds the column-0 cofactors, entry (r, c) otherwise cofactor(c, r);
+    and the determinant's c0 + (c1 + c2) differs from (c0 + c1) + c2 in some blocks, so the
+    fixture does tell the two orders apart."""
+    g = np.load(SCHUR)
+    assert sorted(map(tuple, g["table"].tolist())) == [(r, c, c, r) for r in range(3) for c in range(3)]
+    H, lam = g["H"].reshape(-1, 3, 3), float(g["lam"])
+    differ = 0
+    for t in range(len(H)):
+        m = H[t].tolist()
+        for i in range(3):
+            m[i][i] += lam
+        cof = lambda i, j: (m[(i + 1) % 3][(j + 1) % 3] * m[(i + 2) % 3][(j + 2) % 3]
+                            - m[(i + 1) % 3][(j + 2) % 3] * m[(i + 2) % 3][(j + 1) % 3])
+        p = [cof(k, 0) * m[k][0] for k in range(3)]
+        differ += (p[0] + (p[1] + p[2])) != ((p[0] + p[1]) + p[2])
+        assert g["Dinv"][t, 0] == cof(0, 0) * (1.0 / (p[0] + (p[1] + p[2])))
+    assert differ > 10
+
+
+@pytest.mark.gpu
+def test_gpu_point_block_matches_reference_order(gpu):
+    """The product's device Dinv / db / Y helpers (the ones k_build_trial and k_point_trial run)
+    reproduce the per-landmark block of the reference's BlockSolver::solve bit for bit."""
+    import mcs_amd
+    from mcs_amd import ba
+    g = np.load(SCHUR)
+    n = len(g["H"])
+    Dinv, db, Y = np.zeros((n, 9)), np.zeros((n, 3)), np.zeros((n, 18))
+    rc = mcs_amd.lib().mcs_ba_point_block_eval(0, ba._p(np.ascontiguousarray(g["H"])), float(g["lam"]),
+                                               ba._p(np.ascontiguousarray(g["b"])),
+                                               ba._p(np.ascontiguousarray(g["hpl"])), n, ba._p(Dinv),
+                                               ba._p(db), ba._p(Y))
+    assert rc == 0
+    assert np.array_equal(Dinv, g["Dinv"])
+    assert np.array_equal(db, g["db"])
+    assert np.array_equal(Y, g["Y"])
