@@ -83,6 +83,14 @@ def sq_issue():
                           ("k_orient_desc", "orient_desc"), ("k_top2_mfma32<true>", "match_mfma")):
             if name in k:
                 out[key + "_valu_util"] = k[name]["valu_util"]
+        # VALU lane-operations per pixel (tools/valu_per_pixel.py on the SQ pass A counters)
+        vp = os.path.join(ROOT, "profiles", "valu_per_pixel.json")
+        if os.path.exists(vp):
+            v = json.load(open(vp))
+            for name, key in (("k_pyr_rows<true, 2>", "pyramid"), ("k_fast_rows<16>", "fast")):
+                if name in v:
+                    out[key + "_valu_lane_ops_per_pixel"] = v[name]["valu_lane_ops_per_pixel"]
+            out["valu_per_pixel_source"] = v.get("source")
         return {"issue": out}
     except (KeyError, ValueError):
         return {}

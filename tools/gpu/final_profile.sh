@@ -8,7 +8,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-r02}
 O=gpurun_out/fp_$TAG; mkdir -p $O
-ARGS="--steps 5 --warmup 1 --no-cpu-baseline --ba-calls 0 --gba-calls 0 --d-multiframes 0 --bow-reps 0 --latency-reps 0"
+ARGS="--steps 5 --warmup 1 --no-cpu-baseline --ba-calls 0 --gba-calls 0 --d-multiframes 0 --bow-reps 0 --latency-reps 0 --tri-reps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py $ARGS > $O/bench_stats.json 2> $O/stats.err || { echo "stats pass failed"; tail -5 $O/stats.err; exit 1; }
 S=$(find $O/stats -name '*kernel_stats.csv' | head -1); cp "$S" $O/kernel_stats.csv
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py $ARGS > /dev/null 2> $O/fetch.err || { echo "fetch pass failed"; tail -5 $O/fetch.err; exit 1; }
@@ -21,6 +21,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_AC
 A=$(find $O/sqa -name '*counter_collection.csv' | head -1)
 B=$(find $O/sqb -name '*counter_collection.csv' | head -1)
 python3 tools/sq_summary.py "$A" > $O/sq_summary.txt
+python3 tools/valu_per_pixel.py "$A" 513 > $O/valu_per_pixel.json
 python3 tools/sq_summary.py --all --json=$O/sq_issue.json "$B" > $O/sq_summary_b.txt
 head -14 $O/kernel_stats.csv | cut -d, -f1-4 | cut -c1-120
 python3 -c "import json; d=json.load(open('$O/pmc_traffic.json')); print({k: v for k, v in d.items() if k != 'kernels'})"
