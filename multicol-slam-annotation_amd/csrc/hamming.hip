@@ -273,7 +273,15 @@ __global__ __launch_bounds__(256, MCS_TOP2_MINB) void k_top2_mfma32(
     for (int st = 0; st < 2; st++) {
       if (st * 32 >= ntile) break;
       const int tb = t0 + st * 32 + 4 * h;
-      v16i acc0 = {0}, acc1 = {0};
+      // KEYED: both accumulators start from the rows' key offsets (2^20 + tile base + the row's
+      // offset), one set shared by the two query groups, so the MFMA result is the key itself
+      v16i cinit = {0};
+      if (KEYED) {
+        const uint32_t tbk = (uint32_t)tb + (1u << 20);
+#pragma unroll
+        for (int r = 0; r < 16; r++) cinit[r] = (int)(tbk + (uint32_t)((r & 3) + 8 * (r >> 2)));
+      }
+      v16i acc0 = cinit, acc1 = cinit;
       const uint8_t* arow = s_t + (st * 32 + col) * kMfPitch + 16 * h;
 #pragma unroll
       for (int s = 0; s < 8; s++) {
@@ -283,12 +291,11 @@ __global__ __launch_bounds__(256, MCS_TOP2_MINB) void k_top2_mfma32(
       }
       const bool full = st * 32 + 32 <= ntile;
       if (KEYED) {
-        const uint32_t tbk = (uint32_t)tb + (1u << 20);
         uint32_t key0[16], key1[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-          key0[r] = (uint32_t)acc0[r] + tbk + (uint32_t)((r & 3) + 8 * (r >> 2));
-          key1[r] = (uint32_t)acc1[r] + tbk + (uint32_t)((r & 3) + 8 * (r >> 2));
+          key0[r] = (uint32_t)acc0[r];
+          key1[r] = (uint32_t)acc1[r];
         }
         if (!full) {   // the last, partial tile (a scalar branch: no selects in full tiles)
           asm volatile("" ::: "memory");
