@@ -158,10 +158,20 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
         kept++;
       }
     }
-    int P, K, E2;
-    const int pushBase = dev::block_excl_scan<kOctThreads>(pushes, s_scan, &P);
-    const int keptBase = dev::block_excl_scan<kOctThreads>(kept, s_scan, &K);
-    dev::block_excl_scan<kOctThreads>(expandKids, s_scan, &E2);
+    int P, K, E2, pushBase, keptBase;
+    if (MAXL <= 512) {
+      // one scan of the three counts packed in 10-bit fields: each total is <= MAXL (the list
+      // a round builds, P + K, stays <= N <= MAXL, and E2 <= P), so no field carries into the
+      // next (3 barriers and one wave scan instead of three of each)
+      int T3;
+      const int ex = dev::block_excl_scan<kOctThreads>(pushes | (kept << 10) | (expandKids << 20), s_scan, &T3);
+      pushBase = ex & 0x3FF; keptBase = (ex >> 10) & 0x3FF;
+      P = T3 & 0x3FF; K = (T3 >> 10) & 0x3FF; E2 = (T3 >> 20) & 0x3FF;
+    } else {
+      pushBase = dev::block_excl_scan<kOctThreads>(pushes, s_scan, &P);
+      keptBase = dev::block_excl_scan<kOctThreads>(kept, s_scan, &K);
+      dev::block_excl_scan<kOctThreads>(expandKids, s_scan, &E2);
+    }
     {
       int s = pushBase, kp = keptBase;
       for (int j = 0; j < kOctPer; j++) {
