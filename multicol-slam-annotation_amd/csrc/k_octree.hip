@@ -55,9 +55,12 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
 
   // ---- 1. gather candidates of this level in reference (cell, row, col) order
   int n = 0;
+  // the cells' slot offsets go to LDS beside the prefix (ccnt is free until the main loop), so
+  // a candidate's gather below is one global load instead of two dependent ones
   for (int base = 0; base < nc; base += kOctThreads) {
     const int i = base + tid;
     const int v = i < nc ? counts[i] : 0;
+    if (i < nc) ccnt[i] = a.cells[L.cell_begin + i].slot_off;
     int tot;
     const int ex = dev::block_excl_scan<kOctThreads>(v, s_scan, &tot);
     if (i < nc) s_pref[i] = n + ex;
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       else hi = mid;
     }
     const int c = lo - 1;
-    const uint32_t v = slots[a.cells[L.cell_begin + c].slot_off + (i - s_pref[c])];
+    const uint32_t v = slots[ccnt[c] + (i - s_pref[c])];
     cand[i] = v;
     if (inl) gcand[i] = v;
   }
