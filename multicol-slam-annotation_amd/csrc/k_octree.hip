@@ -42,6 +42,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   __shared__ int ccnt[MAXL * 4];      // child counts; reused for best keys
   __shared__ int16_t npos[MAXL * 4];  // new position per (node, child); kept uses slot 0
   __shared__ uint8_t nflag[MAXL];     // expanding / in-E / processed flags
+  __shared__ uint8_t nflag2[MAXL];    // the main loop's next-round flags
   __shared__ int s_var[8];
   __shared__ uint32_t s_cand[CAP > 0 ? CAP : 1];
   __shared__ int32_t s_cnode[CAP > 0 ? CAP : 1];
@@ -126,32 +127,40 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   __syncthreads();
 
   // ---- 3. main subdivision loop (:692-837)
+  // When a round is followed by another main-loop round, its candidate update and the next
+  // round's child counting are one pass (the next round's flags and cleared counts are set
+  // between them): one pass over the candidates and one barrier fewer per round.
   bool finished = false;
   int lastPushBase = 0;
+  uint8_t* fl = nflag;     // this round's expanding flags
+  uint8_t* fln = nflag2;   // the next round's, set ahead
+  bool counted = false;    // this round's child counts came from the previous round's pass
   while (true) {
     const int prevSize = Lsz;
     const int nxt = cur ^ 1;
-    for (int i = tid; i < Lsz; i += kOctThreads) {
-      nflag[i] = ncnt[cur][i] > 1;
-      ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
-    }
-    __syncthreads();
-    _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
-      const int nd = cnode[k];
-      if (nflag[nd]) {
-        const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
-        const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
-        atomicAdd(&ccnt[4 * nd + oct_quad(cand[k], midx, midy)], 1);
+    if (!counted) {
+      for (int i = tid; i < Lsz; i += kOctThreads) {
+        fl[i] = ncnt[cur][i] > 1;
+        ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
       }
+      __syncthreads();
+      _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+        const int nd = cnode[k];
+        if (fl[nd]) {
+          const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+          const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+          atomicAdd(&ccnt[4 * nd + oct_quad(cand[k], midx, midy)], 1);
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
     // per thread: kOctPer consecutive nodes -> pushes (expanding) / kept
     int pushes = 0, kept = 0, expandKids = 0;
     const int i0 = tid * kOctPer;
     for (int j = 0; j < kOctPer; j++) {
       const int i = i0 + j;
       if (i >= Lsz) break;
-      if (nflag[i]) {
+      if (fl[i]) {
         for (int q = 0; q < 4; q++) {
           const int cq = ccnt[4 * i + q];
           pushes += cq > 0;
@@ -180,7 +189,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       for (int j = 0; j < kOctPer; j++) {
         const int i = i0 + j;
         if (i >= Lsz) break;
-        if (nflag[i]) {
+        if (fl[i]) {
           const int x0 = nx0[cur][i], y0 = ny0[cur][i], x1 = nx1[cur][i], y1 = ny1[cur][i];
           const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
           for (int q = 0; q < 4; q++) {
@@ -208,23 +217,56 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       }
     }
     __syncthreads();
-    _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
-      const int nd = cnode[k];
-      if (nflag[nd]) {
-        const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
-        const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
-        cnode[k] = npos[4 * nd + oct_quad(cand[k], midx, midy)];
-      } else {
-        cnode[k] = npos[4 * nd];
+    const int Lnew = P + K;
+    // the loop's own exit tests (:826-836), known as soon as the round's totals are
+    const bool more = !(Lnew >= N || Lnew == prevSize) && !(Lnew + 3 * E2 > N);
+    if (more) {
+      for (int i = tid; i < Lnew; i += kOctThreads) {
+        fln[i] = ncnt[nxt][i] > 1;
+        ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
+      }
+      __syncthreads();
+      _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+        const int nd = cnode[k];
+        const uint32_t pk = cand[k];
+        int nn;
+        if (fl[nd]) {
+          const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+          const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+          nn = npos[4 * nd + oct_quad(pk, midx, midy)];
+        } else {
+          nn = npos[4 * nd];
+        }
+        cnode[k] = nn;
+        if (fln[nn]) {
+          const int midx = nx0[nxt][nn] + ((nx1[nxt][nn] - nx0[nxt][nn] + 1) >> 1);
+          const int midy = ny0[nxt][nn] + ((ny1[nxt][nn] - ny0[nxt][nn] + 1) >> 1);
+          atomicAdd(&ccnt[4 * nn + oct_quad(pk, midx, midy)], 1);
+        }
+      }
+    } else {
+      _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+        const int nd = cnode[k];
+        if (fl[nd]) {
+          const int midx = nx0[cur][nd] + ((nx1[cur][nd] - nx0[cur][nd] + 1) >> 1);
+          const int midy = ny0[cur][nd] + ((ny1[cur][nd] - ny0[cur][nd] + 1) >> 1);
+          cnode[k] = npos[4 * nd + oct_quad(cand[k], midx, midy)];
+        } else {
+          cnode[k] = npos[4 * nd];
+        }
       }
     }
     lastPushBase = seqc;
     seqc += P;
-    Lsz = P + K;
+    Lsz = Lnew;
     cur = nxt;
     __syncthreads();
-    if (Lsz >= N || Lsz == prevSize) { finished = true; break; }
-    if (Lsz + 3 * E2 > N) break;  // -> final phase
+    if (!more) {
+      if (Lsz >= N || Lsz == prevSize) finished = true;
+      break;   // finished, or -> final phase
+    }
+    uint8_t* const t = fl; fl = fln; fln = t;
+    counted = true;
   }
 
   // ---- 4. final phase (:771-836): divide largest nodes first until >= N
