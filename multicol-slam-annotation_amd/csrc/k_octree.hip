@@ -120,10 +120,25 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
     s_var[0] = m;
   }
   __syncthreads();
-  _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) cnode[k] = npos[cnode[k]];
   cur = 1;
   int Lsz = s_var[0];
   int seqc = nIni;
+  // the first round's flags and cleared counts, then the remap to the kept initial nodes and
+  // that round's child counting in one pass
+  for (int i = tid; i < Lsz; i += kOctThreads) {
+    nflag[i] = ncnt[1][i] > 1;
+    ccnt[4 * i] = ccnt[4 * i + 1] = ccnt[4 * i + 2] = ccnt[4 * i + 3] = 0;
+  }
+  __syncthreads();
+  _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
+    const int nn = npos[cnode[k]];
+    cnode[k] = nn;
+    if (nflag[nn]) {
+      const int midx = nx0[1][nn] + ((nx1[1][nn] - nx0[1][nn] + 1) >> 1);
+      const int midy = ny0[1][nn] + ((ny1[1][nn] - ny0[1][nn] + 1) >> 1);
+      atomicAdd(&ccnt[4 * nn + oct_quad(cand[k], midx, midy)], 1);
+    }
+  }
   __syncthreads();
 
   // ---- 3. main subdivision loop (:692-837)
@@ -134,7 +149,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   int lastPushBase = 0;
   uint8_t* fl = nflag;     // this round's expanding flags
   uint8_t* fln = nflag2;   // the next round's, set ahead
-  bool counted = false;    // this round's child counts came from the previous round's pass
+  bool counted = true;     // this round's child counts came from the previous pass
   while (true) {
     const int prevSize = Lsz;
     const int nxt = cur ^ 1;
