@@ -315,22 +315,31 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
           }
         }
       }
-      for (int i = M + tid; i < M2; i += kOctThreads) keys[i] = 0ull;
       __syncthreads();
-      // bitonic sort, descending
-      for (int k = 2; k <= M2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = tid; i < M2; i += kOctThreads) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const unsigned long long ki = keys[i], kj = keys[ixj];
-              const bool desc = (i & k) == 0;
-              if (desc ? (ki < kj) : (ki > kj)) { keys[i] = kj; keys[ixj] = ki; }
-            }
+      // descending order by rank counting (the keys are distinct: they end in the node index):
+      // two barriers instead of the bitonic network's log2(M)^2 / 2
+      (void)M2;
+      {
+        unsigned long long mk[kOctPer];
+        int rk[kOctPer];
+#pragma unroll
+        for (int t = 0; t < kOctPer; t++) {
+          const int i = tid + t * kOctThreads;
+          rk[t] = -1;
+          if (i < M) {
+            const unsigned long long kv = keys[i];
+            int r = 0;
+            for (int j = 0; j < M; j++) r += keys[j] > kv;
+            mk[t] = kv;
+            rk[t] = r;
           }
-          __syncthreads();
         }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < kOctPer; t++)
+          if (rk[t] >= 0) keys[rk[t]] = mk[t];
       }
+      __syncthreads();
       // child counts of E nodes
       _Pragma("unroll 4") for (int k = tid; k < n; k += kOctThreads) {
         const int nd = cnode[k];
