@@ -382,20 +382,53 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       }
       __syncthreads();
       const int Mp = s_var[1];
-      // pushes of processed sorted nodes (in sorted order, children n1..n4)
-      int mykids = 0;
-      for (int jj = 0; jj < kOctPer; jj++)
-        if (j0 + jj < Mp) mykids += kl[jj];
-      int Pn;
-      int kbase = dev::block_excl_scan<kOctThreads>(mykids, s_scan, &Pn);
-      // mark processed (nflag = 2) and place children
+      int Pn, kbase, kb, Kn;
+      if (MAXL <= 512) {
+        // mark the processed nodes first, so that the children's and the kept nodes' places
+        // come from one packed scan (10-bit fields: both totals stay <= MAXL)
+        for (int jj = 0; jj < kOctPer; jj++) {
+          const int j = j0 + jj;
+          if (j >= Mp) break;
+          nflag[(int)(keys[j] & 0xFFF)] = 2;
+        }
+        __syncthreads();
+        int mykids = 0, kept = 0;
+        for (int jj = 0; jj < kOctPer; jj++)
+          if (j0 + jj < Mp) mykids += kl[jj];
+        for (int j = 0; j < kOctPer; j++) {
+          const int i = i0 + j;
+          if (i < Lsz && nflag[i] != 2) kept++;
+        }
+        int T2;
+        const int ex = dev::block_excl_scan<kOctThreads>(mykids | (kept << 10), s_scan, &T2);
+        kbase = ex & 0x3FF; kb = ex >> 10;
+        Pn = T2 & 0x3FF; Kn = T2 >> 10;
+      } else {
+        // pushes of processed sorted nodes (in sorted order, children n1..n4)
+        int mykids = 0;
+        for (int jj = 0; jj < kOctPer; jj++)
+          if (j0 + jj < Mp) mykids += kl[jj];
+        kbase = dev::block_excl_scan<kOctThreads>(mykids, s_scan, &Pn);
+        for (int jj = 0; jj < kOctPer; jj++) {
+          const int j = j0 + jj;
+          if (j >= Mp) break;
+          nflag[(int)(keys[j] & 0xFFF)] = 2;
+        }
+        __syncthreads();
+        int kept = 0;
+        for (int j = 0; j < kOctPer; j++) {
+          const int i = i0 + j;
+          if (i < Lsz && nflag[i] != 2) kept++;
+        }
+        kb = dev::block_excl_scan<kOctThreads>(kept, s_scan, &Kn);
+      }
+      // place the processed nodes' children (sorted order, n1..n4) and the kept nodes after them
       {
         int s = kbase;
         for (int jj = 0; jj < kOctPer; jj++) {
           const int j = j0 + jj;
           if (j >= Mp) break;
           const int nd = (int)(keys[j] & 0xFFF);
-          nflag[nd] = 2;
           const int x0 = nx0[cur][nd], y0 = ny0[cur][nd], x1 = nx1[cur][nd], y1 = ny1[cur][nd];
           const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
           for (int q = 0; q < 4; q++) {
@@ -413,15 +446,6 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
           }
         }
       }
-      __syncthreads();
-      // remaining (unprocessed) list nodes keep their order after the pushes
-      int kept = 0;
-      for (int j = 0; j < kOctPer; j++) {
-        const int i = i0 + j;
-        if (i < Lsz && nflag[i] != 2) kept++;
-      }
-      int Kn;
-      int kb = dev::block_excl_scan<kOctThreads>(kept, s_scan, &Kn);
       for (int j = 0; j < kOctPer; j++) {
         const int i = i0 + j;
         if (i < Lsz && nflag[i] != 2) {
