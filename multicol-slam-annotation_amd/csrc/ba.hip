@@ -977,8 +977,13 @@ __global__ __launch_bounds__(256) void k_schur(Dev d) {
   double acc[42];
 #pragma unroll
   for (int v = 0; v < 42; v++) acc[v] = 0.0;
-  for (int q = q0 + lane; q < q1; q += 64) {
-    const uint2 pq = d.pr[q];
+  // the next pair's index is loaded ahead, so each pair costs one dependent round trip (its
+  // rows), not two
+  int q = q0 + lane;
+  uint2 pqn = q < q1 ? d.pr[q] : make_uint2(0u, 0u);
+  for (; q < q1; q += 64) {
+    const uint2 pq = pqn;
+    if (q + 64 < q1) pqn = d.pr[q + 64];
     const double* Y = d.y + 18 * pq.x;
     const double* B = d.hpl + 18 * pq.y;
     double y[18], bb[18];
@@ -1037,8 +1042,20 @@ __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nblk) {
   if (n <= 1) return;
   const int s0 = d.blk_slot0[b];
   double v = 0.0;
-  if (lane < 42)
-    for (int c = 0; c < n; c++) v += d.schur_part[(size_t)(s0 + c) * 42 + lane];
+  if (lane < 42) {
+    // eight slots' loads in flight, then added in chunk order (the same sum, bit for bit, as
+    // one slot at a time, without a dependent round trip per slot)
+    const double* P = d.schur_part + (size_t)s0 * 42 + lane;
+    int c = 0;
+    for (; c + 8 <= n; c += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) t[u] = P[(size_t)(c + u) * 42];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v += t[u];
+    }
+    for (; c < n; c++) v += P[(size_t)c * 42];
+  }
   schur_write(d, d.blk_i[b], d.blk_j[b], lam0, lane, v);
 }
 
