@@ -740,8 +740,7 @@ __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool 
   double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
   if (lin) {
     if (act) {
-      for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
-        const int e = d.pt_edges[q];
+      auto term = [&](int e) {
         const double* jl = d.jl + 6 * e;
         const double w = d.w[e];
         const double we0 = -w * d.err[2 * e], we1 = -w * d.err[2 * e + 1];
@@ -749,6 +748,14 @@ __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool 
           for (int bb = 0; bb < 3; bb++) H[3 * a + bb] += w * (jl[a] * jl[bb] + jl[3 + a] * jl[3 + bb]);
           b[a] += jl[a] * we0 + jl[3 + a] * we1;
         }
+      };
+      // the quad lane's entries q and q + 4 with their index loads together, added in q order
+      const int q1 = d.pt_ptr[l + 1];
+      for (int q = d.pt_ptr[l] + sub; q < q1; q += 8) {
+        const bool two = q + 4 < q1;
+        const int ea = d.pt_edges[q], eb = d.pt_edges[two ? q + 4 : q];
+        term(ea);
+        if (two) term(eb);
       }
     }
 #pragma unroll
@@ -772,8 +779,8 @@ __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool 
     db_of(Di, b, d.db + 3 * l);
   }
   for (int q = d.pt_ptr[l] + sub; q < d.pt_ptr[l + 1]; q += 4) {
-    const int e = d.pt_edges[q];
-    if (d.pose_h[d.e_pose[e]] >= 0) y_of(d, e, Di);
+    // pt_h[q] = pose_h[e_pose[pt_edges[q]]] (host-built): one load instead of a chain of three
+    if (d.pt_h[q] >= 0) y_of(d, d.pt_edges[q], Di);
   }
 }
 
@@ -887,7 +894,7 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
   const int e = d.pt_edges[q];
   const int l = d.point_h[d.e_point[e]];
   const bool first = (q == d.pt_ptr[l]);
-  const bool pose_act = d.pose_h[d.e_pose[e]] >= 0;
+  const bool pose_act = d.pt_h[q] >= 0;
   if (!first && !pose_act) return;
   double Di[9];
   dinv_of(d.Hll + 9 * l, lam_of(d), Di);
@@ -1000,15 +1007,22 @@ __global__ __launch_bounds__(256) void k_schur(Dev d) {
     const int e0 = min(d.ps_ptr[bi] + c * kSchurChunk, d.ps_ptr[bi + 1]);
     const int e1 = min(e0 + kSchurChunk, d.ps_ptr[bi + 1]);
     nact = max(nact, e1 - e0);
-    for (int q = e0 + lane; q < e1; q += 64) {
-      const int e = d.ps_edges[q];
-      const int lh = d.point_h[d.e_point[e]];
-      if (lh < 0) continue;   // fixed point (pose-only BA): no Schur term
+    auto term = [&](int e, int lh) {
+      if (lh < 0) return;   // fixed point (pose-only BA): no Schur term
       const double* B = d.hpl + 18 * e;
       const double* g = d.db + 3 * lh;
       const double g0 = g[0], g1 = g[1], g2 = g[2];
 #pragma unroll
       for (int a = 0; a < 6; a++) acc[36 + a] += B[3 * a] * g0 + B[3 * a + 1] * g1 + B[3 * a + 2] * g2;
+    };
+    // a lane's edges q and q + 64 (the chunk is 2 x 64) with their three-deep index chains
+    // interleaved, then added in q order
+    for (int q = e0 + lane; q < e1; q += 128) {
+      const bool two = q + 64 < e1;
+      const int ea = d.ps_edges[q], eb = d.ps_edges[two ? q + 64 : q];
+      const int la = d.point_h[d.e_point[ea]], lb = d.point_h[d.e_point[eb]];
+      term(ea, la);
+      if (two) term(eb, lb);
     }
   }
   (void)nact;
@@ -1073,7 +1087,7 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
     double c[3] = {0.0, 0.0, 0.0};
     for (int q = d.pt_ptr[k] + sub; q < d.pt_ptr[k + 1]; q += 4) {
       const int e = d.pt_edges[q];
-      const int i1 = d.pose_h[d.e_pose[e]];
+      const int i1 = d.pt_h[q];
       if (i1 < 0) continue;
       const double* B = d.hpl + 18 * e;
       for (int b = 0; b < 3; b++)
