@@ -13,7 +13,10 @@
 namespace mcs {
 namespace ba {
 
-constexpr int kSchurChunk = 128;   // pairs per k_schur wave (config C: 128 beat 32 / 64 / 256)
+#ifndef MCS_SCHUR_CHUNK
+#define MCS_SCHUR_CHUNK 128
+#endif
+constexpr int kSchurChunk = MCS_SCHUR_CHUNK;   // pairs per k_schur wave (config C: 128 beat 32 / 64 / 256)
 
 // host-side structure of one optimize() call (build_structure); owned by the context so its
 // capacity is reused across that context's calls and released with it

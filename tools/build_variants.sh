@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 P=multicol-slam-annotation_amd
-EXTR="extractor.hip k_pyramid.hip k_fast_rows.hip k_octree.hip k_desc.hip extractor_plan.cpp hamming.hip"
+EXTR=${EXTR:-"extractor.hip k_pyramid.hip k_fast_rows.hip k_octree.hip k_desc.hip extractor_plan.cpp hamming.hip"}
 while [ $# -ge 2 ]; do
   NAME=$1; FLAGS=$2; shift 2
   D=$P/lib/var_$NAME; rm -rf $D; mkdir -p $D
