@@ -784,21 +784,56 @@ __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool 
   }
 }
 
-// Deterministic block sum of NV per-thread partials over a workgroup of NW waves: fixed
-// xor-butterfly inside each wave, then the NW wave sums in wave order.  On return
+// One level of a wave's recursive halving over N values (of NA slots): values [0, H) and
+// [H, N) (zero-padded to H) split by lane bit O; the lane keeps one half in acc[0, H) and adds
+// its partner's copy of that half.  Own + partner at every level is what a full xor butterfly
+// forms for every value, bit for bit, with ~N exchanges instead of 6 N.
+template <int NA, int N, int O>
+__device__ __forceinline__ void wave_halve(double (&acc)[NA], int lane) {
+  constexpr int H = (N + 1) / 2;
+  const bool hi = (lane & O) != 0;
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    const double a = acc[i], b = (H + i < N) ? acc[H + i] : 0.0;
+    const double keep = hi ? b : a, give = hi ? a : b;
+    acc[i] = keep + __shfl_xor(give, O);
+  }
+}
+// the six levels (bits 32 .. 1) over N <= 64 values; returns the value whose wave sum the lane
+// then holds in acc[0] (-1: a padding slot).  The split points are the static H of each level;
+// a lane's real count shrinks to n - H on the high side, so some slots of the last levels are
+// zero padding.
+template <int N, int NA>
+__device__ __forceinline__ int wave_halve_all(double (&acc)[NA], int lane) {
+  static_assert(N <= 64 && N <= NA, "one value per lane at most");
+  constexpr int N1 = (N + 1) / 2, N2 = (N1 + 1) / 2, N3 = (N2 + 1) / 2, N4 = (N3 + 1) / 2,
+                N5 = (N4 + 1) / 2;
+  wave_halve<NA, N, 32>(acc, lane);
+  wave_halve<NA, N1, 16>(acc, lane);
+  wave_halve<NA, N2, 8>(acc, lane);
+  wave_halve<NA, N3, 4>(acc, lane);
+  wave_halve<NA, N4, 2>(acc, lane);
+  wave_halve<NA, N5, 1>(acc, lane);
+  int idx = 0, n = N, nk = N;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int h = (nk + 1) / 2;
+    if (lane & (32 >> k)) { idx += h; n -= h; } else n = n < h ? n : h;
+    nk = h;
+  }
+  return n > 0 ? idx : -1;
+}
+
+// Deterministic block sum of NV per-thread partials over a workgroup of NW waves: the fixed
+// xor-butterfly's sums inside each wave, then the NW wave sums in wave order.  On return
 // sm[v * NW] holds sum v (after the barrier).
 template <int NV, int NW>
 __device__ __forceinline__ void block_sum_vec(double (&acc)[NV], double* sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc[v] += __shfl_xor(acc[v], o);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int v = 0; v < NV; v++) sm[v * NW + w] = acc[v];
-  }
+  // the wave sums by recursive halving (the xor butterfly's sums, bit for bit); sum v ends in
+  // one lane, which writes it
+  const int mine = wave_halve_all<NV>(acc, lane);
+  if (mine >= 0) sm[mine * NW + w] = acc[0];
   __syncthreads();
   if (threadIdx.x < NV) {
     const int v = threadIdx.x;
@@ -924,7 +959,7 @@ __global__ __launch_bounds__(kRedNT) void k_build_trial(Dev d) {
 // Work items (host-built, `build_schur_items`): item = (block, chunk c of nch); chunk c covers
 // pairs [q0 + c*CH, ...) and, on a diagonal block, pose edges [e0 + c*CH, ...).  One wave per
 // item: lane L accumulates entries L, L+64, ... in registers, a fixed recursive halving over
-// the wave (schur_halve) leaves each of the 42 sums in one lane.  A block with one chunk (config E: ~90 pairs per
+// the wave (wave_halve_all) leaves each of the 42 sums in one lane.  A block with one chunk (config E: ~90 pairs per
 // block) writes S / bschur directly; otherwise the chunk's sums go to a partial slot and
 // the wave that completes the block's last chunk adds the slots in chunk order (config C: 55
 // blocks of thousands of pairs, so a
@@ -945,31 +980,6 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
   }
 }
 
-// one level of k_schur's recursive halving over N values: values [0, H) and [H, N) (zero-padded
-// to H) split by lane bit O; the lane keeps one half in acc[0, H)
-template <int N, int O>
-__device__ __forceinline__ void schur_halve(double (&acc)[42], int lane) {
-  constexpr int H = (N + 1) / 2;
-  const bool hi = (lane & O) != 0;
-#pragma unroll
-  for (int i = 0; i < H; i++) {
-    const double a = acc[i], b = (H + i < N) ? acc[H + i] : 0.0;
-    const double keep = hi ? b : a, give = hi ? a : b;
-    acc[i] = keep + __shfl_xor(give, O);
-  }
-}
-// the sum a lane holds after the six levels (-1: a padding slot).  The split points are the
-// static H of each level (21, 11, 6, 3, 2, 1); a lane's real count shrinks to n - H on the
-// high side, so some slots of the last levels are zero padding.
-__device__ __forceinline__ int schur_idx(int lane) {
-  constexpr int kH[6] = {21, 11, 6, 3, 2, 1};
-  int idx = 0, n = 42;
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    if (lane & (32 >> k)) { idx += kH[k]; n -= kH[k]; } else n = n < kH[k] ? n : kH[k];
-  }
-  return n > 0 ? idx : -1;
-}
 
 __global__ __launch_bounds__(256) void k_schur(Dev d) {
   if (lm_done(d)) return;
@@ -1029,14 +1039,8 @@ __global__ __launch_bounds__(256) void k_schur(Dev d) {
   // the 42 wave sums by recursive halving: at level o a lane keeps the half of its values
   // selected by lane bit o and adds its partner's copy of that half (own + partner: the same
   // sum, bit for bit, as a full xor butterfly forms for every value), so 44 exchanges instead
-  // of 6 x 42, and sum v ends in one lane (schur_idx), which writes it
-  schur_halve<42, 32>(acc, lane);
-  schur_halve<21, 16>(acc, lane);
-  schur_halve<11, 8>(acc, lane);
-  schur_halve<6, 4>(acc, lane);
-  schur_halve<3, 2>(acc, lane);
-  schur_halve<2, 1>(acc, lane);
-  const int v = schur_idx(lane);
+  // of 6 x 42, and sum v ends in one lane (wave_halve_all), which writes it
+  const int v = wave_halve_all<42>(acc, lane);
   if (v < 0) return;
   if (slot < 0) schur_write(d, bi, bj, lam0, v, acc[0]);
   else d.schur_part[(size_t)slot * 42 + v] = acc[0];
