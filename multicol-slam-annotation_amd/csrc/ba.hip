@@ -1089,13 +1089,21 @@ __global__ __launch_bounds__(256) void k_update(Dev d) {
   if (gt < 4 * d.nl) {   // points: four lanes per point, as the point build
     const int k = gt >> 2, sub = gt & 3;
     double c[3] = {0.0, 0.0, 0.0};
-    for (int q = d.pt_ptr[k] + sub; q < d.pt_ptr[k + 1]; q += 4) {
-      const int e = d.pt_edges[q];
-      const int i1 = d.pt_h[q];
-      if (i1 < 0) continue;
+    auto term = [&](int e, int i1) {
+      if (i1 < 0) return;
       const double* B = d.hpl + 18 * e;
       for (int b = 0; b < 3; b++)
         for (int a = 0; a < 6; a++) c[b] -= B[3 * a + b] * d.xp[6 * i1 + a];
+    };
+    // the quad lane's entries q and q + 4 with their index loads together, applied in q order
+    const int q1 = d.pt_ptr[k + 1];
+    for (int q = d.pt_ptr[k] + sub; q < q1; q += 8) {
+      const bool two = q + 4 < q1;
+      const int qb = two ? q + 4 : q;
+      const int ea = d.pt_edges[q], eb = d.pt_edges[qb];
+      const int ia = d.pt_h[q], ib = d.pt_h[qb];
+      term(ea, ia);
+      if (two) term(eb, ib);
     }
 #pragma unroll
     for (int b = 0; b < 3; b++) c[b] = d.bl[3 * k + b] + quad_sum(c[b]);
