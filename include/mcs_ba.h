@@ -281,11 +281,18 @@ int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const doubl
                          int32_t* zero_pivot);
 /* Same, choosing the kernels: path 0 = what the BA uses (n <= 64: the fused one-tile solve,
  * else pad + the pipelined factorisation (one launch) + backward), path 1 = always pad + one
- * panel launch per step + backward, path 2 = always pad + pipelined factorisation + backward
- * (bitwise equal to path 1).  All
- * give bitwise equal x (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled). */
+ * panel launch per step + the multi-workgroup backward, path 2 = always pad + pipelined
+ * factorisation + backward (bitwise equal to path 1), path 3 = pad + one panel launch per step
+ * + the one-workgroup backward substitution (what every path runs above 96 tiles, n > 6144,
+ * and the BA with MCS_LDLT_PIPE=0).  Paths 0-2 give bitwise equal x
+ * (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled).  A timed-out hand-off wait
+ * of the pipelined kernels returns MCS_ERR_HIP (never a zero pivot). */
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
                             int32_t* zero_pivot, int32_t path);
+/* Test hook: the pipelined LDL^T's hand-off wait bound in ticks of the 100 MHz real-time counter
+ * (<= 0 restores the default 25,000,000 = 0.25 s).  Process-wide; tests lower it to force the
+ * timeout path, which must surface as MCS_ERR_HIP from the solve and the BA entries. */
+int mcs_ldlt_set_wait_ticks(int64_t ticks);
 
 #ifdef __cplusplus
 }

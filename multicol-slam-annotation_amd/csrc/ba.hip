@@ -226,6 +226,7 @@ struct LmCtl {
   double chi0, lambda_final;
   int ni, qmax, nBad, it, iter;
   int done, lin, restore, stop_out, ext_stop;
+  int dev_err;       // a solve's hand-off wait timed out (ldlt::kFlagTimeout): the run is aborted
   int max_iterations, max_trials, terminate_max_iter;
   unsigned arrive;   // k_edges_end's arrival counter (0 between launches)
   double trace[kLmTraceCap];
@@ -567,8 +568,14 @@ __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig) {
   {
     const int stop = __hip_atomic_load(&sig->ext_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     c->ext_stop = stop;
+    if (flag & ldlt::kFlagTimeout) {   // x is garbage: no LM decision, the host reports MCS_ERR_HIP
+      c->dev_err = 1;
+      c->done = 1;
+      c->restore = 1;                  // k_edges_end pops the trial's state
+      return;
+    }
     double tempChi = sc[0];
-    if (flag) tempChi = 1.7976931348623157e308;
+    if (flag & ldlt::kFlagZeroPivot) tempChi = 1.7976931348623157e308;
     double rho = c->currentChi - tempChi;
     double scale = sc[2] + sc[1];
     scale += 1e-3;
@@ -1978,6 +1985,10 @@ struct Optimizer {
           if ((rc = enqueue_trial(*stop != 0))) return rc;
           int fl;   // identical on every rank (same reduced system)
           if ((rc = wait_trial(&fl))) return rc;
+          if (fl & ldlt::kFlagTimeout) {
+            set_error("BA: the LDL^T solve's hand-off wait timed out (ldlt kFlagTimeout); result discarded");
+            return MCS_ERR_HIP;
+          }
           if (c->timing) {
             if (lin_pending) { c->acc_ms[0] += ms(0, 1); lin_pending = false; }
             if (sh.ordered) c->acc_ms[2] += ms(3, 4);
@@ -1992,7 +2003,7 @@ struct Optimizer {
           const double scale_pose = sharded ? c->pinned[3] : c->pinned[2];
           agreed_stop = sharded ? tr[2] > 0 : *stop != 0;
           double tempChi = tr[0];
-          if (fl) tempChi = std::numeric_limits<double>::max();
+          if (fl & ldlt::kFlagZeroPivot) tempChi = std::numeric_limits<double>::max();
           rho = currentChi - tempChi;
           double scale = scale_pose + tr[1];
           scale += 1e-3;
@@ -2182,6 +2193,10 @@ struct Optimizer {
     // per-edge chi2 of every edge at the final estimate, poses, points: the common tail
     const int rtail = download(poses, points, edge_chi2);
     if (rtail) return rtail;
+    if (hc->dev_err) {
+      set_error("BA: the LDL^T solve's hand-off wait timed out (ldlt kFlagTimeout); optimisation aborted");
+      return MCS_ERR_HIP;
+    }
     if (hc->stop_out) *stop = 1;   // the terminate action raised the flag (host-visible)
     if (rep) {
       rep->chi2_initial = empty ? 0.0 : hc->chi0;
@@ -2619,6 +2634,11 @@ int mcs_ba_point_block_eval(int32_t device, const double* H, double lambda, cons
   return rc;
 }
 
+int mcs_ldlt_set_wait_ticks(int64_t ticks) {
+  ldlt::set_wait_ticks((long long)ticks);
+  return MCS_OK;
+}
+
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
                          int32_t* zero_pivot) {
   return mcs_dense_ldlt_solve_ex(device, S, n, b, x, zero_pivot, 0);
@@ -2626,7 +2646,7 @@ int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const doubl
 
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,
                             int32_t* zero_pivot, int32_t path) {
-  if (!S || !b || !x || n < 1 || path < 0 || path > 2) return MCS_ERR_ARG;
+  if (!S || !b || !x || n < 1 || path < 0 || path > 3) return MCS_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     set_error("no HIP device visible (no CPU fallback)");
@@ -2662,8 +2682,11 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
       chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
       ldlt::Work w{dL, dI, dz};
       // path 0 and 2: the pipelined factorisation (one launch); path 1: one launch per step;
-      // both with the multi-workgroup backward substitution
-      if (rc == MCS_OK) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
+      // both with the multi-workgroup backward substitution.  Path 3, and every path above
+      // kPipeMaxT tiles (as in the BA): one launch per step + the one-workgroup backward
+      // substitution, without the pipeline's sync words.
+      const bool pipelined = path != 3 && T <= ldlt::kPipeMaxT;
+      if (rc == MCS_OK && pipelined) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
       w.per_step = (path == 1);
       chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
       chk(hipStreamSynchronize(st), "sync");
@@ -2675,7 +2698,11 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
     chk(hipMemcpyAsync(&fl, dflag, 4, hipMemcpyDeviceToHost, st), "d2h");
     chk(hipStreamSynchronize(st), "sync");
     for (int r = 0; r < n; r++) x[r] = hx[r];
-    if (zero_pivot) *zero_pivot = fl;
+    if (rc == MCS_OK && (fl & ldlt::kFlagTimeout)) {
+      set_error("dense LDL^T: a hand-off wait of the pipelined solve timed out; x discarded");
+      rc = MCS_ERR_HIP;
+    }
+    if (zero_pivot) *zero_pivot = fl & ldlt::kFlagZeroPivot;
   }
   for (void* q : {(void*)dA, (void*)dL, (void*)dI, (void*)db, (void*)dx, (void*)dz, (void*)dflag})
     if (q) (void)hipFree(q);

@@ -5,6 +5,8 @@
 //            SearchForTriangulationRaw          src/cORBmatcher.cpp:968-1156
 //            best/second-best scans             src/cORBmatcher.cpp:67-163, 326-475
 #include "common.hpp"
+#include <map>
+#include <mutex>
 #include "../../include/mcs_matcher.h"
 #include "ldlt.hpp"
 #include <cstring>
@@ -1112,14 +1114,24 @@ static int search_for_triangulation(const uint8_t* desc1, const uint8_t* mask1,
   chk(hipMemcpy(dE, E, 72 * (size_t)ncams * ncams, hipMemcpyHostToDevice));
   int dev = 0;
   chk(hipGetDevice(&dev));
-  mcs_tri_workspace* ws = nullptr;
-  if (e == hipSuccess && (rc = mcs_tri_workspace_create(dev, n1, n2, &ws)) != MCS_OK) e = hipErrorOutOfMemory;
-  if (e == hipSuccess)
-    e = tri_run(ws, dA, dmA, dcA, dhA, drA, n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, bytes, th_low,
-                epi_thresh, dm12, dn, nullptr);
-  chk(hipMemcpy(matches12, dm12, 4 * (size_t)n1, hipMemcpyDeviceToHost));
-  chk(hipMemcpy(n_matches, dn, 4, hipMemcpyDeviceToHost));
-  mcs_tri_workspace_destroy(ws);
+  {
+    // one workspace per device, kept for the process and grown on demand (a call holds the
+    // lock for its whole run: calls on one device share the buffers)
+    static std::mutex mu;
+    static std::map<int, mcs_tri_workspace*> cache;
+    std::lock_guard<std::mutex> g(mu);
+    mcs_tri_workspace*& ws = cache[dev];
+    if (e == hipSuccess && (!ws || ws->max_n1 < n1 || ws->max_n2 < n2)) {
+      const int32_t g1 = ws ? std::max(ws->max_n1, n1) : n1, g2 = ws ? std::max(ws->max_n2, n2) : n2;
+      if (ws) { mcs_tri_workspace_destroy(ws); ws = nullptr; }
+      if ((rc = mcs_tri_workspace_create(dev, g1, g2, &ws)) != MCS_OK) { ws = nullptr; e = hipErrorOutOfMemory; }
+    }
+    if (e == hipSuccess)
+      e = tri_run(ws, dA, dmA, dcA, dhA, drA, n1, dB, dmB, dcB, dhB, drB, n2, ncams, dE, bytes, th_low,
+                  epi_thresh, dm12, dn, nullptr);
+    chk(hipMemcpy(matches12, dm12, 4 * (size_t)n1, hipMemcpyDeviceToHost));
+    chk(hipMemcpy(n_matches, dn, 4, hipMemcpyDeviceToHost));
+  }
   void* bufs[] = {dA, dB, dmA, dmB, dhA, dhB, dcA, dcB, drA, drB, dE, dm12, dn};
   for (void* p : bufs)
     if (p) (void)hipFree(p);

@@ -15,6 +15,7 @@
 //                      the right-hand side b_i -= L_ik u_k.
 // backward (one workgroup): x_k = Linv_kk^T z_k, z_j -= L_kj^T x_k for j < k.
 #include "ldlt.hpp"
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -597,7 +598,7 @@ __global__ __launch_bounds__(256) void k_panel(double* __restrict__ A, double* _
     double* gI = Linv + (size_t)k * TB * TB;
     for (int e = t; e < TB * TB; e += 256) gI[e] = sI[(e >> 6) * LS + (e & 63)];
     if (t < TB) z[k * TB + t] = su[t] / sK[t * LS + t];
-    if (t == 0 && fail) *flag = 1;
+    if (t == 0 && fail) atomicOr(flag, kFlagZeroPivot);
     return;
   }
   d4 wi[4], wj[4];
@@ -710,7 +711,7 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
 // Deadlock freedom does not depend on residency or dispatch order: tickets are taken from one
 // device-scope counter; the diag workgroup at step k waits only on tasks of steps <= k - 1, and
 // every task waits only on earlier tickets or on diag steps <= its own step.  Every wait is
-// bounded (kWaitTicks): a timeout sets the error word and the solve's failure flag, and
+// bounded (PipeArgs::wait_ticks): a timeout sets the error word and the solve's failure flag, and
 // every workgroup then drains out.
 // Hand-offs (MI355X_MICROARCH.md, visibility; cdna_hip_programming.md Guideline 16, R1):
 // payload stored write-through (sc1: 16-B buffer stores from LDS, 8-B stores from registers),
@@ -723,8 +724,8 @@ namespace {
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
-// a wait gives up after this many ticks of the 100 MHz real-time counter (0.25 s)
-constexpr long long kWaitTicks = 25000000;
+// a wait gives up after PipeArgs::wait_ticks ticks of the 100 MHz real-time counter
+constexpr long long kWaitTicksDefault = 25000000;   // 0.25 s
 
 __device__ __forceinline__ unsigned pl_load(const unsigned* p) {
   return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -751,14 +752,15 @@ __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
 // Lane 0 waits until *w_i >= v_i for every non-null word (bounded in time), then acquires; all threads get the
 // outcome (false: timed out here or elsewhere).
 __device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const unsigned* w1, unsigned v1,
-                                     const unsigned* w2, unsigned v2, unsigned* err, int* sh_ok) {
+                                     const unsigned* w2, unsigned v2, unsigned* err, int* sh_ok,
+                                     long long ticks) {
   if (threadIdx.x == 0) {
     int ok = 1;
     const long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
       if ((!w0 || pl_load(w0) >= v0) && (!w1 || pl_load(w1) >= v1) && (!w2 || pl_load(w2) >= v2)) break;
       if (pl_load(err) != 0u) { ok = 0; break; }
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { pl_store(err, 1u); ok = 0; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { pl_store(err, 1u); ok = 0; break; }
       __builtin_amdgcn_s_sleep(1);
     }
     if (ok) {
@@ -795,6 +797,7 @@ struct PipeArgs {
   int ntasks, T, ntile;
   int* flag;
   const int* skip;
+  long long wait_ticks;
 };
 
 __device__ __forceinline__ int tix(int I, int J, int T) { return (int)band_tiles(I - J, T) + J; }
@@ -894,7 +897,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     DSTAMP(k, 0);
     // A_kk after products 0 .. k-2 (UPDATE tasks), then product k-1 from the tiles this
     // workgroup formed at step k-1 (still in sX / sY, u_{k-1} in su)
-    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok)) break;
+    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
     DSTAMP(k, 1);
     // A_kk -= L_{k,k-1} W_{k,k-1}^T on the 10 lower 16x16 blocks only (the upper ones are
     // not read by the factorisation), 3 / 3 / 2 / 2 blocks per wave; each block is the same
@@ -956,14 +959,14 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
       st_sc1(g.du + (size_t)k * 128 + TB + t, su[t]);
       g.z[k * TB + t] = su[t] / dk;
     }
-    if (t == 0 && *fail) *g.flag = 1;
+    if (t == 0 && *fail) atomicOr(g.flag, kFlagZeroPivot);
     DSTAMP(k, 3);
     wg_publish(dg + k, 1u);
     PTRACE(11, k, 0);
     DSTAMP(k, 4);
     if (k + 1 < T) {
       // the next panel tile: A_{k+1,k} after products 0 .. k-1
-      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok)) break;
+      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
       DSTAMP(k, 5);
       {
         d2 v[8];
@@ -980,7 +983,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
       DSTAMP(k, 6);
     }
   }
-  if (t == 0 && pl_load(err) != 0u) *g.flag = 1;
+  if (t == 0 && pl_load(err) != 0u) atomicOr(g.flag, kFlagTimeout);
 }
 
 __device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_ok, int tk) {
@@ -993,7 +996,7 @@ __device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_o
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
   unsigned* dg = pan + g.ntile;
-  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok)) return false;
+  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok, g.wait_ticks)) return false;
   TSTAMP(tk, 1);
   {
     d2 vx[8], vi[8];
@@ -1020,7 +1023,7 @@ __device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, 
   unsigned* err = g.sync + 1;
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
-  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok))
+  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok, g.wait_ticks))
     return false;
   TSTAMP(tk, 1);
   double a[4][4];
@@ -1085,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
     TSTAMP(tk, 3);
     PTRACE(3, ok, 0);
     if (!ok) {
-      if (threadIdx.x == 0) *g.flag = 1;
+      if (threadIdx.x == 0) atomicOr(g.flag, kFlagTimeout);
       break;
     }
   }
@@ -1104,7 +1107,7 @@ __global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
 // the fused one-tile solve.  sync: [0] ticket, [1] error, [4 .. 4+T) column flags.
 __global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const double* __restrict__ Linv,
                                              const double* __restrict__ z, double* x, unsigned* sync,
-                                             int T, int* flag, const int* skip) {
+                                             int T, int* flag, const int* skip, long long ticks) {
   if (skip && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double bsm[];
   double* part = bsm;              // [16][64]
@@ -1142,8 +1145,12 @@ __global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const
       const long long t0 = __builtin_amdgcn_s_memrealtime();
       while (pl_load(xf + i) == 0u) {
         if (pl_load(err) != 0u) { good = 0; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { pl_store(err, 1u); good = 0; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { pl_store(err, 1u); good = 0; break; }
         __builtin_amdgcn_s_sleep(1);
+      }
+      if (good) {   // acquire x_i before the barrier, as wg_wait does
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       ish[1] = good;
     }
@@ -1190,7 +1197,7 @@ __global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const
     __syncthreads();
     if (t == 0) pl_store(xf + k, 1u);
   } else if (t == 0) {
-    *flag = 1;
+    atomicOr(flag, kFlagTimeout);
   }
 }
 
@@ -1245,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_solve1(const double* __restrict__ A, co
   if ((t & 3) == 0) su[t >> 2] = u;
   __syncthreads();
   if (t < TB) sv[t] = su[t] / sK[t * LS + t];
-  if (t == 0 && fail) *flag = 1;
+  if (t == 0 && fail) atomicOr(flag, kFlagZeroPivot);
   __syncthreads();
   const int c = t & 63;
 #pragma unroll
@@ -1363,6 +1370,10 @@ static int device_cus() {
   return cache[dev];
 }
 
+static std::atomic<long long> g_wait_ticks{kWaitTicksDefault};
+void set_wait_ticks(long long ticks) { g_wait_ticks.store(ticks > 0 ? ticks : kWaitTicksDefault); }
+long long wait_ticks() { return g_wait_ticks.load(); }
+
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st,
                  const int* skip) {
   hipError_t e = set_lds_limit((const void*)k_panel, (int)kPanelLds);
@@ -1373,7 +1384,8 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
   if (w.sync && w.pipe_T == T) {
     e = hipMemsetAsync(w.sync, 0, pipe_sync_words(T) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
-    PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, T * (T + 1) / 2, flag, skip};
+    const long long ticks = wait_ticks();
+    PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, T * (T + 1) / 2, flag, skip, ticks};
     if (w.per_step) {
       for (int k = 0; k < T; k++) {
         const int m = T - 1 - k;
@@ -1385,7 +1397,7 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
       hipLaunchKernelGGL(k_pipe, dim3(grid), dim3(256), kPanelLds, st, g);
     }
     hipLaunchKernelGGL(k_bwd, dim3(T), dim3(256), kBwdLds, st, (const double*)w.L, (const double*)w.Linv,
-                       (const double*)w.z, x, w.sync + pipe_sync_words(T) - bwd_sync_words(T), T, flag, skip);
+                       (const double*)w.z, x, w.sync + pipe_sync_words(T) - bwd_sync_words(T), T, flag, skip, ticks);
     return hipGetLastError();
   }
   for (int k = 0; k < T; k++) {

@@ -59,8 +59,21 @@ hipError_t pipe_prepare(Work& w, int T, hipStream_t st);   // allocates W, du, s
 const std::vector<int4>& pipe_tasks_host(int T);
 void pipe_release(Work& w);
 
-// A: tiles (destroyed), b: 64 T (destroyed), x: 64 T (out).  *flag (device) = 1 on an
-// exact zero pivot, else left untouched (callers clear it).  All launches on st.
+// Solve status bits in *flag (device; callers clear it, the kernels only OR bits in):
+//   kFlagZeroPivot: an exact zero pivot (the reference's failed solve, g2o rejects the trial);
+//   kFlagTimeout:   a hand-off wait of the pipelined factorisation / backward substitution gave
+//                   up (kernels on other streams holding its workgroups off the CUs, preemption,
+//                   profiler serialisation).  x is garbage; the caller must report an error, never
+//                   treat it as a rejected trial.
+constexpr int kFlagZeroPivot = 1;
+constexpr int kFlagTimeout = 2;
+// hand-off wait bound in ticks of the 100 MHz real-time counter (default 25,000,000 = 0.25 s);
+// a test hook (mcs_ldlt_set_wait_ticks) lowers it to force the timeout path
+void set_wait_ticks(long long ticks);
+long long wait_ticks();
+
+// A: tiles (destroyed), b: 64 T (destroyed), x: 64 T (out).  Status bits into *flag (above).
+// All launches on st.
 // skip (nullable, device): every kernel returns at once when *skip != 0 (a device-driven
 // optimisation loop that has ended, ba.hip).
 hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* flag, hipStream_t st,

@@ -128,6 +128,7 @@ SIGNATURES = {
     "mcs_global_ba": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_dense_ldlt_solve": (ctypes.c_int, [_I32, _P, _I32, _P, _P, _P]),
     "mcs_dense_ldlt_solve_ex": (ctypes.c_int, [_I32, _P, _I32, _P, _P, _P, _I32]),
+    "mcs_ldlt_set_wait_ticks": (ctypes.c_int, [ctypes.c_int64]),
     "mcs_ba_lm_replay": (ctypes.c_int, [_I32, _P, _P, _P, _I32, _P, _P]),
     "mcs_ba_huber_eval": (ctypes.c_int, [_I32, _P, _I32, ctypes.c_double, _P, _P]),
     "mcs_ba_enable_timing": (ctypes.c_int, [_P, _I32]),

@@ -750,7 +750,9 @@ Solver.optimize_sharded = _solver_optimize_sharded
 def dense_ldlt_solve(S, b, device=0, tiled=False, path=None):
     """Device LDL^T solve of the reduced camera system (test hook) -> (x, zero_pivot).
     tiled=True forces the pad + per-step panel + backward kernels even for n <= 64 (path 1);
-    path=2 forces the pipelined factorisation (one launch); default path 0 = what BA uses."""
+    path=2 forces the pipelined factorisation (one launch); path=3 the per-step panels with the
+    one-workgroup backward substitution (every path above 96 tiles); default path 0 = what BA
+    uses."""
     from . import lib, _check
     S = np.ascontiguousarray(S, np.float64)
     b = np.ascontiguousarray(b, np.float64)
@@ -762,6 +764,12 @@ def dense_ldlt_solve(S, b, device=0, tiled=False, path=None):
     _check(lib().mcs_dense_ldlt_solve_ex(int(device), _p(S), n, _p(b), _p(x), ctypes.byref(zp),
                                          int(path)))
     return x, zp.value
+
+
+def set_ldlt_wait_ticks(ticks):
+    """Test hook: the pipelined LDL^T's hand-off wait bound (100 MHz ticks; <= 0 = default)."""
+    from . import lib, _check
+    _check(lib().mcs_ldlt_set_wait_ticks(int(ticks)))
 
 
 BA_STAGES = ("linearize", "schur", "exchange", "solve", "update")

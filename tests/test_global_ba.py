@@ -204,6 +204,74 @@ def test_gpu_pipelined_solve_matches_per_step(gpu, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [65, 300])
+def test_gpu_legacy_solve_path(gpu, n):
+    """Path 3 (one k_panel launch per step + the one-workgroup k_backward, what every path runs
+    above 96 tiles) solves like the others (it sums the backward substitution in another order,
+    so the comparison is to the solution, not bitwise); a zero pivot is reported the same way."""
+    from mcs_amd import ba
+    rng = np.random.default_rng(900 + n)
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    x3, z3 = ba.dense_ldlt_solve(S, b, path=3)
+    assert z3 == 0
+    ref = np.linalg.solve(S, b)
+    assert np.allclose(x3, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+    S2 = S.copy()
+    S2[n - 2, :] = 0.0
+    S2[:, n - 2] = 0.0
+    _, z3 = ba.dense_ldlt_solve(S2, b, path=3)
+    assert z3 == 1
+
+
+@pytest.mark.gpu
+def test_gpu_solve_above_pipeline_tiles(gpu):
+    """T = 97 tiles (n = 6150 > 96 * 64): every path runs the per-step kernels without the
+    pipeline's sync words (pipe_prepare is never asked for more than kPipeMaxT tiles)."""
+    from mcs_amd import ba
+    n = 6150
+    rng = np.random.default_rng(6150)
+    S = np.zeros((n, n))
+    for d in range(0, 70, 7):            # a symmetric band, diagonally dominant
+        v = rng.uniform(-1, 1, n - d)
+        S[np.arange(d, n), np.arange(n - d)] = v
+        S[np.arange(n - d), np.arange(d, n)] = v
+    S[np.arange(n), np.arange(n)] = 20.0
+    b = rng.normal(size=n)
+    for path in (0, 1, 2):
+        x, zp = ba.dense_ldlt_solve(S, b, path=path)
+        assert zp == 0
+        assert np.linalg.norm(S @ x - b) <= 1e-10 * np.linalg.norm(b) * 30.0
+
+
+@pytest.mark.gpu
+def test_gpu_ldlt_timeout_is_an_error(gpu, gproblem):
+    """A hand-off wait that gives up (forced with a 1-tick bound) is an error of the solve
+    (MCS_ERR_HIP), never a zero pivot that the LM would take as a rejected trial; the BA
+    entries return it too, and a normal bound afterwards solves again."""
+    from mcs_amd import ba, McsError
+    n = 1194
+    rng = np.random.default_rng(77)
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    b = rng.normal(size=n)
+    try:
+        ba.set_ldlt_wait_ticks(1)
+        with pytest.raises(McsError) as ei:
+            ba.dense_ldlt_solve(S, b, path=2)
+        assert "timed out" in str(ei.value)
+        with pytest.raises(McsError) as ei:
+            ba.Solver().global_ba(gproblem, trace=20)
+        assert "timed out" in str(ei.value)
+    finally:
+        ba.set_ldlt_wait_ticks(0)
+    x, zp = ba.dense_ldlt_solve(S, b, path=2)
+    assert zp == 0
+    assert np.allclose(x, np.linalg.solve(S, b), rtol=1e-9)
+
+
+@pytest.mark.gpu
 def test_gpu_dense_ldlt_zero_pivot(gpu):
     from mcs_amd import ba
     S = np.eye(70)
