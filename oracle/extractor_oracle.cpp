@@ -769,6 +769,23 @@ int oracle_level_candidates_type(const uint8_t* img, const uint8_t* mask, int w,
   return 0;
 }
 
+// FastFeatureDetector(th, true, type)::detect on a whole w x h block (the ROI the reference cuts
+// out, copied) with its mask block (NULL: none): triples (x, y, score) in emission order.  Used
+// as the OpenCV stand-in of tests/golden/gen_extractor_ref.py.
+int oracle_fast_detect_block(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
+                             int fast_type, int* xys_out, int cap, int* n_out) {
+  Img im; im.create(w, h); std::memcpy(im.d.data(), img, (size_t)w * h);
+  Img mk; if (mask) { mk.create(w, h); std::memcpy(mk.d.data(), mask, (size_t)w * h); }
+  std::vector<Cand> c;
+  fast_detect_roi(im, mask ? &mk : nullptr, 0, 0, w, h, fastTh, c, fast_type);
+  *n_out = (int)c.size();
+  if ((int)c.size() > cap) return -1;
+  for (size_t i = 0; i < c.size(); i++) {
+    xys_out[3 * i] = c[i].x; xys_out[3 * i + 1] = c[i].y; xys_out[3 * i + 2] = c[i].score;
+  }
+  return 0;
+}
+
 int oracle_level_candidates(const uint8_t* img, const uint8_t* mask, int w, int h, int fastTh,
                             int* xys_out, int cap, int* n_out) {
   return oracle_level_candidates_type(img, mask, w, h, fastTh, 2, xys_out, cap, n_out);

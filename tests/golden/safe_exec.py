@@ -22,6 +22,9 @@ _NODES = (
     ast.BinOp, ast.UnaryOp, ast.BoolOp, ast.Compare, ast.IfExp,
     ast.Add, ast.Sub, ast.Mult, ast.Div, ast.Mod, ast.Pow, ast.USub, ast.UAdd, ast.Not,
     ast.And, ast.Or, ast.Eq, ast.NotEq, ast.Lt, ast.LtE, ast.Gt, ast.GtE,
+    # cxx_eval.py (round 5): loops with continue, bit operators, pointer null tests
+    ast.Continue, ast.BitAnd, ast.BitOr, ast.BitXor, ast.LShift, ast.RShift, ast.Invert,
+    ast.Is, ast.IsNot,
 )
 _ATTRS = {"make", "eye", "t", "get_minor", "sqrt", "atan", "pow", "fabs", "log"}
 

@@ -159,6 +159,26 @@ def level_candidates(level_img, level_mask, fast_th, fast_type=2):
     return out[:3 * n.value].reshape(-1, 3)
 
 
+def fast_detect_block(block, mask_block, fast_th, fast_type=2):
+    """FastFeatureDetector::detect on a whole block (+ mask block or None) -> (x, y, score) rows."""
+    h, w = block.shape
+    cap = w * h // 4 + 16
+    out = np.zeros(3 * cap, np.int32)
+    n = ctypes.c_int()
+    rc = lib().oracle_fast_detect_block(_p(np.ascontiguousarray(block)),
+                                        _p(None if mask_block is None else np.ascontiguousarray(mask_block)),
+                                        w, h, fast_th, fast_type, _p(out), cap, ctypes.byref(n))
+    assert rc == 0
+    return out[:3 * n.value].reshape(-1, 3)
+
+
+def fast_atan2(y, x):
+    f = lib().oracle_fast_atan2
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_float, ctypes.c_float]
+    return float(f(y, x))
+
+
 def octree(cands, w, h, N):
     cands = np.ascontiguousarray(cands, np.int32)
     minB = 22
