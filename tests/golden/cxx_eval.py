@@ -112,9 +112,25 @@ def is_arith(t):
 
 
 def is_obj(t):
-    """Mutable class objects (value semantics: copied on construction, assigned in place)."""
+    """Mutable class objects (value semantics: copied on construction, assigned in place).
+    VALUE_CLASSES (cv::Matx, time points) are immutable values in the runtime: rebinding them
+    is their assignment."""
     return isinstance(t, Cls) and t.name not in ("iterator", "Ptr", "InputArray", "OutputArray",
-                                                 "PointView", "Cell")
+                                                 "PointView", "Cell") and t.name not in VALUE_CLASSES
+
+
+VALUE_CLASSES = {"Matx33d", "Matx44d", "Matx22d", "Matx", "HResClk::time_point"}
+
+
+def elem_type(cont):
+    """Element type of a container type (what an iterator dereferences to)."""
+    if cont.name in ("map", "unordered_map"):
+        return Cls("pair", (cont.args[0], cont.args[1]))
+    return cont.args[0]
+
+
+_VEC_NAMES = {"Vec2d": (2, DOUBLE), "Vec3d": (3, DOUBLE), "Vec4d": (4, DOUBLE), "Vec2f": (2, FLOAT),
+              "Vec3f": (3, FLOAT), "Vector2d": (2, DOUBLE), "Vector3d": (3, DOUBLE)}
 
 
 def arith_result(a, b):
@@ -313,7 +329,9 @@ def find_function(src, signature):
     """(params text, body text) of the definition starting with `signature` (a prefix up to and
     including the function name)."""
     i = src.index(signature)
-    j = src.index("(", i + len(signature) - 1)
+    # a signature ending in "(" names the parameter list's own parenthesis (operator()( ...);
+    # otherwise the first "(" of the matched header opens it
+    j = i + len(signature) - 1 if signature.endswith("(") else src.index("(", i)
     depth, k = 0, j
     while True:
         if src[k] == "(":
@@ -398,17 +416,21 @@ class Parser:
         """-> (Ty, is_ref) or None (position restored)."""
         save = self.i
         quals = []
-        while self.peek() in _QUALS or (self.peek() in ("unsigned", "signed", "long", "short") and
-                                        self.peekk(1) == "id"):
+        while self.peek() in _QUALS:
             quals.append(self.take().text)
         name = None
-        if self.peekk() == "id" and self.peek() not in _KEYWORDS:
+        ints = ("unsigned", "signed", "long", "short", "int", "char")
+        if self.peek() in ints:                          # `long unsigned int`, `unsigned long`, ...
+            while self.peek() in ints:
+                self.take()
+            name = "int"
+            while self.peek() in _QUALS:
+                self.take()
+        elif self.peekk() == "id" and self.peek() not in _KEYWORDS:
             name = self.take().text
             while self.peek() == "::" and self.peekk(1) == "id":
                 self.take()
                 name += "::" + self.take().text
-        elif quals and quals[-1] in ("unsigned", "signed", "long", "short"):
-            name = "int"
         if name is None:
             self.i = save
             return None
@@ -438,7 +460,7 @@ class Parser:
 
     def _templ_ok(self, base):
         return base in ("vector", "list", "pair", "Point_", "Ptr", "Matx", "Vec", "numeric_limits",
-                        "set", "map") or base in self.type_names
+                        "set", "map", "unordered_map") or base in self.type_names
 
     def template_args(self):
         self.take("<")
@@ -447,9 +469,9 @@ class Parser:
             if self.peek() == ">":
                 self.take()
                 break
-            if self.peek() == ">>":
-                self.t[self.i] = Tok("op", ">")
-                break
+            if self.peek() == ">>":                      # C++11 `>>` closing two lists
+                self.t[self.i:self.i + 1] = [Tok("op", ">"), Tok("op", ">")]
+                continue
             if self.peekk() == "num":
                 args.append(int(self.take().text.rstrip("uUlL")))
             else:
@@ -473,6 +495,8 @@ class Parser:
             return BOOL
         if base == "void":
             return VOID
+        if base == "auto":
+            return Cls("auto")
         if base == "Point":
             return Cls("Point2i")
         if base in ("Vec2d", "Vec3d", "Vec4d", "Vec2f", "Vec3f"):
@@ -512,6 +536,16 @@ class Parser:
         if p == "for":
             self.take()
             self.take("(")
+            # range-for: for (T x : container)
+            save = self.i
+            r = self.try_type()
+            if r is not None and self.peekk() == "id" and self.peek(1) == ":":
+                name = self.take().text
+                self.take(":")
+                cont = self.expr()
+                self.take(")")
+                return ("rfor", r[0], r[1], name, cont, self.statement())
+            self.i = save
             if self.peek() == ";":
                 init = None
             else:
@@ -687,7 +721,12 @@ class Parser:
                 name = self.take().text
                 targs = ()
                 if self.peek() == "<" and name in ("at", "ptr"):
-                    targs = self.template_args()
+                    self.take("<")
+                    raw = []
+                    while self.peek() != ">":
+                        raw.append(self.take().text)
+                    self.take(">")
+                    targs = (_strip("".join(raw)),)
                 e = ("member", e, name, p == "->", targs)
             elif p in ("++", "--"):
                 self.take()
@@ -711,6 +750,28 @@ class Parser:
             e = self.expr()
             self.take(")")
             return ("paren", e)
+        if k == "id" and p == "new":
+            self.take()
+            name = self.take().text
+            while self.peek() == "::" and self.peekk(1) == "id":
+                self.take()
+                name += "::" + self.take().text
+            if self.peek() == "<":                        # template arguments of the allocated type
+                depth = 0
+                while True:
+                    t = self.take().text
+                    depth += t.count("<") - t.count(">")
+                    if depth <= 0:
+                        break
+            args = []
+            if self.peek() == "(":
+                self.take()
+                while self.peek() != ")":
+                    args.append(self.assign_expr())
+                    if self.peek() == ",":
+                        self.take()
+                self.take(")")
+            return ("new", _strip(name), args)
         if k == "id":
             name = self.take().text
             if name in ("static_cast", "const_cast", "reinterpret_cast", "dynamic_cast"):
@@ -741,11 +802,12 @@ class Parser:
 class Fn:
     """Signature of a callable the translated code may call."""
 
-    def __init__(self, pyname, params, ret, method_of=None):
+    def __init__(self, pyname, params, ret, method_of=None, defaults=()):
         self.pyname = pyname
         self.params = params          # [(Ty, is_ref, is_const)] or None (unchecked stand-in)
         self.ret = ret                # Ty, or a callable(arg types) -> Ty
         self.method_of = method_of
+        self.defaults = list(defaults)   # Python code of the trailing default arguments
 
 
 class ClassSpec:
@@ -776,6 +838,7 @@ class Ctx:
         self.consts = {}       # C++ name -> (pyname, Ty)
         self.type_names = set()
         self.factories = {}    # env name -> Ty of default elements the code constructs
+        self.scalable = {}     # class name -> env helper for `object * scalar`
 
     def add_class(self, spec):
         self.classes[spec.name] = spec
@@ -876,6 +939,8 @@ class FuncTranslator:
                 return "_Vector(%s)" % self.factory(ty.args[0])
             if ty.name == "list":
                 return "_List(%s)" % self.factory(ty.args[0])
+            if ty.name in ("map", "unordered_map"):
+                return "_Map(%s, %s)" % (self.factory(ty.args[1]), "True" if ty.name == "map" else "False")
             if ty.name == "pair":
                 return "_Pair(%s, %s)" % (self.default(ty.args[0]), self.default(ty.args[1]))
             if ty.name == "iterator":
@@ -951,13 +1016,14 @@ class FuncTranslator:
         if op == "*":
             if isinstance(e.ty, PtrT):
                 to = e.ty.to
-                if is_obj(to):
-                    return E("_deref(%s)" % e.code, to, obj=True)
+                if isinstance(to, Cls):
+                    return E("_deref(%s)" % e.code, to, obj=is_obj(to))
                 return E("%s[0]" % e.code, to, ("sub", e.code, "0"))
             if isinstance(e.ty, Cls) and e.ty.name == "iterator":
-                to = e.ty.args[0].args[0]
+                to = elem_type(e.ty.args[0])
                 if is_obj(to):
                     return E("_deref(%s)" % e.code, to, obj=True)
+                return E("_deref(%s)" % e.code, to)
             raise Unsupported("dereference of %r" % e.ty)
         if op == "!":
             return E("(not %s)" % e.code, BOOL)
@@ -1004,17 +1070,29 @@ class FuncTranslator:
 
     def ex_cast(self, n):
         ty, e = n[1], self.ex(n[2])
+        if isinstance(ty, PtrT) and e.ty == NULLT:
+            return E("None", ty)
         if isinstance(ty, PtrT) and isinstance(e.ty, PtrT):
             if ty.to == Cls("Point2i") and e.ty.to == INT:
                 return E("_PointView(%s)" % e.code, PtrT(Cls("Point2i")))
             if ty.to == e.ty.to or (ty.to == INT and e.ty.to == INT):
                 return E(e.code, ty)
+            if isinstance(ty.to, Cls) and isinstance(e.ty.to, Cls):
+                return E(e.code, ty)              # static / dynamic cast between class pointers
             raise Unsupported("pointer cast %r -> %r" % (e.ty, ty))
         if isinstance(ty, Prim):
             if ty == INT and e.ty == INT:
                 return E(e.code, INT)
             return E(self.conv(e, ty), ty)
         raise Unsupported("cast to %r" % ty)
+
+    def ex_new(self, n):
+        name, args = n[1], n[2]
+        spec = self.ctx.classes.get(name)
+        if spec is None or spec.ctor is None:
+            raise Unsupported("new %s" % name)
+        es = [self.ex(a) for a in args]
+        return E("_addr(%s(%s))" % (spec.ctor, ", ".join(e.code for e in es)), PtrT(Cls(name)))
 
     def ex_cast8(self, n):
         e = self.ex(n[1])
@@ -1045,6 +1123,8 @@ class FuncTranslator:
                 if isinstance(a.ty, Cls) and a.ty.name == "iterator" and b.ty == a.ty:
                     return E("(%s %s %s)" % (a.code, op, b.code), BOOL)
             raise Unsupported("comparison %r %s %r" % (a.ty, op, b.ty))
+        if isinstance(a.ty, Cls) and op == "*" and is_arith(b.ty) and a.ty.name in self.ctx.scalable:
+            return E("%s(%s, %s)" % (self.ctx.scalable[a.ty.name], a.code, self.conv(b, DOUBLE)), a.ty)
         if isinstance(a.ty, PtrT) and op in ("+", "-") and is_arith(b.ty):
             return E("(%s %s %s)" % (a.code, op, self.conv(b, INT)), a.ty)
         if isinstance(a.ty, Cls) and a.ty.name == "iterator" and op in ("+", "-") and is_arith(b.ty):
@@ -1080,6 +1160,10 @@ class FuncTranslator:
             el = ty.args[0]
             kc = self.conv(k, INT)
             return E("%s[%s]" % (base.code, kc), el, ("sub", base.code, kc), obj=is_obj(el))
+        if isinstance(ty, Cls) and ty.name in ("map", "unordered_map"):
+            el = ty.args[1]
+            kc = self.conv(k, ty.args[0])
+            return E("%s[%s]" % (base.code, kc), el, ("sub", base.code, kc), obj=is_obj(el))
         if isinstance(ty, Cls) and ty.name == "carray":
             el = ty.args[0]
             kc = self.conv(k, INT)
@@ -1109,7 +1193,7 @@ class FuncTranslator:
                 ty = ty.to
                 code = "_deref(%s)" % code
             elif isinstance(ty, Cls) and ty.name == "iterator":
-                ty = ty.args[0].args[0]
+                ty = elem_type(ty.args[0])
                 code = "_deref(%s)" % code
             elif isinstance(ty, Cls) and (ty.name == "Ptr" or self.ctx.classes.get(ty.name, ClassSpec("")).smart):
                 ty = ty.args[0] if ty.name == "Ptr" else ty
@@ -1170,12 +1254,20 @@ class FuncTranslator:
                 out.append(self.conv(e, pty) if isinstance(e.ty, Ty) else e.code)
         return out
 
+    def fill_defaults(self, fn, a):
+        if fn.params is not None and len(a) < len(fn.params):
+            need = len(fn.params) - len(a)
+            if need > len(fn.defaults):
+                raise Unsupported("too few arguments for %s" % fn.pyname)
+            a = a + fn.defaults[len(fn.defaults) - need:]
+        return a
+
     def ret_type(self, fn, argtys):
         return fn.ret(argtys) if callable(fn.ret) else fn.ret
 
     _MATH = {"sqrt": "_sqrt", "ceil": "_ceil", "floor": "_floor", "fabs": "_fabs", "abs": "_fabs",
              "pow": "_pow", "cos": "_cos", "sin": "_sin", "atan": "_atan", "atan2": "_atan2",
-             "exp": "_exp", "log": "_log"}
+             "exp": "_exp", "log": "_log", "round": "_cround"}
     _EXACT_F = ("sqrt", "ceil", "floor", "fabs", "abs")   # float overloads equal to rounding the double result
 
     def ex_call(self, n):
@@ -1188,10 +1280,16 @@ class FuncTranslator:
             return self.method_call(base.code, oty, mname, targs, args)
         if fnode[0] == "tname":
             base, targs = fnode[1], fnode[2]
-            if base == "vector" and len(args) == 1:
+            if base in ("vector", "list", "map", "unordered_map") and len(args) == 0:
+                ty = Cls(base, targs)
+                return E(self.default(ty), ty, obj=True)
+            if base == "vector" and len(args) in (1, 2):
                 es = [self.ex(a) for a in args]
-                return E("_vector_n(%s, %s)" % (self.factory(targs[0]), self.conv(es[0], INT)),
-                         Cls("vector", targs), obj=True)
+                if len(args) == 1:
+                    return E("_vector_n(%s, %s)" % (self.factory(targs[0]), self.conv(es[0], INT)),
+                             Cls("vector", targs), obj=True)
+                return E("_vector_nv(%s, %s, %s)" % (self.factory(targs[0]), self.conv(es[0], INT),
+                                                     self.conv(es[1], targs[0])), Cls("vector", targs), obj=True)
             raise Unsupported("call of template %s" % base)
         if fnode[0] != "name":
             e = self.ex(fnode)
@@ -1203,7 +1301,7 @@ class FuncTranslator:
         # a method of the object being translated
         if self.this is not None and s in self.this.methods and self.lookup(s) is None:
             fn = self.this.methods[s]
-            a = self.call_args(fn.params, args)
+            a = self.fill_defaults(fn, self.call_args(fn.params, args))
             return E("%s(%s)" % (fn.pyname, ", ".join(["M"] + a)), self.ret_type(fn, None))
         v = self.lookup(name)
         if v is not None and isinstance(v[1], Cls):
@@ -1228,8 +1326,14 @@ class FuncTranslator:
             argtys = None
             if callable(fn.ret):
                 argtys = [self.ex(a).ty for a in args]
-            a = self.call_args(fn.params, args)
+            a = self.fill_defaults(fn, self.call_args(fn.params, args))
             return E("%s(%s)" % (fn.pyname, ", ".join(a)), self.ret_type(fn, argtys))
+        if s in _VEC_NAMES:
+            n, et = _VEC_NAMES[s]
+            es = [self.ex(a) for a in args]
+            if len(es) != n:
+                raise Unsupported("%s with %d values" % (s, len(es)))
+            return E("_VecInit(%s)" % ", ".join(self.conv(e, et) for e in es), Cls("Vec", (et, n)), obj=True)
         if s in self.ctx.classes or s == "Point":
             cn = "Point2i" if s == "Point" else s
             spec = self.ctx.classes[cn]
@@ -1257,10 +1361,25 @@ class FuncTranslator:
                 a = [self.conv(es[0], INT)] + ([self.conv(es[1], el)] if len(es) > 1 else [])
                 return E("%s['resize'](%s)" % (code, ", ".join(a)), VOID)
             if mname == "erase":
-                return E("%s['erase'](%s)" % (code, es[0].code), Cls("iterator", (oty,)))
+                return E("%s['erase'](%s)" % (code, ", ".join(e.code for e in es)), Cls("iterator", (oty,)))
             if mname == "insert":
                 return E("%s['insert'](%s)" % (code, ", ".join(e.code for e in es)), VOID)
             raise Unsupported("%s::%s" % (oty.name, mname))
+        if isinstance(oty, Cls) and oty.name in ("map", "unordered_map"):
+            es = [self.ex(a) for a in args]
+            if mname == "find":
+                return E("%s['find'](%s)" % (code, self.conv(es[0], oty.args[0])), Cls("iterator", (oty,)))
+            if mname == "count":
+                return E("%s['count'](%s)" % (code, self.conv(es[0], oty.args[0])), INT)
+            if mname in ("begin", "end"):
+                return E("%s[%r]()" % (code, mname), Cls("iterator", (oty,)))
+            if mname in ("size",):
+                return E("%s['size']()" % code, INT)
+            if mname == "empty":
+                return E("%s['empty']()" % code, BOOL)
+            if mname == "clear":
+                return E("%s['clear']()" % code, VOID)
+            raise Unsupported("map::%s" % mname)
         if isinstance(oty, Cls) and oty.name == "Vec" and mname == "()":
             es = [self.ex(a) for a in args]
             kc = self.conv(es[0], INT)
@@ -1270,12 +1389,19 @@ class FuncTranslator:
         if spec is None or mname not in spec.methods:
             raise Unsupported("method %r::%s" % (oty, mname))
         fn = spec.methods[mname]
-        a = self.call_args(fn.params, args)
+        a = self.fill_defaults(fn, self.call_args(fn.params, args))
         rt = self.ret_type(fn, None)
         if fn.pyname is None:            # runtime method: obj['name'](...)
             key = {"()": "call"}.get(mname, mname)
-            if mname in ("at", "ptr") and targs and rt is None:
-                rt = INT if mname == "at" else PtrT(INT)
+            if mname in ("at", "ptr") and targs:
+                t = targs[0]             # the element type's name: ptr<uchar> / ptr<uint64_t> / at<double>
+                et = {"uchar": INT, "uint8_t": INT, "uint64_t": INT, "int": INT, "double": DOUBLE,
+                      "float": FLOAT}.get(t)
+                if et is None:
+                    raise Unsupported("Mat::%s<%s>" % (mname, t))
+                rt = et if mname == "at" else PtrT(et)
+                if t not in ("uchar", "uint8_t"):
+                    key = "%s_%s" % (mname, t)
             return E("%s[%r](%s)" % (code, key, ", ".join(a)), rt, obj=is_obj(rt))
         return E("%s(%s)" % (fn.pyname, ", ".join([code] + a)), rt, obj=is_obj(rt))
 
@@ -1304,7 +1430,12 @@ class FuncTranslator:
 
     def st_if(self, n, ind):
         pad = "    " * ind
-        c, pre = self.cond(n[1])
+        e, pre, post = self.ex_full(n[1])
+        c = self.conv(e, BOOL)
+        if post:
+            t = self.newtmp()
+            pre = pre + ["%s = %s" % (t, c)] + post
+            c = t
         lines = [pad + x for x in pre] + [pad + "if %s:" % c]
         lines += self.block(self.as_list(n[2]), ind + 1)
         if n[3] is not None:
@@ -1348,6 +1479,40 @@ class FuncTranslator:
         self.loops.pop()
         self.scopes.pop()
         return lines
+
+    def st_rfor(self, n, ind):
+        """for (T x : c): x walks c's elements by iterator (vector, list, map)."""
+        pad = "    " * ind
+        _, ty, ref, name, cont_n, body = n
+        c, pre, post = self.ex_full(cont_n)
+        if post or not (isinstance(c.ty, Cls) and c.ty.name in ("vector", "list", "map", "unordered_map")):
+            raise Unsupported("range-for over %r" % (c.ty,))
+        el = elem_type(c.ty)
+        self.scopes.append({})
+        ct = self.newtmp()
+        it = self.newtmp()
+        lines = [pad + x for x in pre] + [pad + "%s = %s" % (ct, c.code), pad + "%s = %s['begin']()" % (it, ct)]
+        lines.append(pad + "while %s != %s['end']():" % (it, ct))
+        self.scopes.append({})
+        if ty == Prim("auto") if False else False:
+            pass
+        vty = el if (isinstance(ty, Cls) and ty.name == "auto") else ty
+        if ref:
+            py = self.declare(name, vty, "ref" if is_obj(vty) else "val")
+            head = ["%s = _deref(%s)" % (py, it)]
+        else:
+            py = self.declare(name, vty)
+            head = ["%s = %s" % (py, ("_cp(_deref(%s))" if is_obj(vty) else "_deref(%s)") % it)]
+        step = ["%s = _inc(%s)" % (it, it)]
+        self.loops.append(step)
+        inner = [pad + "    " + x for x in head]
+        for st in self.as_list(body):
+            inner += self.st(st, ind + 1)
+        inner += [pad + "    " + x for x in step]
+        self.loops.pop()
+        self.scopes.pop()
+        self.scopes.pop()
+        return lines + inner
 
     def st_break(self, n, ind):
         return ["    " * ind + "break"]
@@ -1405,6 +1570,8 @@ class FuncTranslator:
             raise Unsupported("++ on %r" % t.ty)
         if k == "assign":
             return self.assign_stmt(e)
+        if k == "bin" and e[1] == "<<" and self._is_stream(e):
+            return []                                   # std::cout / cerr output: no effect here
         if k == "call":
             c, pre, post = self.ex_full(e)
             return pre + [c.code] + post
@@ -1414,6 +1581,8 @@ class FuncTranslator:
 
     def assign_stmt(self, e):
         _, op, lhs_n, rhs_n = e
+        if op == "=" and rhs_n[0] == "post":          # x = y++: the old value, then the increment
+            return self.assign_stmt(("assign", "=", lhs_n, rhs_n[2])) + self.expr_stmt(rhs_n, 0)
         # comma on the right: the side effects in order, then the last value
         pre = []
         while rhs_n[0] == "paren":
@@ -1436,6 +1605,8 @@ class FuncTranslator:
                 return pre + ["_assign(%s, %s)" % (lhs.code, rhs.code)]
             if isinstance(lt, Prim) or isinstance(lt, PtrT) or (isinstance(lt, Cls) and lt.name == "iterator"):
                 return pre + [self.store(lhs.lv, self.conv(rhs, lt))]
+            if isinstance(lt, Cls) and lt.name in VALUE_CLASSES:
+                return pre + [self.store(lhs.lv, self.conv(rhs, lt))]
             raise Unsupported("assignment to %r" % lt)
         bop = op[:-1]
         if is_obj(lt) and lt == Cls("Point2f") and bop == "*":
@@ -1446,6 +1617,12 @@ class FuncTranslator:
             raise Unsupported("compound assignment %s on %r" % (op, lt))
         val = self.ex_bin(("bin", bop, ("__e", lhs), ("__e", rhs)))
         return pre + [self.store(lhs.lv, self.conv(val, lt))]
+
+    @staticmethod
+    def _is_stream(e):
+        while e[0] == "bin" and e[1] == "<<":
+            e = e[2]
+        return e[0] == "name" and _strip(e[1]) in ("cout", "cerr", "clog")
 
     def ex___e(self, n):
         return n[1]
@@ -1515,6 +1692,10 @@ class FuncTranslator:
                 lines.append("%s = %s" % (py, self.default(ty)))
                 a = [self.conv(es[0], INT)] + ([self.conv(es[1], el)] if len(es) > 1 else [])
                 lines.append("%s['resize'](%s)" % (py, ", ".join(a)))
+            elif isinstance(ty, Cls) and ty.name == "Vec":
+                if len(es) != ty.args[1]:
+                    raise Unsupported("Vec of %d with %d values" % (ty.args[1], len(es)))
+                lines.append("%s = _VecInit(%s)" % (py, ", ".join(self.conv(e, ty.args[0]) for e in es)))
             else:
                 spec = self.ctx.classes.get(ty.name)
                 if spec is None:
@@ -1638,6 +1819,8 @@ def make_default(ctx, ty, rt):
             return rt.Vector(lambda: make_default(ctx, ty.args[0], rt))
         if ty.name == "list":
             return rt.List(lambda: make_default(ctx, ty.args[0], rt))
+        if ty.name in ("map", "unordered_map"):
+            return rt.Map(lambda: make_default(ctx, ty.args[1], rt), ordered=ty.name == "map")
         if ty.name == "pair":
             return rt.Pair(make_default(ctx, ty.args[0], rt), make_default(ctx, ty.args[1], rt))
         if ty.name == "iterator":
@@ -1646,10 +1829,19 @@ def make_default(ctx, ty, rt):
             return rt.Vector(lambda: 0.0, [0.0] * ty.args[1])
         spec = ctx.classes.get(ty.name)
         if spec is not None and spec.fields and spec.runtime_ctor is None:
-            return rt.Struct(ty.name, {k: make_default(ctx, t, rt) for k, t in spec.fields.items()})
+            return rt.Struct(ty.name, {k: _field_default(ctx, t, rt) for k, t in spec.fields.items()})
         if spec is not None and spec.runtime_ctor is not None:
             return spec.runtime_ctor()
     raise Unsupported("no default value for %r" % (ty,))
+
+
+def _field_default(ctx, ty, rt):
+    """A data member's initial value; members of classes the runtime does not model (DBoW2
+    vectors, the vocabulary, ...) stay unset (None): touching one fails loudly."""
+    try:
+        return make_default(ctx, ty, rt)
+    except Unsupported:
+        return None
 
 
 def build_env(ctx, rt, extra=None):
@@ -1657,9 +1849,13 @@ def build_env(ctx, rt, extra=None):
     env = rt.env()
     env["_Vector"] = rt.Vector
     env["_List"] = rt.List
+    env["_Map"] = lambda fac, ordered: rt.Map(fac, ordered)
     env["_carray"] = lambda n, fac: [fac() for _ in range(n)]
     env["_vector_n"] = lambda fac, n: rt.Vector(fac, [fac() for _ in range(n)])
     env["_VecN"] = lambda n: rt.Vector(lambda: 0.0, [0.0] * n)
+    env["_vector_nv"] = lambda fac, n, v: rt.Vector(fac, [rt.cp(v) for _ in range(n)])
+    env["_VecInit"] = lambda *xs: rt.Vector(lambda: 0.0, list(xs))
+    env["_cround"] = lambda x: float(rt.c_round(x))
     for key, ty in ctx.factories.items():
         env[key] = (lambda t: (lambda: make_default(ctx, t, rt)))(ty)
     for name, spec in ctx.classes.items():

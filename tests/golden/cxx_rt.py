@@ -71,6 +71,11 @@ def cv_round(x):
     return int(round(x)) if isinstance(x, float) else int(x)
 
 
+def c_round(x):
+    """C round(): half away from zero."""
+    return math.floor(x + 0.5) if x >= 0 else -math.floor(-x + 0.5)
+
+
 def cv_floor(x):
     return int(math.floor(x))
 
@@ -143,7 +148,7 @@ class Struct:
 
 
 def _mutable(x):
-    return isinstance(x, (Struct, Vector, List, Mat, Pair))
+    return isinstance(x, (Struct, Vector, List, Mat, Pair, Map))
 
 
 def cp(x):
@@ -229,6 +234,9 @@ class Ptr:
 
     def __bool__(self):
         return True
+
+    def __lt__(self, o):
+        return self.address() < o.address()
 
     def address(self):
         if self.seq is None:
@@ -380,6 +388,13 @@ class Vector:
     def m_end(self):
         return VecIt(self, len(self.v))
 
+    def m_erase(self, first, last=None):
+        if last is None:
+            del self.v[first.i]
+            return VecIt(self, first.i)
+        del self.v[first.i:last.i]
+        return VecIt(self, first.i)
+
     def m_insert(self, pos, first, last=None):
         if last is None:
             self.v.insert(pos.i, cp(first))
@@ -499,8 +514,110 @@ class List:
         self.n = 0
 
 
+# ------------------------------------------------------------------ std::map / unordered_map
+class MapIt:
+    __slots__ = ("m", "k")
+
+    def __init__(self, m, k):
+        self.m, self.k = m, k
+
+    def __eq__(self, o):
+        return isinstance(o, MapIt) and o.m is self.m and o.k == self.k
+
+    def __ne__(self, o):
+        return not self.__eq__(o)
+
+    def deref(self):
+        if self.k is _END:
+            raise IndexError("dereference of map end()")
+        return self.m.pair(self.k)
+
+    def __getitem__(self, k):
+        return self.deref()[k]
+
+    def inc(self):
+        keys = self.m.keys()
+        i = keys.index(self.k)
+        return MapIt(self.m, keys[i + 1] if i + 1 < len(keys) else _END)
+
+
+_END = object()
+
+
+class _MapPair(Pair):
+    """The (key, value) of a map element; writing .second writes the map."""
+    __slots__ = ("m",)
+
+    def __init__(self, m, k):
+        Pair.__init__(self, k, m.d[k])
+        self.m = m
+
+    def __setitem__(self, k, v):
+        if k != "second":
+            raise ValueError("map keys are const")
+        self.m.d[self.f["first"]] = v
+        self.f["second"] = v
+
+
+class Map:
+    """std::map (ordered by key) / std::unordered_map (iteration order is not used by the
+    translated code: find / operator[] / count only)."""
+    __slots__ = ("d", "fac", "ordered")
+
+    def __init__(self, fac, ordered=False):
+        self.d, self.fac, self.ordered = {}, fac, ordered
+
+    def copy(self):
+        m = Map(self.fac, self.ordered)
+        m.d = {k: cp(v) for k, v in self.d.items()}
+        return m
+
+    def assign(self, o):
+        self.d = {k: cp(v) for k, v in o.d.items()}
+
+    def keys(self):
+        if not self.ordered:
+            raise ValueError("iteration over an unordered_map (order unspecified)")
+        return sorted(self.d)
+
+    def pair(self, k):
+        return _MapPair(self, k)
+
+    def __getitem__(self, k):
+        if isinstance(k, str) and k in ("find", "count", "begin", "end", "size", "empty", "clear"):
+            return getattr(self, "m_" + k)
+        if k not in self.d:
+            self.d[k] = self.fac()
+        return self.d[k]
+
+    def __setitem__(self, k, v):
+        self.d[k] = v
+
+    def m_clear(self):
+        self.d = {}
+
+    def m_find(self, k):
+        return MapIt(self, k if k in self.d else _END)
+
+    def m_count(self, k):
+        return 1 if k in self.d else 0
+
+    def m_begin(self):
+        ks = self.keys()
+        return MapIt(self, ks[0] if ks else _END)
+
+    def m_end(self):
+        return MapIt(self, _END)
+
+    def m_size(self):
+        return len(self.d)
+
+    def m_empty(self):
+        return not self.d
+
+
 def deref(p):
-    if isinstance(p, (Ptr, VecIt, ListIt)):
+    if isinstance(p, (Ptr, VecIt, ListIt, MapIt)):
         return p.deref()
     if p is None:
         raise ValueError("null pointer dereference")
@@ -537,6 +654,15 @@ def std_sort(first, last):
         vec.v[first.i:last.i] = seg
         return
     raise ValueError("sort over %r" % (first,))
+
+
+def std_remove(first, last, value):
+    """std::remove on a vector range: keeps the other elements in order, returns the new end."""
+    vec = first.vec
+    seg = vec.v[first.i:last.i]
+    kept = [x for x in seg if not (x == value)]
+    vec.v[first.i:first.i + len(kept)] = kept
+    return VecIt(vec, first.i + len(kept))
 
 
 def std_copy(first, last, out):
@@ -648,6 +774,13 @@ class Mat:
     def m_ptr(self, row):
         return Ptr(self.buf.reshape(-1), (self.r0 + row) * self.buf.shape[1] + self.c0)
 
+    def m_ptr_uint64_t(self, row):
+        """ptr<uint64_t>(row) of a byte matrix whose rows are whole 64-bit words."""
+        if self.cols % 8:
+            raise ValueError("ptr<uint64_t> of a row of %d bytes" % self.cols)
+        words = np.ascontiguousarray(self.view()).view("<u8").reshape(-1)
+        return Ptr(words, row * (self.cols // 8))
+
     def m_at(self, r, c=None):
         if c is None:
             return int(self.view().reshape(-1)[r])
@@ -729,7 +862,7 @@ def env():
         "_atan2": math.atan2, "_exp": math.exp, "_log": math.log,
         "_cp": cp, "_assign": assign, "_deref": deref, "_inc": inc, "_dec": dec,
         "_addr": addr, "_addr_elem": addr_elem, "_Pair": Pair, "_Cell": Cell,
-        "_sort": std_sort, "_copy": std_copy, "_back_inserter": back_inserter,
+        "_sort": std_sort, "_copy": std_copy, "_back_inserter": back_inserter, "_remove": std_remove,
         "_point_imul": point_imul, "_PointView": PointView,
         "_range": range, "_len": len,
     }

@@ -1,0 +1,579 @@
+"""Generate tests/golden/localba_ref.npz: cOptimizer::LocalBundleAdjustment's OWN assembly and
+bookkeeping, evaluated from the reference TEXT (no reference source is stored: numbers only).
+
+Translated from /root/reference by tests/golden/cxx_eval.py (safe_exec, no builtins):
+  cOptimizer::LocalBundleAdjustment            src/cOptimizer.cpp:489-908 (the whole body:
+      local / fixed keyframe selection, the oneFixed quirk, vertex and edge construction,
+      both optimize rounds, culling, write-back)
+  cMapPoint::isBad, GetObservations, EraseObservation, TotalNrObservations, SetBadFlag
+                                               src/cMapPoint.cpp:120-206, 259-264
+  cOptimizer::stdRecon                         src/cOptimizer.cpp:54
+  OptimizationAlgorithm::SolverResult          ThirdParty/g2o/g2o/core/optimization_algorithm.h:49
+Stand-ins:
+  * keyframes / map / rig accessors return a scripted map (mcs_amd.ba.make_map geometry:
+    keyframe poses, map-point matches with NULLs, observations, bad keyframes and points);
+    std::map<cMultiKeyFrame*, ...> iterates in keyframe creation order (pointer order of a
+    monotone allocator, as DESIGN.md §3.3);
+  * g2o's SparseOptimizer records the vertices / edges the text builds; optimize(n) runs one
+    g2o round on the recorded graph through this project's g2o restatement
+    (oracle/ba_oracle.cpp oracle_ba_optimize, whose LM control / terminate action / Huber are
+    pinned to the g2o text by g2o_solver.npz), with the force-stop flag the text installs
+    (pbStopFlag, or the terminate action's auxiliary flag) carried between the rounds.
+Recorded: local keyframes (returned list), the vertex sequence (id, kind, fixed), every edge
+in vpEdges order (keyframe, point, observation, camera, measurement, information), the edges
+erased in each culling pass, the points that turned bad, the poses and points written back,
+and each optimize() call (iterations, stop flag before / after).
+
+    python tests/golden/gen_localba_ref.py [--ref /root/reference]
+"""
+import argparse
+import math
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "multicol-slam-annotation_amd"))
+import cxx_eval  # noqa: E402
+import cxx_rt as rt  # noqa: E402
+from cxx_eval import (BOOL, DOUBLE, FLOAT, INT, VOID, ClassSpec, Cls, Ctx, Fn, PtrT,  # noqa: E402
+                      Unsupported, build_env, class_body, parse_members, translate_function)
+from safe_exec import safe_exec  # noqa: E402
+
+V = lambda t: Cls("vector", (t,))  # noqa: E731
+KP = Cls("KeyPoint")
+MP, MKF = Cls("cMapPoint"), Cls("cMultiKeyFrame")
+c_ref = lambda t: (t, True, True)  # noqa: E731
+m_ref = lambda t: (t, True, False)  # noqa: E731
+val = lambda t: (t, False, True)  # noqa: E731
+
+
+def _sig(params, ret):
+    return Fn(None, params, ret)
+
+
+def find_fn(src, pattern):
+    m = re.search(pattern, src)
+    if not m:
+        raise Unsupported("no definition matching %r" % pattern)
+    return cxx_eval.find_function(src, src[m.start():m.end()])
+
+
+G2O_VERTEX = ("VertexMt_cayley", "VertexMc_cayley", "VertexOmniCameraParameters", "VertexPointXYZ",
+              "OptimizableGraph::Vertex")
+
+
+def setup(ref):
+    rd = lambda *p: open(os.path.join(ref, *p), encoding="latin-1").read()  # noqa: E731
+    ocpp, oh = rd("src", "cOptimizer.cpp"), rd("include", "cOptimizer.h")
+    mcpp, mh = rd("src", "cMapPoint.cpp"), rd("include", "cMapPoint.h")
+    oa_h = rd("ThirdParty", "g2o", "g2o", "core", "optimization_algorithm.h")
+    ctx = Ctx()
+    for vc in ("cMultiCamSys_", "cCamModelGeneral_", "Matx61d", "VecXd", "Matrix2d", "mutex"):
+        cxx_eval.VALUE_CLASSES.add(vc)
+    ctx.add_class(ClassSpec("KeyPoint", {"pt": Cls("Point2f"), "size": FLOAT, "angle": FLOAT, "response": FLOAT,
+                                         "octave": INT, "class_id": INT}, ctor="KeyPoint_", runtime_ctor=rt.KeyPoint))
+    ctx.add_class(ClassSpec("Point2f", {"x": FLOAT, "y": FLOAT}, ctor="Point2f_", runtime_ctor=rt.Point2f))
+    ctx.add_class(ClassSpec("Matx61d"))
+    ctx.add_class(ClassSpec("VecXd"))
+    ctx.add_class(ClassSpec("Matrix2d"))
+    ctx.add_class(ClassSpec("mutex"))
+    ctx.add_class(ClassSpec("unique_lock", ctor="Lock_", runtime_ctor=lambda *a: None))
+    cxx_eval.VALUE_CLASSES.add("unique_lock")
+    ctx.add_class(ClassSpec("cCamModelGeneral_", {}, {"toVector": _sig([], Cls("VecXd"))}))
+    ctx.add_class(ClassSpec("cMultiCamSys_", {}, {
+        "Get_M_t_min": _sig([], Cls("Matx61d")), "Set_M_t_from_min": _sig([c_ref(Cls("Matx61d"))], VOID),
+        "GetNrCams": _sig([], INT), "Get_M_c_min": _sig([val(INT)], Cls("Matx61d")),
+        "GetCamModelObj": _sig([val(INT)], Cls("cCamModelGeneral_"))}))
+    ctx.add_class(ClassSpec("cMultiKeyFrame", {
+        "mnId": INT, "mnBALocalForKF": INT, "mnBAFixedForKF": INT, "camSystem": Cls("cMultiCamSys_"),
+        "keypoint_to_cam": Cls("unordered_map", (INT, INT))}, {
+        "isBad": _sig([], BOOL), "GetVectorCovisibleKeyFrames": _sig([], V(PtrT(MKF))),
+        "GetMapPointMatches": _sig([], V(PtrT(MP))), "GetKeyPoint": _sig([c_ref(INT)], KP),
+        "GetInvSigma2": _sig([val(INT)], DOUBLE), "EraseMapPointMatch": _sig([c_ref(INT)], VOID)}))
+    ctx.add_class(ClassSpec("cMap", {}, {"EraseMapPoint": _sig([val(PtrT(MP))], VOID)}))
+    mp = ClassSpec("cMapPoint", ctor="MapPoint_")
+    ctx.add_class(mp)
+    mp.fields = parse_members(ctx, class_body(mh, "cMapPoint"))
+    for name, ret, params in (("GetWorldPos", Cls("Vec", (DOUBLE, 3)), []),
+                              ("SetWorldPos", VOID, [c_ref(Cls("Vec", (DOUBLE, 3)))]),
+                              ("UpdateNormalAndDepth", VOID, []), ("ComputeDistinctiveDescriptors", VOID, [])):
+        mp.methods[name] = _sig(params, ret)
+    obs_t = Cls("map", (PtrT(MKF), V(INT)))
+    mp.methods["isBad"] = Fn("f_mp_isBad", [], BOOL)
+    mp.methods["GetObservations"] = Fn("f_mp_GetObservations", [], obs_t)
+    mp.methods["TotalNrObservations"] = Fn("f_mp_TotalNrObservations", [], INT)
+    mp.methods["EraseObservation"] = Fn("f_mp_EraseObservation", [val(PtrT(MKF)), c_ref(INT)], VOID)
+    mp.methods["SetBadFlag"] = Fn("f_mp_SetBadFlag", [], VOID)
+    # g2o objects (recording stand-ins)
+    vmeth = {"setEstimate": _sig(None, VOID), "setId": _sig([val(INT)], VOID), "setFixed": _sig([val(BOOL)], VOID),
+             "fixed": _sig([], BOOL), "setMarginalized": _sig([val(BOOL)], VOID),
+             "estimate": _sig([], Cls("Matx61d")), "hessianIndex": _sig([], INT), "edges": _sig([], Cls("EdgeSet"))}
+    for name in G2O_VERTEX:
+        ms = dict(vmeth)
+        if name == "VertexPointXYZ":
+            ms["estimate"] = _sig([], Cls("Vec", (DOUBLE, 3)))
+        ctx.add_class(ClassSpec(name, {}, ms, ctor="G2O_" + name.replace("::", "_")))
+    ctx.add_class(ClassSpec("EdgeSet", {}, {"size": _sig([], INT)}))
+    ctx.add_class(ClassSpec("EdgeProjectXYZ2MCS", {}, {
+        "setMeasurement": _sig(None, VOID), "setInformation": _sig(None, VOID),
+        "setVertex": _sig(None, VOID), "setRobustKernel": _sig(None, VOID), "chi2": _sig([], DOUBLE),
+        "setLevel": _sig([val(INT)], VOID)}, ctor="G2O_Edge"))
+    ctx.add_class(ClassSpec("RobustKernelHuber", {}, {"setDelta": _sig([val(DOUBLE)], VOID)}, ctor="G2O_Huber"))
+    ctx.add_class(ClassSpec("SparseOptimizerTerminateAction", {}, {
+        "setGainThreshold": _sig([val(DOUBLE)], VOID), "setMaxIterations": _sig([val(INT)], VOID)},
+        ctor="G2O_Terminate"))
+    for name in ("LinearSolverEigen", "BlockSolver_6_3", "OptimizationAlgorithmLevenberg",
+                 "BlockSolver_6_3::LinearSolverType"):
+        ctx.add_class(ClassSpec(name, {}, {}, ctor="G2O_Solver"))
+    ctx.add_class(ClassSpec("SparseOptimizer", {}, {
+        "setAlgorithm": _sig(None, VOID), "setVerbose": _sig([val(BOOL)], VOID),
+        "setForceStopFlag": _sig(None, VOID), "addPostIterationAction": _sig(None, VOID),
+        "addVertex": _sig(None, BOOL), "vertex": _sig([val(INT)], PtrT(Cls("OptimizableGraph::Vertex"))),
+        "addEdge": _sig(None, BOOL), "initializeOptimization": _sig([val(INT)], BOOL),
+        "optimize": _sig([val(INT)], INT)}, ctor="G2O_Optimizer"))
+    opt = ClassSpec("cOptimizer", ctor="Optimizer_")
+    ctx.add_class(opt)
+    opt.fields = parse_members(ctx, class_body(oh, "cOptimizer"))
+    ctx.funcs["make_pair"] = Fn("_Pair", None, lambda ts: Cls("pair", tuple(ts)))
+    ctx.funcs["remove"] = Fn("_remove", None, lambda ts: Cls("iterator", (V(INT),)))
+    ctx.funcs["Matrix2d::Identity"] = Fn("s_Identity2", None, Cls("Matrix2d"))
+    ctx.scalable["Matrix2d"] = "s_mscale"
+    # enum SolverResult {...} of the g2o header
+    en = re.search(r"enum\s+SolverResult\s*\{([^}]*)\}", oa_h).group(1)
+    enum = {}
+    for it in en.split(","):
+        k, v = it.split("=")
+        enum[k.strip()] = int(v)
+        ctx.consts["OptimizationAlgorithm::" + k.strip()] = ("c_SR_" + k.strip(), INT)
+    std_recon = float(re.search(r"double cOptimizer::stdRecon\s*=\s*([\d.]+)\s*;", ocpp).group(1))
+    return ctx, ocpp, mcpp, mp, opt, enum, std_recon
+
+
+def translate_all(ref):
+    ctx, ocpp, mcpp, mp, opt, enum, std_recon = setup(ref)
+    srcs, n_stmt = [], [0]
+
+    def fn(pyname, src, pattern, this=None, ret=VOID):
+        params, init, body = find_fn(src, pattern)
+        n_stmt[0] += body.count(";")
+        srcs.append(translate_function(ctx, pyname, params, body, this_cls=this, ret=ret))
+    fn("f_mp_isBad", mcpp, r"bool cMapPoint::isBad\(\)", this=mp, ret=BOOL)
+    fn("f_mp_GetObservations", mcpp, r"std::map<cMultiKeyFrame\*, std::vector<size_t>> cMapPoint::GetObservations\(\)",
+       this=mp, ret=Cls("map", (PtrT(MKF), V(INT))))
+    fn("f_mp_TotalNrObservations", mcpp, r"int cMapPoint::TotalNrObservations\(\)", this=mp, ret=INT)
+    fn("f_mp_EraseObservation", mcpp, r"void cMapPoint::EraseObservation\(", this=mp)
+    fn("f_mp_SetBadFlag", mcpp, r"void cMapPoint::SetBadFlag\(\)", this=mp)
+    fn("f_lba", ocpp, r"std::list<cMultiKeyFrame\*> cOptimizer::LocalBundleAdjustment\(", this=opt,
+       ret=Cls("list", (PtrT(MKF),)))
+    return ctx, srcs, n_stmt[0], enum, std_recon
+
+
+# ------------------------------------------------------------------------------ g2o stand-ins
+class Standin:
+    _n = [0]
+
+    def __init__(self):
+        Standin._n[0] += 1
+        self.serial = 10 ** 9 + Standin._n[0]
+
+    def __getitem__(self, k):
+        return getattr(self, "m_" + k)
+
+
+class GVertex(Standin):
+    def __init__(self, kind, arg=None):
+        Standin.__init__(self)
+        self.kind, self.est, self.id, self.fix, self.marg, self.edges = kind, None, None, False, False, []
+
+    last_point = [None]      # the map point whose GetWorldPos was read last
+
+    def m_setEstimate(self, x):
+        self.est = [float(v) for v in (x.v if isinstance(x, rt.Vector) else x)]
+        if self.kind == "P":
+            self.point = GVertex.last_point[0]
+
+    def m_setId(self, i):
+        self.id = int(i)
+
+    def m_setFixed(self, b):
+        self.fix = bool(b)
+
+    def m_fixed(self):
+        return self.fix
+
+    def m_setMarginalized(self, b):
+        self.marg = bool(b)
+
+    def m_estimate(self):
+        return list(self.est)
+
+    def m_hessianIndex(self):
+        return -1 if self.fix else 0
+
+    def m_edges(self):
+        n = len(self.edges)
+
+        class S:
+            def __getitem__(self, k):
+                return lambda: n
+        return S()
+
+
+class GEdge(Standin):
+    def __init__(self):
+        Standin.__init__(self)
+        self.meas = self.info = self.kernel = None
+        self.v = [None] * 4
+        self.level, self.chi = 0, 0.0
+
+    def m_setMeasurement(self, m):
+        self.meas = [float(x) for x in m.v]
+
+    def m_setInformation(self, I):
+        self.info = I
+
+    def m_setVertex(self, i, vp):
+        self.v[int(i)] = rt.deref(vp)
+        self.v[int(i)].edges.append(self)
+
+    def m_setRobustKernel(self, k):
+        self.kernel = rt.deref(k)
+
+    def m_chi2(self):
+        return self.chi
+
+    def m_setLevel(self, lvl):
+        self.level = int(lvl)
+
+
+class GHuber(Standin):
+    def __init__(self):
+        Standin.__init__(self)
+        self.delta = None
+
+    def m_setDelta(self, d):
+        self.delta = float(d)
+
+
+class GTerminate(Standin):
+    def __init__(self):
+        Standin.__init__(self)
+        self.gain, self.maxit = None, None
+
+    def m_setGainThreshold(self, g):
+        self.gain = float(g)
+
+    def m_setMaxIterations(self, n):
+        self.maxit = int(n)
+
+
+class GOptimizer(Standin):
+    """g2o::SparseOptimizer: records the graph; optimize(n) = one restated g2o round."""
+
+    def __init__(self, ob, log):
+        Standin.__init__(self)
+        self.ob, self.log = ob, log
+        self.vertices, self.order, self.edges = {}, [], []
+        self.force, self.aux, self.actions, self.level = None, None, [], None
+
+    def m_setAlgorithm(self, a):
+        pass
+
+    def m_setVerbose(self, b):
+        pass
+
+    def m_setForceStopFlag(self, cell):
+        self.force = cell
+
+    def m_addPostIterationAction(self, a):
+        self.actions.append(rt.deref(a))
+
+    def m_addVertex(self, vp):
+        v = rt.deref(vp)
+        self.vertices[v.id] = v
+        self.order.append(v)
+        return True
+
+    def m_vertex(self, i):
+        v = self.vertices.get(int(i))
+        return None if v is None else rt.Ptr(obj=v)
+
+    def m_addEdge(self, ep):
+        self.edges.append(rt.deref(ep))
+        return True
+
+    def m_initializeOptimization(self, level):
+        self.level = int(level)
+        return True
+
+    def _flag(self):
+        if self.force is not None:
+            return bool(self.force[0])
+        return bool(self.aux)
+
+    def m_optimize(self, n):
+        from mcs_amd import ba
+        ta = self.actions[0]
+        mt = [v for v in self.order if v.kind == "Mt"]
+        mcs = [v for v in self.order if v.kind == "Mc"]
+        ios = [v for v in self.order if v.kind == "IO"]
+        pts = [v for v in self.order if v.kind == "P"]
+        pidx = {id(v): i for i, v in enumerate(mt)}
+        lidx = {id(v): i for i, v in enumerate(pts)}
+        cidx = {id(v): i for i, v in enumerate(mcs)}
+        for e in self.edges:                       # an edge's IO vertex is its Mc's camera
+            assert ios.index(e.v[3]) == cidx[id(e.v[2])]
+        E = self.edges
+        deltas = {e.kernel.delta for e in E}
+        assert len(deltas) == 1
+        info = [e.info for e in E]
+        pr = dict(poses=np.array([v.est for v in mt]), pose_fixed=np.array([v.fix for v in mt], np.uint8),
+                  points=np.array([v.est for v in pts]).reshape(-1, 3), mc=np.array([v.est for v in mcs]),
+                  cam=np.array([v.est for v in ios]),
+                  edge_pose=np.array([pidx[id(e.v[0])] for e in E], np.int32),
+                  edge_point=np.array([lidx[id(e.v[1])] for e in E], np.int32),
+                  edge_cam=np.array([cidx[id(e.v[2])] for e in E], np.int32),
+                  edge_meas=np.array([e.meas for e in E]), edge_info=np.array([i[1] for i in info]),
+                  huber_delta=deltas.pop())
+        assert all(i[0] == "I" for i in info)
+        lvl = np.array([0 if e.level == self.level else 1 for e in E], np.uint8)
+        before = self._flag()
+        opts = ba.BAOptions(max_iterations=int(n), gain_threshold=ta.gain, terminate_max_iter=ta.maxit)
+        r = self.ob.ba_optimize(pr, opts, edge_level=lvl, stop_flag=int(before))
+        after = bool(r["stop_flag"])
+        if self.force is not None:
+            self.force[0] = after
+        elif after or self.aux is not None:
+            self.aux = after                       # the terminate action's auxiliary flag
+        rep = r["report"]
+        for i, v in enumerate(mt):
+            v.est = [float(x) for x in r["poses"][i]]
+        for i, v in enumerate(pts):
+            v.est = [float(x) for x in r["points"][i]]
+        for e, c in zip(E, r["edge_chi2"]):
+            e.chi = float(c)
+        empty = rep.n_active_poses + rep.n_active_points == 0
+        self.log.append((int(n), int(rep.iterations), int(before), int(self._flag()), int(empty)))
+        return -1 if empty else int(rep.iterations)
+
+
+# ------------------------------------------------------------------------------ the map
+def inv_sigma2_table(levels=8, scale=1.2):
+    """mvInvLevelSigma2 as the cMultiFrame ctor builds it (src/cMultiFrame.cpp:196-209) with
+    mfScaleFactor = the extractor's double(float 1.2)."""
+    f = float(np.float32(scale))
+    s, out = 1.0, []
+    for i in range(levels):
+        if i:
+            s = s * f
+        out.append(1 / (s * s))
+    return out
+
+
+def build_world(m, rec):
+    """Scripted keyframes / map points over a make_map dict (meas rounded to float, info from
+    the octave table)."""
+    nk = len(m["kf_id"])
+    npt = len(m["pt_bad"])
+    inv = inv_sigma2_table()
+    mapobj = rt.Struct("cMap", {"EraseMapPoint": lambda p: rec["erased_mp"].append(_ptr_idx(p))})
+    kfs = []
+    for k in range(nk):                        # creation order = pointer order
+        kfs.append(rt.Struct("cMultiKeyFrame", {}))
+    mps = [rt.Struct("cMapPoint", {}) for _ in range(npt)]
+    for i, p in enumerate(mps):
+        p.f["_idx"] = i
+    for k, kf in enumerate(kfs):
+        kf.f["_idx"] = k
+    octv = np.rint(np.log(1.0 / m["obs_info"]) / (2 * math.log(1.2))).astype(int)
+    assert np.allclose(m["obs_info"], [1 / 1.2 ** (2 * o) for o in octv], rtol=1e-12)
+    m["obs_info"] = np.array([inv[o] for o in octv])
+    m["obs_meas"] = m["obs_meas"].astype(np.float32).astype(np.float64)
+    obs_of_kf = [[] for _ in range(nk)]
+    for p in range(npt):
+        for o in range(m["pt_obs_off"][p], m["pt_obs_off"][p + 1]):
+            obs_of_kf[m["obs_kf"][o]].append(o)
+    from mcs_amd import ba
+    for k, kf in enumerate(kfs):
+        covis = ba.covisibles(m, k)
+        mplist = m["kf_mp"][m["kf_mp_off"][k]:m["kf_mp_off"][k + 1]]
+        k2c = rt.Map(lambda: 0)
+        for o in obs_of_kf[k]:
+            k2c.d[o] = int(m["obs_cam"][o])
+
+        def gkp(idx, o_oct=octv):
+            kp = rt.KeyPoint()
+            kp["pt"] = rt.Point2f(m["obs_meas"][idx, 0], m["obs_meas"][idx, 1])
+            kp["octave"] = int(o_oct[idx])
+            return kp
+        cams = Standin()
+        cams.m_Get_M_t_min = (lambda k=k: [float(x) for x in m["kf_pose"][k]])
+        cams.m_Set_M_t_from_min = (lambda x, k=k: rec["pose_write"].append((k, list(x))))
+        cams.m_GetNrCams = lambda: len(m["mc"])
+        cams.m_Get_M_c_min = lambda c: [float(x) for x in m["mc"][c]]
+        cams.m_GetCamModelObj = lambda c: _CamObj(m["cam"][c])
+        kf.f.update(mnId=int(m["kf_id"][k]), mnBALocalForKF=0, mnBAFixedForKF=0, camSystem=cams,
+                    keypoint_to_cam=k2c,
+                    isBad=(lambda k=k: bool(m["kf_bad"][k])),
+                    GetVectorCovisibleKeyFrames=(lambda cv=covis: rt.Vector(lambda: None, [rt.Ptr(obj=kfs[j]) for j in cv])),
+                    GetMapPointMatches=(lambda ml=mplist: rt.Vector(lambda: None, [rt.Ptr(obj=mps[j]) if j >= 0 else None for j in ml])),
+                    GetKeyPoint=gkp, GetInvSigma2=(lambda lvl: inv[lvl]),
+                    EraseMapPointMatch=(lambda idx, k=k: rec["erased_match"].append((k, int(idx)))))
+    for p, mp in enumerate(mps):
+        obs = rt.Map(lambda: rt.Vector(lambda: 0), ordered=True)
+        for o in range(m["pt_obs_off"][p], m["pt_obs_off"][p + 1]):
+            key = rt.Ptr(obj=kfs[m["obs_kf"][o]])
+            if key not in obs.d:
+                obs.d[key] = rt.Vector(lambda: 0)
+            obs.d[key].v.append(int(o))
+        first = min(obs.d, key=lambda q: q.address()) if obs.d else None
+        mp.f.update(mnId=1000 + p, mnBALocalForKF=0, mObservations=obs, mpRefKF=first, mbBad=bool(m["pt_bad"][p]),
+                    mpMap=rt.Ptr(obj=mapobj), mMutexFeatures=None, mMutexPos=None,
+                    GetWorldPos=(lambda p=p: _world_pos(p, m)),
+                    SetWorldPos=(lambda x, p=p: rec["point_write"].append((p, [float(v) for v in x]))),
+                    UpdateNormalAndDepth=lambda: None, ComputeDistinctiveDescriptors=lambda: None)
+    return kfs, mps
+
+
+def _world_pos(p, m):
+    GVertex.last_point[0] = p
+    return rt.Vector(lambda: 0.0, [float(x) for x in m["pt_pos"][p]])
+
+
+class _CamObj:
+    def __init__(self, v):
+        self.v = [float(x) for x in v]
+
+    def __getitem__(self, k):
+        if k == "toVector":
+            return lambda: list(self.v)
+        raise KeyError(k)
+
+
+def _ptr_idx(p):
+    o = p.obj if isinstance(p, rt.Ptr) else p
+    return o.f["_idx"]
+
+
+SCENARIOS = [
+    # name, make_map kwargs, current keyframe, number of covisibles (None = all), stop flag
+    ("s0", dict(n_kf=10, n_points=400, target_edges=2600, seed=3, bad_kf=(4,)), 9, None, 0),
+    ("s1", dict(n_kf=10, n_points=400, target_edges=2600, seed=3, bad_kf=(4,)), 9, None, None),
+    ("s2", dict(n_kf=12, n_points=500, target_edges=3200, seed=4, zero_id_kf=5), 11, 6, 0),
+    ("s3", dict(n_kf=12, n_points=500, target_edges=3200, seed=4, zero_id_kf=11, bad_points=0.05), 2, 4, None),
+    ("s4", dict(n_kf=9, n_points=350, target_edges=2300, seed=8, bad_kf=(1, 6)), 0, None, 0),
+    ("s5", dict(n_kf=8, n_points=300, target_edges=1900, seed=9), 7, 2, 1),
+    # small maps whose first round converges (gain < 1e-6) before 10 iterations: the stop flag
+    # (pbStopFlag, or the terminate action's auxiliary flag) then decides round 2
+    ("s6", dict(n_kf=4, n_points=60, target_edges=360, seed=11), 3, None, 0),
+    ("s7", dict(n_kf=4, n_points=60, target_edges=360, seed=11), 3, None, None),
+    ("s8", dict(n_kf=5, n_points=90, target_edges=520, seed=12, zero_id_kf=0), 4, None, None),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=os.path.join(HERE, "localba_ref.npz"))
+    ap.add_argument("--dump", default=None)
+    a = ap.parse_args()
+    from tests import oracle_bind as ob
+    from mcs_amd import ba
+    ctx, srcs, n_stmt, enum, std_recon = translate_all(a.ref)
+    if a.dump:
+        open(a.dump, "w").write("\n".join(srcs))
+    log, rec = [], {}
+    extra = {"s_Identity2": lambda: ("I", 1.0), "s_mscale": lambda I, s: (I[0], I[1] * s),
+             "Lock_": lambda *x: None,
+             "G2O_VertexMt_cayley": lambda: GVertex("Mt"), "G2O_VertexMc_cayley": lambda: GVertex("Mc"),
+             "G2O_VertexOmniCameraParameters": lambda cam: GVertex("IO"),
+             "G2O_VertexPointXYZ": lambda: GVertex("P"), "G2O_Edge": GEdge, "G2O_Huber": GHuber,
+             "G2O_Terminate": GTerminate, "G2O_Solver": lambda *x: Standin(),
+             "G2O_Optimizer": lambda: GOptimizer(ob, log)}
+    for k, v in enum.items():
+        extra["c_SR_" + k] = v
+    env = build_env(ctx, rt, extra)
+    G = safe_exec("\n".join(srcs), env, "<ref:cOptimizer.cpp / cMapPoint.cpp>")
+    out = {"n_statements": n_stmt, "std_recon": std_recon}
+    for name, kw, cur, ncov, stop in SCENARIOS:
+        m = ba.make_map(**kw)
+        log.clear()
+        rec.clear()
+        rec.update(erased_mp=[], erased_match=[], pose_write=[], point_write=[])
+        kfs, mps = build_world(m, rec)
+        opt_obj = G["Optimizer_"]()
+        opt_obj["stdRecon"] = std_recon
+        # the covisible list the text sees (GetVectorCovisibleKeyFrames), optionally truncated
+        full = ba.covisibles(m, cur)
+        cv = full if ncov is None else full[:ncov]
+        kfs[cur].f["GetVectorCovisibleKeyFrames"] = (lambda cv=cv: rt.Vector(lambda: None, [rt.Ptr(obj=kfs[j]) for j in cv]))
+        cell = None if stop is None else [bool(stop)]
+        captured = {}
+        orig = GOptimizer.m_addEdge
+
+        def add_edge(self, ep, _orig=orig):
+            captured.setdefault("opt", self)
+            return _orig(self, ep)
+        GOptimizer.m_addEdge = add_edge
+        try:
+            res = G["f_lba"](opt_obj, rt.Ptr(obj=kfs[cur]), rt.Ptr(obj=rt.Struct("cMap", {})), 10, False, cell)
+        finally:
+            GOptimizer.m_addEdge = orig
+        p = name + "_"
+        out[p + "meta"] = np.array([cur, -1 if ncov is None else ncov, -1 if stop is None else stop], np.int64)
+        out[p + "covis"] = np.asarray(cv, np.int32)
+        for k in ("kf_id", "kf_bad", "kf_mp_off", "kf_mp", "pt_bad", "pt_obs_off", "obs_kf", "obs_cam",
+                  "obs_meas", "obs_info", "kf_pose", "pt_pos", "mc", "cam"):
+            out[p + "map_" + k] = np.asarray(m[k])
+        out[p + "local"] = np.array([_ptr_idx(q) for q in res.v] if isinstance(res, rt.List) is False else
+                                    _list_idx(res), np.int32)
+        opt = captured.get("opt")
+        if opt is not None:
+            vs = [(v.id, {"Mt": 0, "Mc": 1, "IO": 2, "P": 3}[v.kind], int(v.fix)) for v in opt.order]
+            out[p + "vertices"] = np.array(vs, np.int64)
+            kf_of = {}
+            for kf in kfs:
+                kf_of[kf.f["mnId"]] = kf.f["_idx"]
+            # every edge in vpEdges order = addEdge order: (kf, point vertex id, cam)
+            ev = []
+            for e in opt.edges:
+                ev.append((kf_of[e.v[0].id], e.v[1].id, [v.id for v in opt.order if v.kind == "Mc"].index(e.v[2].id),
+                           e.level))
+            out[p + "edges"] = np.array(ev, np.int64).reshape(-1, 4)
+            out[p + "edge_meas"] = np.array([e.meas for e in opt.edges]).reshape(-1, 2)
+            out[p + "edge_info"] = np.array([e.info[1] for e in opt.edges])
+            out[p + "edge_delta"] = np.array([e.kernel.delta for e in opt.edges])
+            out[p + "est_poses"] = np.array([v.est for v in opt.order if v.kind == "Mt"])
+            out[p + "est_points"] = np.array([v.est for v in opt.order if v.kind == "P"]).reshape(-1, 3)
+            out[p + "point_vertices"] = np.array([(v.id, v.point) for v in opt.order if v.kind == "P"],
+                                                 np.int64).reshape(-1, 2)
+        out[p + "optimize_log"] = np.array(log, np.int64).reshape(-1, 5)
+        out[p + "erased_match"] = np.array(rec["erased_match"], np.int64).reshape(-1, 2)
+        out[p + "erased_mp"] = np.array(rec["erased_mp"], np.int64)
+        out[p + "pt_bad_after"] = np.array([bool(mp.f["mbBad"]) for mp in mps], np.uint8)
+        out[p + "pose_write"] = np.array([[k] + x for k, x in rec["pose_write"]]).reshape(-1, 7)
+        out[p + "point_write"] = np.array([[q] + x for q, x in rec["point_write"]]).reshape(-1, 4)
+        out[p + "stop_after"] = -1 if cell is None else int(cell[0])
+        print("%s: %d local KFs, %d edges, optimize log %s, %d points written" % (
+            name, len(out[p + "local"]), len(out.get(p + "edges", [])), log, len(rec["point_write"])), flush=True)
+    np.savez_compressed(a.out, **out)
+    print("wrote %s (%d statements translated)" % (a.out, n_stmt))
+
+
+def _list_idx(lst):
+    out = []
+    it = lst.m_begin()
+    while it != lst.m_end():
+        out.append(_ptr_idx(it.deref()))
+        it = it.inc()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,726 @@
+"""Generate tests/golden/matcher_ref.npz: the reference matcher's OWN code, evaluated from its TEXT
+(no reference source is stored: the fixture holds numbers only).
+
+Translated from /root/reference by tests/golden/cxx_eval.py (typed C++ subset; safe_exec runs
+the result with no builtins):
+  DescriptorDistance64, DescriptorDistance64Masked        src/cORBmatcher.cpp:2443-2477
+  cORBmatcher ctor (TH_HIGH_ / TH_LOW_), RadiusByViewingCos  :44-65, :169-175
+  SearchByProjection(F, vpMapPoints, th)       (rule 0)   :67-166
+  WindowSearch                                 (rule 3)   :326-473
+  SearchForInitialization                      (rule 2)   :579-726
+  SearchForTriangulationRaw                               :968-1155
+  SearchByProjection(CurrentFrame, LastFrame)  (rule 1)   :1991-2123
+  cMultiFrame ctor (grid, concatenation, scale tables)    src/cMultiFrame.cpp:92-216
+  cMultiFrame::GetFeaturesInArea, PosInGrid               :272-353
+  members / FRAME_GRID_COLS, ROWS                         include/cMultiFrame.h:47-193,
+                                                          include/cORBmatcher.h:160-174
+Stand-ins (scripted, cited where they restate a reference function):
+  * the extractor call of the cMultiFrame ctor returns scripted keypoints / descriptors;
+  * ImgToWorld, ComputeE, CheckDistEpipolarLine: the reference text itself, via
+    tests/golden/gen_refmath.py (RefMath: refmath.npz pins them);
+  * cMapPoint / cMultiKeyFrame / cMultiCamSys_ accessors return scripted data (map points with
+    track information, keyframes with map-point matches, rays, descriptors, rig poses); the
+    projection of rule 1 (WorldToCamHom_fast) and the mirror test are scripted per point;
+  * `abs` of a double is std::abs(double) (the reference file sees <cmath>'s overloads).
+Recorded per rule: every GetFeaturesInArea call (cam, x, y, r, minLevel, maxLevel), the index
+list it returned, the query descriptor the caller read next (when it read one), and the
+rule's final output.  tests/test_matcher_ref.py feeds the same calls to the product
+(mcs_window_search_device / mcs_window_select / mcs_window_match) and the triangulation
+inputs to mcs_search_for_triangulation_raw[_masked] and compares exactly.
+
+    python tests/golden/gen_matcher_ref.py [--ref /root/reference]
+"""
+import argparse
+import os
+import re
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "multicol-slam-annotation_amd"))
+import cxx_eval  # noqa: E402
+import cxx_rt as rt  # noqa: E402
+from cxx_eval import (BOOL, DOUBLE, FLOAT, INT, VOID, ClassSpec, Cls, Ctx, Fn, PtrT,  # noqa: E402
+                      Unsupported, build_env, class_body, parse_members, translate_function)
+from safe_exec import safe_exec  # noqa: E402
+
+NC, W, H = 3, 754, 480
+INT_MAX = 2 ** 31 - 1
+
+
+def find_fn(src, pattern):
+    """(params, init, body) of the definition whose header matches the regex `pattern`."""
+    m = re.search(pattern, src)
+    if not m:
+        raise Unsupported("no definition matching %r" % pattern)
+    return cxx_eval.find_function(src, src[m.start():m.end()])
+
+
+def _sig(params, ret):
+    return Fn(None, params, ret)
+
+
+V = lambda t: Cls("vector", (t,))  # noqa: E731
+KP, MAT = Cls("KeyPoint"), Cls("Mat")
+VEC2, VEC3, VEC4 = Cls("Vec", (DOUBLE, 2)), Cls("Vec", (DOUBLE, 3)), Cls("Vec", (DOUBLE, 4))
+MP, MKF, MF = Cls("cMapPoint"), Cls("cMultiKeyFrame"), Cls("cMultiFrame")
+c_ref = lambda t: (t, True, True)  # noqa: E731
+m_ref = lambda t: (t, True, False)  # noqa: E731
+val = lambda t: (t, False, True)  # noqa: E731
+
+
+def setup(ref):
+    mcpp = open(os.path.join(ref, "src", "cORBmatcher.cpp"), encoding="latin-1").read()
+    mh = open(os.path.join(ref, "include", "cORBmatcher.h"), encoding="latin-1").read()
+    fcpp = open(os.path.join(ref, "src", "cMultiFrame.cpp"), encoding="latin-1").read()
+    fh = open(os.path.join(ref, "include", "cMultiFrame.h"), encoding="latin-1").read()
+    ctx = Ctx()
+    for vc in ("cMultiCamSys_", "cCamModelGeneral_", "ORBVocabulary", "mdBRIEFextractorOct",
+               "HResClk::time_point", "Matx33d", "Matx44d"):
+        cxx_eval.VALUE_CLASSES.add(vc)
+    ctx.add_class(ClassSpec("KeyPoint", {"pt": Cls("Point2f"), "size": FLOAT, "angle": FLOAT, "response": FLOAT,
+                                         "octave": INT, "class_id": INT}, ctor="KeyPoint_", runtime_ctor=rt.KeyPoint))
+    ctx.add_class(ClassSpec("Point2f", {"x": FLOAT, "y": FLOAT}, ctor="Point2f_", runtime_ctor=rt.Point2f))
+    r_int = val(INT)
+    ctx.add_class(ClassSpec("Mat", {"rows": INT, "cols": INT}, {"ptr": _sig([r_int], PtrT(INT)),
+                                                                 "empty": _sig([], BOOL)},
+                            ctor="Mat_", runtime_ctor=rt.mat_new))
+    ctx.add_class(ClassSpec("Matx33d", ctor="Matx33d_"))
+    ctx.add_class(ClassSpec("Matx44d", ctor="Matx44d_"))
+    ctx.add_class(ClassSpec("HResClk::time_point"))
+    ctx.add_class(ClassSpec("cCamModelGeneral_", {}, {
+        "GetWidth": _sig([], DOUBLE), "GetHeight": _sig([], DOUBLE), "GetMirrorMask": _sig([r_int], MAT),
+        "ImgToWorld": _sig([m_ref(DOUBLE)] * 3 + [c_ref(DOUBLE)] * 2, VOID),
+        "isPointInMirrorMask": _sig([c_ref(DOUBLE), c_ref(DOUBLE), r_int], BOOL)}))
+    ctx.add_class(ClassSpec("cMultiCamSys_", {}, {
+        "GetNrCams": _sig([], INT), "GetCamModelObj": _sig([r_int], Cls("cCamModelGeneral_")),
+        "Get_MtMc": _sig([r_int], Cls("Matx44d")), "Get_MtMc_inv": _sig([r_int], Cls("Matx44d")),
+        "WorldToCamHom_fast": _sig([r_int, c_ref(VEC4), m_ref(VEC2)], VOID)}))
+    ctx.add_class(ClassSpec("mdBRIEFextractorOct", {}, {
+        "()": _sig([val(MAT), val(MAT), m_ref(V(KP)), m_ref(Cls("cCamModelGeneral_")),
+                    (Cls("OutputArray"), False, True), (Cls("OutputArray"), False, True)], VOID),
+        "GetLevels": _sig([], INT), "GetScaleFactor": _sig([], DOUBLE),
+        "GetMasksLearned": _sig([], BOOL), "GetDescriptorSize": _sig([], INT)}))
+    ctx.add_class(ClassSpec("ORBVocabulary"))
+    ctx.add_class(ClassSpec("cMapPoint", {
+        "mTrackProjX": V(DOUBLE), "mTrackProjY": V(DOUBLE), "mbTrackInView": V(BOOL),
+        "mnTrackScaleLevel": V(INT), "mTrackViewCos": V(DOUBLE)}, {
+        "isBad": _sig([], BOOL), "GetDescriptorPtr": _sig([], PtrT(INT)),
+        "GetDescriptorMaskPtr": _sig([], PtrT(INT)), "GetWorldPos": _sig([], VEC3)}))
+    ctx.add_class(ClassSpec("cMultiKeyFrame", {
+        "camSystem": Cls("cMultiCamSys_"),
+        "keypoint_to_cam": Cls("unordered_map", (INT, INT)),
+        "cont_idx_to_local_cam_idx": Cls("unordered_map", (INT, INT))}, {
+        "GetMapPointMatches": _sig([], V(PtrT(MP))), "GetKeyPoints": _sig([], V(KP)),
+        "GetKeyPointsRays": _sig([], V(VEC3)),
+        "GetDescriptorRowPtr": _sig([c_ref(INT), c_ref(INT)], PtrT(INT)),
+        "GetDescriptorMaskRowPtr": _sig([c_ref(INT), c_ref(INT)], PtrT(INT))}))
+    # cMultiFrame: members from the header (FRAME_GRID_* are macros of the header)
+    macros = {}
+    for m in re.finditer(r"^\s*#define\s+(FRAME_GRID_\w+)\s+(\d+)", fh, re.M):
+        macros[m.group(1)] = (None, cxx_eval.tokenize(m.group(2)))
+    mf = ClassSpec("cMultiFrame", ctor="MultiFrame_")
+    ctx.add_class(mf)
+    mf.fields = parse_members(ctx, class_body(fh, "cMultiFrame"))
+    mf.fields["camSystem"] = Cls("cMultiCamSys_")
+    # int minLevel = -1, int maxLevel = -1 (include/cMultiFrame.h:144-148)
+    mf.methods["GetFeaturesInArea"] = Fn("f_GetFeaturesInArea", [c_ref(INT), c_ref(DOUBLE), c_ref(DOUBLE),
+                                                                  c_ref(DOUBLE), val(INT), val(INT)], V(INT),
+                                         defaults=["-1", "-1"])
+    mf.methods["PosInGrid"] = Fn("f_PosInGrid", [c_ref(INT), m_ref(KP), m_ref(INT), m_ref(INT)], BOOL)
+    om = ClassSpec("cORBmatcher", ctor="Matcher_")
+    ctx.add_class(om)
+    om.fields = parse_members(ctx, class_body(mh, "cORBmatcher"))
+    om.methods["RadiusByViewingCos"] = Fn("f_RadiusByViewingCos", [c_ref(DOUBLE)], DOUBLE)
+    # functions
+    for name, ret in [("cvRound", INT), ("sort", VOID), ("ComputeThreeMaxima", VOID),
+                      ("HResClk::now", Cls("HResClk::time_point")), ("T_in_ms", DOUBLE),
+                      ("ComputeE", Cls("Matx33d")), ("CheckDistEpipolarLine", BOOL),
+                      ("cConverter::toVec4d", VEC4), ("__builtin_popcountll", INT)]:
+        ctx.funcs[name] = Fn("s_" + re.sub(r"\W", "_", name), None, ret)
+    common = lambda ts: ts[0] if ts[0] == ts[1] else (_ for _ in ()).throw(Unsupported("mixed max"))  # noqa: E731
+    ctx.funcs["max"] = Fn("_max", None, common)
+    ctx.funcs["min"] = Fn("_min", None, common)
+    ctx.funcs["make_pair"] = Fn("_Pair", None, lambda ts: Cls("pair", tuple(ts)))
+    ptr64 = val(PtrT(INT))
+    ctx.funcs["DescriptorDistance64"] = Fn("f_DescriptorDistance64", [ptr64, ptr64, c_ref(INT)], INT)
+    ctx.funcs["DescriptorDistance64Masked"] = Fn("f_DescriptorDistance64Masked", [ptr64] * 4 + [c_ref(INT)], INT)
+    ctx.consts["INT_MAX"] = ("c_INT_MAX", INT)
+    return ctx, mcpp, fcpp, macros, mf, om
+
+
+def translate_all(ref):
+    ctx, mcpp, fcpp, macros, mf, om = setup(ref)
+    srcs, n_stmt = [], [0]
+
+    def fn(pyname, src, pattern, this=None, ret=VOID, ctor=False):
+        params, init, body = find_fn(src, pattern)
+        n_stmt[0] += body.count(";")
+        srcs.append(translate_function(ctx, pyname, params, body, this_cls=this, ret=ret, macros=macros,
+                                       init_text=init if ctor else None))
+    fn("f_DescriptorDistance64", mcpp, r"int DescriptorDistance64\(", ret=INT)
+    fn("f_DescriptorDistance64Masked", mcpp, r"int DescriptorDistance64Masked\(", ret=INT)
+    fn("f_matcher_ctor", mcpp, r"cORBmatcher::cORBmatcher\(double nnratio", this=om, ctor=True)
+    fn("f_RadiusByViewingCos", mcpp, r"double cORBmatcher::RadiusByViewingCos\(", this=om, ret=DOUBLE)
+    fn("f_rule0", mcpp, r"int cORBmatcher::SearchByProjection\(cMultiFrame &F,\s*const vector<cMapPoint\*>",
+       this=om, ret=INT)
+    fn("f_rule3", mcpp, r"int cORBmatcher::WindowSearch\(", this=om, ret=INT)
+    fn("f_rule2", mcpp, r"int cORBmatcher::SearchForInitialization\(", this=om, ret=INT)
+    fn("f_tri", mcpp, r"int cORBmatcher::SearchForTriangulationRaw\(", this=om, ret=INT)
+    fn("f_rule1", mcpp, r"int cORBmatcher::SearchByProjection\(cMultiFrame &CurrentFrame,\s*const cMultiFrame &LastFrame",
+       this=om, ret=INT)
+    fn("f_GetFeaturesInArea", fcpp, r"std::vector<size_t> cMultiFrame::GetFeaturesInArea\(", this=mf, ret=V(INT))
+    fn("f_PosInGrid", fcpp, r"bool cMultiFrame::PosInGrid\(", this=mf, ret=BOOL)
+    fn("f_frame_ctor", fcpp, r"cMultiFrame::cMultiFrame\(const std::vector<cv::Mat>& images_", this=mf, ctor=True)
+    histo = int(re.search(r"const int cORBmatcher::HISTO_LENGTH\s*=\s*(\d+)\s*;", mcpp).group(1))
+    return ctx, srcs, n_stmt[0], histo
+
+
+# ------------------------------------------------------------------------------ stand-ins
+class Obj:
+    """A scripted stand-in object: fields and methods by name."""
+
+    def __init__(self, **kw):
+        self.d = kw
+
+    def __getitem__(self, k):
+        return self.d[k]
+
+    def __setitem__(self, k, v):
+        self.d[k] = v
+
+
+def desc_words(desc):
+    return np.ascontiguousarray(desc).view("<u8").reshape(-1)
+
+
+class Recorder:
+    def __init__(self):
+        self.calls = []           # (cam, x, y, r, minL, maxL)
+        self.lists = []
+        self.qsrc = []            # query descriptor source per call: (kind, a, b) or None
+        self.armed = False
+
+
+def make_refmath(ref):
+    sys.path.insert(0, HERE)
+    import gen_refmath
+    return gen_refmath.RefMath(ref), gen_refmath.Matx
+
+
+def load(ref):
+    ctx, srcs, n_stmt, histo = translate_all(ref)
+    R, Matx = make_refmath(ref)
+    rec = Recorder()
+
+    def epi(ray1, ray2, E, th):
+        r, _ = R.check_dist_epipolar_line(list(ray1.v), list(ray2.v), E.arr(), th)
+        return r
+
+    def compute_e(T1, T2):
+        return R._compute_e(T1, T2)
+
+    extra = {
+        "s_cvRound": rt.cv_round, "s_sort": rt.std_sort,
+        "s_ComputeThreeMaxima": lambda *a: (_ for _ in ()).throw(Unsupported("orientation check is off")),
+        "s_HResClk__now": lambda: 0.0, "s_T_in_ms": lambda a, b: 0.0,
+        "s_ComputeE": compute_e, "s_CheckDistEpipolarLine": epi,
+        "s_cConverter__toVec4d": lambda v: rt.Vector(lambda: 0.0, list(v.v) + [1.0]),
+        "s___builtin_popcountll": rt.popcount64, "c_INT_MAX": INT_MAX,
+        "Matx33d_": lambda: Matx(3, 3), "Matx44d_": lambda: Matx(4, 4),
+    }
+    ctx.classes["Matx33d"].runtime_ctor = lambda: Matx(3, 3)
+    ctx.classes["Matx44d"].runtime_ctor = lambda: Matx(4, 4)
+    env = build_env(ctx, rt, extra)
+    G = safe_exec("\n".join(srcs), env, "<ref:cORBmatcher.cpp / cMultiFrame.cpp>")
+    # record every GetFeaturesInArea call (the translated function, wrapped)
+    gfa = G["f_GetFeaturesInArea"]
+
+    def gfa_rec(M, cam, x, y, r, lo, hi):
+        out = gfa(M, cam, x, y, r, lo, hi)
+        if rec.armed:
+            rec.calls.append((cam, x, y, r, lo, hi))
+            rec.lists.append(list(out.v))
+            rec.qsrc.append(None)
+        return out
+    G["f_GetFeaturesInArea"] = gfa_rec
+    return G, R, Matx, rec, n_stmt, histo
+
+
+class RecMat(rt.Mat):
+    """A descriptor Mat whose ptr<uint64_t> reads are the query-descriptor reads of a rule."""
+    __slots__ = ("rec", "cam")
+
+    def m_ptr_uint64_t(self, row):
+        rec = getattr(self, "rec", None)
+        if rec is not None and rec.armed and rec.qsrc and rec.qsrc[-1] is None:
+            rec.qsrc[-1] = ("frame", self.cam, row)
+        return rt.Mat.m_ptr_uint64_t(self, row)
+
+
+class ExtractorStandin:
+    """The extractor call of the cMultiFrame ctor (:138-139): scripted keypoints + descriptors."""
+
+    def __init__(self, per_cam, levels=8, scale=1.2, masks_learned=False, desc_bytes=32):
+        self.per_cam, self.levels, self.scale = per_cam, levels, scale
+        self.masks_learned, self.bytes = masks_learned, desc_bytes
+        self.calls = 0
+
+    def __getitem__(self, k):
+        return {"call": self.call, "GetLevels": lambda: self.levels,
+                "GetScaleFactor": lambda: float(np.float32(self.scale)),
+                "GetMasksLearned": lambda: self.masks_learned,
+                "GetDescriptorSize": lambda: self.bytes}[k]
+
+    def call(self, image, mask, kps, cam, desc, dmask):
+        c = self.calls
+        self.calls += 1
+        xy, octv, d, dm = self.per_cam[c]
+        kps.m_clear()
+        for i in range(len(xy)):
+            k = rt.KeyPoint()
+            k["pt"] = rt.Point2f(float(xy[i, 0]), float(xy[i, 1]))
+            k["octave"] = int(octv[i])
+            k["size"] = rt.f32(32 * 1.2 ** int(octv[i]))
+            kps.v.append(k)
+        desc.assign(rt.Mat(np.array(d, np.uint8)))
+        dmask.assign(rt.Mat(np.array(dm if dm is not None else np.zeros_like(d), np.uint8)))
+
+
+def cam_standin(R, camd, mask=None):
+    def i2w(xc, yc, zc, u, v):
+        x, y, z = R.img_to_world(camd, u, v)
+        xc[0], yc[0], zc[0] = x, y, z
+    return Obj(GetWidth=lambda: float(camd["Iw"]), GetHeight=lambda: float(camd["Ih"]),
+               GetMirrorMask=lambda lvl: rt.Mat(np.zeros((1, 1), np.uint8)), ImgToWorld=i2w,
+               isPointInMirrorMask=mask if mask is not None else (lambda u, v, p: True))
+
+
+def build_frame(G, R, rec, cams, per_cam, masks_learned=False, rig=None):
+    """A cMultiFrame through the reference ctor (:92-216) with scripted extractor outputs."""
+    M = G["MultiFrame_"]()
+    ex = ExtractorStandin(per_cam, masks_learned=masks_learned, desc_bytes=per_cam[0][2].shape[1])
+    cs = rig if rig is not None else Obj()
+    cs.d.setdefault("GetNrCams", lambda: len(cams))
+    cs.d.setdefault("GetCamModelObj", lambda c: cams[c])
+    images = rt.Vector(rt.Mat, [rt.Mat(np.zeros((1, 1), np.uint8)) for _ in cams])
+    extractors = rt.Vector(lambda: None, [rt.Ptr(obj=ex) for _ in cams])
+    G["f_frame_ctor"](M, images, 0.0, extractors, None, cs, 0)
+    for c in range(len(cams)):         # descriptor Mats whose row reads are recorded
+        for key in ("mDescriptors", "mDescriptorMasks"):
+            old = M[key][c]
+            rm = RecMat(old.buf, old.r0, old.c0, old.rows, old.cols)
+            rm.rec, rm.cam = None, c
+            M[key].v[c] = rm
+    return M
+
+
+def arm_frame(M, rec, on):
+    for key in ("mDescriptors",):
+        for m in M[key].v:
+            m.rec = rec if on else None
+
+
+class MapPointStandin(Obj):
+    pass
+
+
+def make_mp(idx, rec, desc, dmask=None, bad=False, track=None, world=None):
+    d = np.ascontiguousarray(desc, np.uint8)
+    words = desc_words(d)
+    mwords = desc_words(np.ascontiguousarray(dmask, np.uint8)) if dmask is not None else None
+
+    def gdp():
+        if rec.armed and rec.qsrc and rec.qsrc[-1] is None:
+            rec.qsrc[-1] = ("mp", idx, 0)
+        return rt.Ptr(words, 0)
+    t = track or {}
+    mp = MapPointStandin(
+        id=idx, isBad=lambda: bad, GetDescriptorPtr=gdp,
+        GetDescriptorMaskPtr=(lambda: rt.Ptr(mwords, 0)) if mwords is not None else (lambda: None),
+        GetWorldPos=lambda: rt.Vector(lambda: 0.0, list(world if world is not None else (0.0, 0.0, 0.0))),
+        mTrackProjX=rt.Vector(lambda: 0.0, list(t.get("x", [0.0] * NC))),
+        mTrackProjY=rt.Vector(lambda: 0.0, list(t.get("y", [0.0] * NC))),
+        mbTrackInView=rt.Vector(lambda: False, list(t.get("view", [False] * NC))),
+        mnTrackScaleLevel=rt.Vector(lambda: 0, list(t.get("level", [0] * NC))),
+        mTrackViewCos=rt.Vector(lambda: 0.0, list(t.get("cos", [1.0] * NC))))
+    return mp
+
+
+# ------------------------------------------------------------------------------ scenarios
+def lafida_cams():
+    from mcs_amd import synth
+    return synth.LAFIDA_CAMS
+
+
+def _cam_dict(c):
+    return dict(c=c["c"], d=c["d"], e=c["e"], u0=c["u0"], v0=c["v0"], p=list(c["a"]),
+                invp=list(c["pol"]), Iw=c["Iw"], Ih=c["Ih"])
+
+
+def _flip(d, nbits, rng):
+    bits = np.unpackbits(d.copy())
+    if nbits:
+        bits[rng.choice(bits.size, nbits, replace=False)] ^= 1
+    return np.packbits(bits)
+
+
+LEVEL_P = np.array([434, 362, 302, 251, 209, 175, 145, 122], np.float64)
+
+
+def frame_pair(rng, n_per_cam=300, nbytes=32, masked=False):
+    """Two frames' per-camera keypoints: F2 = F1 moved a little, descriptors noisy copies,
+    plus extra random keypoints; coordinates partly outside the image (PosInGrid drops them)."""
+    f1, f2 = [], []
+    for c in range(NC):
+        n = n_per_cam
+        xy1 = np.stack([rng.uniform(-3, W + 3, n), rng.uniform(-3, H + 3, n)], 1).astype(np.float32)
+        xy1[:20] = np.round(xy1[:20])
+        xy1[20:40, 0] = ((np.arange(20) + 0.5) * (W / 64.0)).astype(np.float32)   # PosInGrid ties
+        oct1 = rng.choice(8, n, p=LEVEL_P / LEVEL_P.sum()).astype(np.int32)
+        d1 = rng.integers(0, 256, (n, nbytes), dtype=np.uint8)
+        m1 = np.packbits((rng.random((n, nbytes * 8)) < 0.85).astype(np.uint8), axis=1) if masked else None
+        k = int(n * 0.8)
+        xy2 = np.concatenate([xy1[:k] + rng.normal(0, 2.0, (k, 2)).astype(np.float32),
+                              np.stack([rng.uniform(0, W, n - k), rng.uniform(0, H, n - k)], 1).astype(np.float32)])
+        oct2 = np.concatenate([np.clip(oct1[:k] + rng.integers(-1, 2, k), 0, 7),
+                               rng.choice(8, n - k, p=LEVEL_P / LEVEL_P.sum())]).astype(np.int32)
+        d2 = np.concatenate([np.stack([_flip(d1[i], int(rng.integers(0, 70)), rng) for i in range(k)]),
+                             rng.integers(0, 256, (n - k, nbytes), dtype=np.uint8)])
+        # near-duplicate descriptors: competing candidates for the greedy rules
+        d2[k - 10:k] = d2[k - 20:k - 10]
+        m2 = np.packbits((rng.random((n, nbytes * 8)) < 0.85).astype(np.uint8), axis=1) if masked else None
+        f1.append((xy1, oct1, d1, m1))
+        f2.append((xy2.astype(np.float32), oct2, d2, m2))
+    return f1, f2
+
+
+def frame_arrays(M):
+    """Concatenated keypoints of a translated frame (mvKeys order)."""
+    n = M["mvKeys"].m_size()
+    xy = np.zeros((n, 2), np.float32)
+    octv = np.zeros(n, np.int32)
+    cam = np.zeros(n, np.int32)
+    loc = np.zeros(n, np.int32)
+    for i, k in enumerate(M["mvKeys"].v):
+        xy[i] = (k["pt"]["x"], k["pt"]["y"])
+        octv[i] = k["octave"]
+        cam[i] = M["keypoint_to_cam"].d[i]
+        loc[i] = M["cont_idx_to_local_cam_idx"].d[i]
+    return xy, octv, cam, loc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=os.path.join(HERE, "matcher_ref.npz"))
+    ap.add_argument("--dump", default=None)
+    a = ap.parse_args()
+    G, R, Matx, rec, n_stmt, histo = load(a.ref)
+    if a.dump:
+        _, srcs, _, _ = translate_all(a.ref)
+        open(a.dump, "w").write("\n".join(srcs))
+    cams_d = [_cam_dict(c) for c in lafida_cams()]
+    out = {"n_statements": n_stmt, "histo_length": histo}
+    t0 = time.time()
+
+    def matcher(nnratio, feat_dim, masks):
+        Mo = G["Matcher_"]()
+        G["f_matcher_ctor"](Mo, nnratio, False, feat_dim, masks)
+        Mo["HISTO_LENGTH"] = histo
+        return Mo
+
+    # ---------------------------------------------------------------- windowed rules
+    for sc, (seed, masked, nbytes) in enumerate([(11, False, 32), (12, True, 32), (13, False, 16)]):
+        rng = np.random.default_rng(seed)
+        f1d, f2d = frame_pair(rng, nbytes=nbytes, masked=masked)
+        cams = [cam_standin(R, cams_d[c]) for c in range(NC)]
+        F1 = build_frame(G, R, rec, cams, f1d, masks_learned=masked)
+        F2 = build_frame(G, R, rec, cams, f2d, masks_learned=masked)
+        pre = "w%d_" % sc
+        for tag, F in (("f1", F1), ("f2", F2)):
+            xy, octv, cam, loc = frame_arrays(F)
+            out[pre + tag + "_xy"], out[pre + tag + "_oct"], out[pre + tag + "_cam"] = xy, octv, cam
+            out[pre + tag + "_loc"] = loc
+            out[pre + tag + "_desc"] = np.concatenate([np.array(F["mDescriptors"][c].view()) for c in range(NC)])
+            if masked:
+                out[pre + tag + "_dmask"] = np.concatenate([np.array(F["mDescriptorMasks"][c].view()) for c in range(NC)])
+            gp = np.zeros((NC, 4))
+            for c in range(NC):
+                gp[c] = (F["mnMinX"][c], F["mnMinY"][c], F["mfGridElementWidthInv"][c], F["mfGridElementHeightInv"][c])
+            out[pre + tag + "_gp"] = gp
+            # the frame's grid as the ctor filled it: (cam, col, row) -> index list
+            cells = []
+            for c in range(NC):
+                for ix in range(64):
+                    for iy in range(48):
+                        for idx in F["mGrids"][c][ix][iy].v:
+                            cells.append((c, ix, iy, idx))
+            out[pre + tag + "_grid"] = np.array(cells, np.int32).reshape(-1, 4)
+            out[pre + tag + "_scale"] = np.array(F["mvScaleFactors"].v)
+            out[pre + tag + "_invsig2"] = np.array(F["mvInvLevelSigma2"].v)
+        n1, n2 = F1["mvKeys"].m_size(), F2["mvKeys"].m_size()
+        out[pre + "meta"] = np.array([seed, int(masked), nbytes, n1, n2])
+
+        def run(rule, fn, qframe, setup_state, result):
+            rec.calls, rec.lists, rec.qsrc = [], [], []
+            if qframe is not None:
+                arm_frame(qframe, rec, True)
+            rec.armed = True
+            nm = fn()
+            rec.armed = False
+            if qframe is not None:
+                arm_frame(qframe, rec, False)
+            k = pre + "r%d_" % rule
+            out[k + "calls"] = np.array(rec.calls, np.float64).reshape(-1, 6)
+            out[k + "list_ptr"] = np.cumsum([0] + [len(x) for x in rec.lists]).astype(np.int32)
+            out[k + "list_idx"] = np.array([i for x in rec.lists for i in x], np.int32)
+            src = np.full((len(rec.qsrc), 3), -1, np.int32)
+            for i, s in enumerate(rec.qsrc):
+                if s is not None:
+                    src[i] = (0 if s[0] == "mp" else 1, s[1], s[2])
+            out[k + "qsrc"] = src
+            out[k + "nmatches"] = nm
+            for kk, vv in result().items():
+                out[k + kk] = vv
+            print("  rule %d: %d GetFeaturesInArea calls, %d matches" % (rule, len(rec.calls), nm), flush=True)
+
+        th_high = 3 * nbytes if not masked else int(np.floor(1.5 * nbytes))
+        # rule 0: SearchByProjection(F2, map points, th): map points near F2 keypoints
+        nmp = 500
+        mps, mp_desc, mp_mask = [], [], []
+        xy2 = out[pre + "f2_xy"]
+        cam2 = out[pre + "f2_cam"]
+        oct2 = out[pre + "f2_oct"]
+        d2all = out[pre + "f2_desc"]
+        for i in range(nmp):
+            j = int(rng.integers(n2))
+            view = [bool(rng.random() < 0.7) for _ in range(NC)]
+            view[cam2[j]] = bool(rng.random() < 0.95)
+            tr = {"x": [float(xy2[j, 0] + rng.normal(0, 3)) if c == cam2[j] else float(rng.uniform(0, W)) for c in range(NC)],
+                  "y": [float(xy2[j, 1] + rng.normal(0, 3)) if c == cam2[j] else float(rng.uniform(0, H)) for c in range(NC)],
+                  "view": view, "level": [int(np.clip(oct2[j] + rng.integers(-1, 2), 0, 7)) for _ in range(NC)],
+                  "cos": [float(rng.choice([0.999, 0.99])) for _ in range(NC)]}
+            dd = _flip(d2all[j], int(rng.integers(0, 90)), rng)
+            dm = np.packbits((rng.random(nbytes * 8) < 0.85).astype(np.uint8)) if masked else None
+            mp = make_mp(i, rec, dd, dm, bad=bool(rng.random() < 0.05), track=tr)
+            mps.append(mp)
+            mp_desc.append(dd)
+            mp_mask.append(dm if dm is not None else np.zeros(nbytes, np.uint8))
+        out[pre + "mp_desc"] = np.array(mp_desc)
+        out[pre + "mp_mask"] = np.array(mp_mask)
+        pre_assigned = rng.choice(n2, 40, replace=False)
+        out[pre + "r0_pre_assigned"] = pre_assigned.astype(np.int32)
+        for th in (1.0, 3.0):
+            Mo = matcher(0.8, nbytes, masked)
+            for j in range(n2):
+                F2["mvpMapPoints"].v[j] = None
+            holder = make_mp(10 ** 6, rec, np.zeros(nbytes, np.uint8))
+            for j in pre_assigned:
+                F2["mvpMapPoints"].v[int(j)] = rt.Ptr(obj=holder)
+            vp = rt.Vector(lambda: None, [rt.Ptr(obj=m) for m in mps])
+
+            def res():
+                a = np.full(n2, -1, np.int32)
+                for j, p in enumerate(F2["mvpMapPoints"].v):
+                    if p is not None:
+                        a[j] = p.obj["id"]
+                return {"th%d_assign" % int(th): a}
+            rule0 = lambda: G["f_rule0"](Mo, F2, vp, th)  # noqa: E731
+            run(0, rule0, None, None, res)
+            for k2 in ("calls", "list_ptr", "list_idx", "qsrc", "nmatches"):
+                out[pre + "r0_th%d_%s" % (int(th), k2)] = out.pop(pre + "r0_" + k2)
+        # rule 3: WindowSearch(F1, F2, windowSize, vpMapPointMatches2, minLevel, maxLevel)
+        mp1 = [make_mp(20000 + i, rec, np.zeros(nbytes, np.uint8), bad=bool(rng.random() < 0.05)) for i in range(n1)]
+        has1 = rng.random(n1) < 0.6
+        out[pre + "r3_f1_has_mp"] = has1.astype(np.uint8)
+        out[pre + "r3_f1_mp_bad"] = np.array([m["isBad"]() for m in mp1], np.uint8)
+        for j in range(n1):
+            F1["mvpMapPoints"].v[j] = rt.Ptr(obj=mp1[j]) if has1[j] else None
+        for ws, lo, hi in ((40, 0, INT_MAX), (80, 1, 5)):
+            Mo = matcher(0.7, nbytes, masked)
+            vpm2 = rt.Vector(lambda: None)
+
+            def res():
+                a = np.full(n2, -1, np.int32)
+                for j, p in enumerate(vpm2.v):
+                    if p is not None:
+                        a[j] = p.obj["id"] - 20000
+                return {"assign": a}
+            rule3 = lambda: G["f_rule3"](Mo, F1, F2, ws, vpm2, lo, hi)  # noqa: E731
+            run(3, rule3, F1, None, res)
+            for k2 in ("calls", "list_ptr", "list_idx", "qsrc", "nmatches", "assign"):
+                out[pre + "r3_ws%d_%s" % (ws, k2)] = out.pop(pre + "r3_" + k2)
+        # rule 2: SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+        for ws in (50, 100):
+            Mo = matcher(0.9, nbytes, masked)
+            xy1 = out[pre + "f1_xy"]
+            prev = rt.Vector(lambda: rt.Vector(lambda: 0.0, [0.0, 0.0]),
+                             [rt.Vector(lambda: 0.0, [float(xy1[i, 0]), float(xy1[i, 1])]) for i in range(n1)])
+            vnm = rt.Vector(lambda: -1)
+
+            def res():
+                return {"m12": np.array(vnm.v, np.int32),
+                        "prev": np.array([p.v for p in prev.v], np.float64)}
+            rule2 = lambda: G["f_rule2"](Mo, F1, F2, prev, vnm, ws)  # noqa: E731
+            run(2, rule2, F1, None, res)
+            for k2 in ("calls", "list_ptr", "list_idx", "qsrc", "nmatches", "m12", "prev"):
+                out[pre + "r2_ws%d_%s" % (ws, k2)] = out.pop(pre + "r2_" + k2)
+        # rule 1: SearchByProjection(CurrentFrame = F2, LastFrame = F1, th): F1's map points,
+        # scripted projections into F2 (WorldToCamHom_fast) and mirror tests
+        Mo = matcher(0.9, nbytes, masked)
+        for j in range(n2):
+            F2["mvpMapPoints"].v[j] = None
+        for j in pre_assigned[:20]:
+            F2["mvpMapPoints"].v[int(j)] = rt.Ptr(obj=holder)
+        proj = {}
+        xy1 = out[pre + "f1_xy"]
+        for j in range(n1):
+            w = (float(j), 0.0, 1.0)
+            mp1[j]["GetWorldPos"] = (lambda w=w: rt.Vector(lambda: 0.0, list(w)))
+            proj[float(j)] = (float(xy1[j, 0] + rng.normal(0, 2.5)), float(xy1[j, 1] + rng.normal(0, 2.5)))
+        outl = rng.random(n1) < 0.1
+        F1["mvbOutlier"] = rt.Vector(lambda: False, [bool(x) for x in outl])
+        inmask = {float(j): bool(rng.random() < 0.92) for j in range(n1)}
+        out[pre + "r1_outlier"] = outl.astype(np.uint8)
+        out[pre + "r1_inmask"] = np.array([inmask[float(j)] for j in range(n1)], np.uint8)
+        out[pre + "r1_proj"] = np.array([proj[float(j)] for j in range(n1)])
+
+        def w2c(c, pt4, uv):
+            u, v = proj[pt4.v[0]]
+            uv.v[0], uv.v[1] = u, v
+            rec.last_pt = pt4.v[0]
+        camsys = Obj(GetNrCams=lambda: NC, WorldToCamHom_fast=w2c,
+                     GetCamModelObj=lambda c: Obj(isPointInMirrorMask=lambda u, v, p: inmask[rec.last_pt]))
+        F2["camSystem"] = camsys
+        for th in (7.0, 15.0):
+            def res():
+                a = np.full(n2, -1, np.int32)
+                for j, p in enumerate(F2["mvpMapPoints"].v):
+                    if p is not None:
+                        a[j] = p.obj["id"] - 20000 if p.obj["id"] >= 20000 and p.obj["id"] < 10 ** 6 else -2
+                return {"th%d_assign" % int(th): a}
+            snapshot = list(F2["mvpMapPoints"].v)
+            rule1 = lambda: G["f_rule1"](Mo, F2, F1, th)  # noqa: E731
+            run(1, rule1, F1, None, res)
+            for k2 in ("calls", "list_ptr", "list_idx", "qsrc", "nmatches"):
+                out[pre + "r1_th%d_%s" % (int(th), k2)] = out.pop(pre + "r1_" + k2)
+            F2["mvpMapPoints"].v = snapshot
+        print("windowed scenario %d done (%.1f s)" % (sc, time.time() - t0), flush=True)
+
+    # ---------------------------------------------------------------- SearchForTriangulationRaw
+    for sc, (seed, masked, nbytes, nper) in enumerate([(21, False, 32, 250), (22, True, 32, 250),
+                                                        (23, False, 16, 200), (24, False, 64, 200)]):
+        rng = np.random.default_rng(seed)
+        Mcs = [np.concatenate([rng.normal(0, 0.3, 3), rng.normal(0, 0.1, 3)]) for _ in range(NC)]
+        Mt1 = np.concatenate([rng.normal(0, 0.1, 3), rng.normal(0, 0.5, 3)])
+        Mt2 = Mt1 + np.concatenate([rng.normal(0, 0.03, 3), rng.normal(0, 0.2, 3)])
+        kfs = []
+        X = rng.uniform([-5, -5, -5], [5, 5, 5], (NC * nper, 3))
+        for kf, Mt in enumerate((Mt1, Mt2)):
+            mtmc = [R.mtmc(Mt, Mcs[c]) for c in range(NC)]
+            rays, cams, descs, dms, has = [], [], [], [], []
+            for c in range(NC):
+                MtMc, inv = mtmc[c]
+                A = inv.arr()
+                for i in range(nper):
+                    p = X[c * nper + i]
+                    q = A[:3, :3] @ p + A[:3, 3]
+                    if kf == 1 and rng.random() < 0.25:
+                        q = rng.normal(0, 1, 3)          # no true correspondence
+                    q = q + rng.normal(0, 0.002, 3)
+                    rays.append(q / np.linalg.norm(q))
+                    cams.append(c)
+            rays = np.array(rays)
+            n = len(rays)
+            if kf == 0:
+                base = rng.integers(0, 256, (n, nbytes), dtype=np.uint8)
+                descs = base.copy()
+            else:
+                descs = np.stack([_flip(base[i], int(rng.integers(0, 40)), rng) for i in range(n)])
+                dup = rng.choice(n, n // 10, replace=False)
+                descs[dup] = descs[np.roll(dup, 1)]       # near-identical competitors
+            dms = np.packbits((rng.random((n, nbytes * 8)) < 0.85).astype(np.uint8), axis=1) if masked else None
+            has = rng.random(n) < 0.15
+            kfs.append(dict(rays=rays, cam=np.array(cams, np.int32), desc=descs, dmask=dms, has=has,
+                            mtmc=mtmc))
+        pre = "t%d_" % sc
+        Mo = matcher(0.6, nbytes, masked)
+
+        def kf_standin(k):
+            n = len(k["rays"])
+            words = desc_words(k["desc"])
+            mwords = desc_words(k["dmask"]) if k["dmask"] is not None else None
+            wpr = nbytes // 8
+            holder = make_mp(-1, rec, np.zeros(nbytes, np.uint8))
+            mps = rt.Vector(lambda: None, [rt.Ptr(obj=holder) if k["has"][i] else None for i in range(n)])
+            kps = rt.Vector(rt.KeyPoint, [rt.KeyPoint() for _ in range(n)])
+            rays = rt.Vector(lambda: None, [rt.Vector(lambda: 0.0, list(map(float, k["rays"][i]))) for i in range(n)])
+            k2c = rt.Map(lambda: 0)
+            loc = rt.Map(lambda: 0)
+            for i in range(n):
+                k2c.d[i] = int(k["cam"][i])
+                loc.d[i] = i                                    # descriptor rows: the global order
+            camsys = Obj(GetNrCams=lambda: NC, Get_MtMc_inv=lambda c: k["mtmc"][c][1],
+                         Get_MtMc=lambda c: k["mtmc"][c][0])
+            return Obj(camSystem=camsys, keypoint_to_cam=k2c, cont_idx_to_local_cam_idx=loc,
+                       GetMapPointMatches=lambda: mps.copy(), GetKeyPoints=lambda: kps.copy(),
+                       GetKeyPointsRays=lambda: rays.copy(),
+                       GetDescriptorRowPtr=lambda c, i: rt.Ptr(words, i * wpr),
+                       GetDescriptorMaskRowPtr=lambda c, i: rt.Ptr(mwords, i * wpr))
+        K1, K2 = kf_standin(kfs[0]), kf_standin(kfs[1])
+        mk1, mr1, mk2, mr2 = (rt.Vector(rt.KeyPoint), rt.Vector(lambda: None), rt.Vector(rt.KeyPoint),
+                              rt.Vector(lambda: None))
+        pairs = rt.Vector(lambda: None)
+        t1 = time.time()
+        nm = G["f_tri"](Mo, rt.Ptr(obj=K1), rt.Ptr(obj=K2), mk1, mr1, mk2, mr2, pairs)
+        m12 = np.full(len(kfs[0]["rays"]), -1, np.int32)
+        for p in pairs.v:
+            m12[p["first"]] = p["second"]
+        E = np.zeros((NC, NC, 3, 3))
+        for i in range(NC):
+            for j in range(NC):
+                E[i, j] = R._compute_e(kfs[0]["mtmc"][i][1], kfs[1]["mtmc"][j][0]).arr()
+        for kf, k in enumerate(kfs):
+            out[pre + "k%d_rays" % kf] = k["rays"]
+            out[pre + "k%d_cam" % kf] = k["cam"]
+            out[pre + "k%d_desc" % kf] = k["desc"]
+            out[pre + "k%d_has" % kf] = k["has"].astype(np.uint8)
+            if masked:
+                out[pre + "k%d_dmask" % kf] = k["dmask"]
+        out[pre + "E"] = E
+        out[pre + "meta"] = np.array([seed, int(masked), nbytes, Mo["TH_LOW_"]])
+        out[pre + "m12"] = m12
+        out[pre + "nmatches"] = nm
+        print("triangulation scenario %d: %d matches (%.1f s)" % (sc, nm, time.time() - t1), flush=True)
+    # ---------------------------------------------------------------- a11: the distances themselves
+    rng = np.random.default_rng(31)
+    for nb in (16, 32, 64):
+        A = rng.integers(0, 256, (300, nb), dtype=np.uint8)
+        B = np.stack([_flip(A[i], int(rng.integers(0, nb * 8)), rng) for i in range(300)])
+        B[:5] = A[:5]
+        MA = np.packbits((rng.random((300, nb * 8)) < 0.8).astype(np.uint8), axis=1)
+        MB = np.packbits((rng.random((300, nb * 8)) < 0.8).astype(np.uint8), axis=1)
+        MA[5:8] = 0
+        wa, wb, wma, wmb = desc_words(A), desc_words(B), desc_words(MA), desc_words(MB)
+        k = nb // 8
+        d = [G["f_DescriptorDistance64"](rt.Ptr(wa, i * k), rt.Ptr(wb, i * k), nb) for i in range(300)]
+        dm = [G["f_DescriptorDistance64Masked"](rt.Ptr(wa, i * k), rt.Ptr(wb, i * k), rt.Ptr(wma, i * k),
+                                                rt.Ptr(wmb, i * k), nb) for i in range(300)]
+        out["d%d_a" % nb], out["d%d_b" % nb], out["d%d_ma" % nb], out["d%d_mb" % nb] = A, B, MA, MB
+        out["d%d_dist" % nb] = np.array(d, np.int32)
+        out["d%d_dist_masked" % nb] = np.array(dm, np.int32)
+    for nb, masks in ((32, False), (32, True), (16, False), (64, False)):
+        Mo = matcher(0.6, nb, masks)
+        out["th_%d_%d" % (nb, int(masks))] = np.array([Mo["TH_HIGH_"], Mo["TH_LOW_"]], np.int32)
+    np.savez_compressed(a.out, **out)
+    print("wrote %s (%d statements translated, %.1f s)" % (a.out, n_stmt, time.time() - t0))
+
+
+if __name__ == "__main__":
+    main()
