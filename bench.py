@@ -102,6 +102,74 @@ def alg_bytes_pyr_fast(level_wh):
     return sum(px[l - 1] + px[l] for l in range(1, len(px))) + sum(px)
 
 
+# HALF_PATCH_SIZE = 16 disc of IC_Angle (src/mdBRIEFextractorOct.cpp:85, :153-170 umax)
+def ic_disc_pixels(half=16):
+    import math
+    vmax = int(math.floor(half * math.sqrt(2.0) / 2 + 1))
+    vmin = int(math.ceil(half * math.sqrt(2.0) / 2))
+    umax = [0] * (half + 1)
+    for v in range(vmax + 1):
+        umax[v] = int(round(math.sqrt(half * half - v * v)))
+    v0 = 0
+    for v in range(half, vmin - 1, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    return sum(2 * umax[abs(v)] + 1 for v in range(-half, half + 1))
+
+
+def stage_rooflines(ex, F, stage_ms, n_kp, desc_size):
+    """Roofline lines of the two extractor kernels after pyramid + FAST.
+
+    k_orient_desc, per keypoint: the selection record in (4 B), the IC_Angle disc of the raw
+    level image (845 px, :221-248), the 2 x 8 x desc_size blurred samples of the rotated
+    pattern (:285-354), the keypoint out (28 B) and the descriptor out (desc_size B).  These are
+    the bytes the kernel must touch; neighbouring patches overlap and are served from L2/MALL,
+    so this is a touched-bytes rate against the HBM peak, and the binding limit is VALU issue
+    (committed SQ pass: issue share).
+    k_octree: 4 B per FAST candidate in (packed x|y|score) and 4 B per selection out
+    (:569-861); the per-cell counts (a few hundred words per level) are left out.  Latency /
+    barrier bound."""
+    import mcs_amd
+    L = mcs_amd.lib()
+    nlev = len(ex.levels()[0])
+    n_cand = 0
+    n_out = ctypes.c_int64()
+    for f in range(F):   # cap 0: the call reports the level's candidate count (MCS_ERR_CAPACITY)
+        for lv in range(nlev):
+            L.mcs_extractor_read_stage(ex._h, 2, f, lv, None, 0, ctypes.byref(n_out))
+            n_cand += int(n_out.value)
+    iss = sq_issue().get("issue", {})
+    disc = ic_disc_pixels()
+    b_kp = 4 + disc + 2 * 8 * desc_size + 28 + desc_size
+    od, oc = None, None
+    t_od = stage_ms.get("orient_desc", 0.0) / 1e3
+    if t_od > 0:
+        a = b_kp * n_kp / t_od / 1e9
+        od = {"kernel": "k_orient_desc (IC_Angle + rotated-pattern ORB, one wave per keypoint pair)",
+              "bound": "hbm", "binding": "VALU issue", "achieved": round(a, 1),
+              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 4),
+              "traffic": None, "ms_per_call": round(t_od * 1e3, 4), "keypoints_per_call": n_kp,
+              "alg_bytes_per_keypoint": b_kp,
+              "alg_bytes_note": "4 sel + %d IC disc + %d pattern samples + 28 kp + %d desc; "
+                                "touched bytes (patch overlap is cache-served)" % (
+                                    disc, 16 * desc_size, desc_size),
+              "valu_issue_share": iss.get("orient_desc_valu_util")}
+    t_oc = stage_ms.get("octree", 0.0) / 1e3
+    if t_oc > 0:
+        b = 4 * n_cand + 4 * n_kp
+        a = b / t_oc / 1e9
+        oc = {"kernel": "k_octree (DistributeOctTree, one workgroup per (frame, level))",
+              "bound": "hbm", "binding": "barrier / LDS latency", "achieved": round(a, 1),
+              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 5),
+              "traffic": None, "ms_per_call": round(t_oc * 1e3, 4),
+              "candidates_per_call": n_cand, "selected_per_call": n_kp,
+              "alg_bytes_per_call": b,
+              "valu_issue_share": None}
+    return od, oc
+
+
 def baseline_cpus(k):
     """The first k CPUs of this process's allowed set: the CPU baseline legs pin their threads
     to them (taskset-style, one thread per CPU) so the timing does not migrate across cores."""
@@ -524,7 +592,8 @@ def run_triangulation(args, rank, world, dev, stream, d_kps, d_cnt, d_desc, cap,
            "matches_per_neighbour": [int(v) for v in nm.cpu().numpy()],
            "keypoints": {"kf1": n1, "neighbours": [k["n"] for k in kf[:5]]},
            "th_low": th_low, "epi_thresh": thresh,
-           "path": "mcs_search_for_triangulation_raw_device: k_tri_radius + k_tri_private + k_tri_shared"}
+           "path": "mcs_search_for_triangulation_raw_device: k_tri_radius + k_tri_pass + k_tri_private + "
+                   "k_tri_gather + k_tri_seq (ordered pass, one wave per camera)"}
     cpu = None
     if rank == 0 and world == 1:
         from tests import oracle_bind as ob
@@ -797,6 +866,8 @@ def main():
                     "traffic": None, "alg_bytes_per_call": bpf * F}
         roofline.update(pmc_traffic(bpf * F))
         roofline.update(sq_issue())
+    roofline_od, roofline_oct = (stage_rooflines(ex, F, stage_ms, kp_per_step, params.desc_size)
+                                 if ncalls else (None, None))
 
     # ---- LocalBA (config C): 10 local MultiKeyFrames + 3 fixed observers, 3k points, ~20k edges
     localba = None
@@ -878,6 +949,8 @@ def main():
                        "match_pairs_per_step_per_gpu": NP,
                        "parallelism": "dp%d (independent multi-frame segments)" % world},
             "roofline": roofline,
+            "roofline_orient_desc": roofline_od,
+            "roofline_octree": roofline_oct,
             "cpu_baseline": cpu,
             "parity_check": parity,
             "localba": localba,

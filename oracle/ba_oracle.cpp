@@ -36,6 +36,13 @@
 
 namespace {
 
+// computeScale test hook (tests/test_ba_scale_order.py): per LM trial {currentChi - tempChi,
+// computeScale in g2o's index order, the product's split order (points' sum + poses' sum),
+// sum of |terms|, number of terms, lambda}
+bool g_scale_trace_on = false;
+std::vector<double> g_scale_trace;
+
+
 void cay2rot(const double* c, double* R) {  // misc.h:134-162
   const double c1 = c[0], c2 = c[1], c3 = c[2];
   const double c1s = c1 * c1, c2s = c2 * c2, c3s = c3 * c3;
@@ -464,6 +471,21 @@ struct Graph {
         for (int a = 0; a < 3; a++) points[3 * i + a] += x[6 * np + 3 * point_h[i] + a];
   }
 
+  // computeScale's terms summed with |.|: the bound on any other summation order (test hook)
+  void scale_terms(double lam, double* sum_abs, double* split, int* n) const {
+    double a = 0, sp = 0, sl = 0;
+    int k = 0;
+    for (int i = 0; i < 6 * np; i++, k++) {
+      const double t = x[i] * (lam * x[i] + bp[i]);
+      a += std::fabs(t); sp += t;
+    }
+    for (int j = 0; j < 3 * nl; j++, k++) {
+      const double t = x[6 * np + j] * (lam * x[6 * np + j] + bl[j]);
+      a += std::fabs(t); sl += t;
+    }
+    *sum_abs = a; *split = sl + sp; *n = k;
+  }
+
   double compute_scale(double lam) const {
     double s = 0;
     for (int i = 0; i < np; i++)
@@ -491,6 +513,12 @@ struct Graph {
       if (!ok2) tempChi = std::numeric_limits<double>::max();
       rho = currentChi - tempChi;
       double scale = compute_scale(lambda);
+      if (g_scale_trace_on) {
+        double sa, split; int nt;
+        scale_terms(lambda, &sa, &split, &nt);
+        const double rec[6] = {rho, scale, split, sa, (double)nt, lambda};
+        g_scale_trace.insert(g_scale_trace.end(), rec, rec + 6);
+      }
       scale += 1e-3;
       rho /= scale;
       if (rho > 0 && std::isfinite(tempChi)) {
@@ -566,6 +594,17 @@ int optimize(Graph& g, const mcs_ba_options& o, volatile int32_t* stop_in, mcs_b
 }  // namespace
 
 extern "C" {
+
+void oracle_scale_trace(int32_t enable) {
+  g_scale_trace_on = enable != 0;
+  g_scale_trace.clear();
+}
+int32_t oracle_scale_trace_read(double* out, int32_t cap) {
+  const int32_t n = (int32_t)(g_scale_trace.size() / 6);
+  for (int32_t i = 0; i < n && i < cap; i++)
+    for (int k = 0; k < 6; k++) out[6 * i + k] = g_scale_trace[6 * i + k];
+  return n;
+}
 
 // ComputeE (src/misc.cpp:72-86) for every camera pair as SearchForTriangulationRaw's Es table
 // (src/cORBmatcher.cpp:985-998): E[i][j] = ComputeE(invMat(M_t1 M_c[i]), M_t2 M_c[j]).

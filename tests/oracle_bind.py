@@ -288,6 +288,23 @@ def _ba_sigs():
     return L
 
 
+def scale_trace(enable=True):
+    """Start (clear) or stop the oracle's per-trial computeScale record (oracle_scale_trace)."""
+    lib().oracle_scale_trace(int(bool(enable)))
+
+
+def scale_trace_read():
+    """-> [n_trials, 6]: currentChi - tempChi, computeScale in g2o's index order, the split
+    order (points' sum + poses' sum), sum |terms|, number of terms, lambda."""
+    import ctypes as C
+    L = lib()
+    L.oracle_scale_trace_read.restype = C.c_int32
+    n = L.oracle_scale_trace_read(None, 0)
+    out = np.zeros((n, 6))
+    L.oracle_scale_trace_read(_p(out), n)
+    return out
+
+
 def ba_edge(pose, X, mc, cam, meas):
     L = _ba_sigs()
     a = [np.ascontiguousarray(v, np.float64) for v in (pose, X, mc, cam, meas)]
