@@ -227,6 +227,8 @@ struct LmCtl {
   int ni, qmax, nBad, it, iter;
   int done, lin, restore, stop_out, ext_stop;
   int dev_err;       // a solve's hand-off wait timed out (ldlt::kFlagTimeout): the run is aborted
+  int spec_lin;      // k_edges_end linearises every trial into the other Jacobian buffer
+  int jbuf;          // the linearisation buffer of the current iteration (0 / 1)
   int max_iterations, max_trials, terminate_max_iter;
   unsigned arrive;   // k_edges_end's arrival counter (0 between launches)
   double trace[kLmTraceCap];
@@ -264,6 +266,9 @@ struct Dev {
   int npe;                                            // entries of pt_edges
   // per-edge buffers (indexed by edge id)
   double* err; double* w; double* jp; double* jl; double* hpl; double* y; double* chi; double* rchi;
+  // the second linearisation buffer of a device-driven run (null: one buffer): k_edges_end
+  // linearises each trial there, and an accepted trial makes it the iteration's (ctl->jbuf)
+  double* alt_err; double* alt_w; double* alt_jp; double* alt_jl; double* alt_hpl;
   // system
   double* Hpp; double* bp; double* Hll; double* bl; double* Dinv; double* db;
   double* S; double* bs; double* xp;   // S: lower 64x64 tiles (ldlt.hpp), bs / xp: 64 T
@@ -290,6 +295,15 @@ __device__ __forceinline__ double block_sum256(double v) {
 }
 
 __device__ __forceinline__ double lam_of(const Dev& d) { return d.ctl ? d.ctl->lambda : d.lam; }
+// the linearisation buffer a kernel of a device-driven step reads (spec: the one a trial
+// linearises into); host-driven runs have one buffer
+__device__ __forceinline__ Dev lin_buf(const Dev& d, bool spec) {
+  Dev r = d;
+  if (d.ctl && d.alt_err && ((d.ctl->jbuf ^ (spec ? 1 : 0)) & 1)) {
+    r.err = d.alt_err; r.w = d.alt_w; r.jp = d.alt_jp; r.jl = d.alt_jl; r.hpl = d.alt_hpl;
+  }
+  return r;
+}
 __device__ __forceinline__ double lam0_of(const Dev& d) { return d.ctl ? d.ctl->lambda : d.lam0; }
 // a kernel of a device-driven step that is not needed (the loop has ended)
 __device__ __forceinline__ bool lm_done(const Dev& d) { return d.ctl && d.ctl->done; }
@@ -298,9 +312,10 @@ constexpr int kRedNT = 256;   // k_build workgroup (1024 measured slower: 18.3 v
 
 // per active edge: error (+ robust chi2) and optionally Jacobians / weight / Hpl = w Jp^T Jl
 // (device-driven linearisation: only when the previous trial ended an iteration)
-__global__ __launch_bounds__(256) void k_edges(Dev d, int linearize) {
+__global__ __launch_bounds__(256) void k_edges(Dev d0, int linearize) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  if (lm_done(d) || (linearize && d.ctl && !d.ctl->lin)) return;
+  if (lm_done(d0) || (linearize && d0.ctl && !d0.ctl->lin)) return;
+  const Dev d = lin_buf(d0, false);
   if (!linearize && d.part_chi) {   // trial chi2 of a device-driven step: + workgroup partial
     double r0 = 0.0;
     if (k < d.nae) {
@@ -504,26 +519,46 @@ __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
 // and the end of the step in one launch: each workgroup releases its partial and counts itself
 // in; the last one (device-scope counter, agent-scope acquire) closes the step.  A step past
 // the end still publishes its sequence number (workgroup 0), as the host waits for each.
-__global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d, Sum3 q, LmEnd le) {
+__global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d0, Sum3 q, LmEnd le) {
   __shared__ int last;
-  LmCtl* c = d.ctl;
+  LmCtl* c = d0.ctl;
   if (c->done) {
     if (blockIdx.x == 0 && threadIdx.x == 0) lm_publish(c, le);
     return;
   }
+  // with speculative linearisation the trial's error, Jacobians, weight and Hpl go to the
+  // other buffer: if lm_control accepts the trial they are the next iteration's linearisation
+  // (k_edges at the accepted state, the same arithmetic), and no linearising launch is needed
+  const bool spec = c->spec_lin != 0;
+  const Dev d = lin_buf(d0, spec);
   const int k = blockIdx.x * kRedNT + threadIdx.x;
   double r0 = 0.0;
   if (k < d.nae) {
     const int e = d.aedge ? d.aedge[k] : k;
     const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
+    const double* pose = d.poses + 6 * pi;
+    const double* X = d.points + 3 * li;
     double er[2];
-    edge_error(d.poses + 6 * pi, d.points + 3 * li, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
+    edge_error(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
     const double c2 = d.e_info[e] * (er[0] * er[0] + er[1] * er[1]);
     double r1;
     huber(c2, d.delta, d.dsqr, &r0, &r1);
     d.err[2 * e] = er[0]; d.err[2 * e + 1] = er[1];
     d.chi[e] = c2;
     d.rchi[k] = r0;
+    if (spec) {
+      double jp[12], jl[6];
+      edge_jac(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, jp, jl);
+      for (int i = 0; i < 12; i++) d.jp[12 * e + i] = jp[i];
+      for (int i = 0; i < 6; i++) d.jl[6 * e + i] = jl[i];
+      const double w = r1 * d.e_info[e];
+      d.w[e] = w;
+      if (d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
+        for (int a = 0; a < 6; a++)
+          for (int bb = 0; bb < 3; bb++)
+            d.hpl[18 * e + 3 * a + bb] = w * (jp[a] * jl[bb] + jp[6 + a] * jl[3 + bb]);
+      }
+    }
   }
   const double sum = block_sum256(r0);
   if (threadIdx.x == 0) {
@@ -535,7 +570,7 @@ __global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d, Sum3 q, LmEnd le) {
   if (!last) return;
   __threadfence();     // acquire: every workgroup's partial
   if (threadIdx.x == 0) __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
-  lm_end_body(d, q, le);
+  lm_end_body(d0, q, le);
 }
 
 // chi2 of the starting point -> currentChi (the optimize() call's activeRobustChi2)
@@ -587,6 +622,7 @@ __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig) {
       c->ni = 2;
       c->currentChi = tempChi;
       c->restore = 0;
+      if (c->spec_lin) c->jbuf ^= 1;   // the trial's linearisation (k_edges_end) is current
     } else {
       c->lambda *= c->ni;
       c->ni *= 2;
@@ -912,8 +948,9 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
   }
 }
 // both builds in one launch: workgroups [0, np) per pose, the rest four lanes per point
-__global__ __launch_bounds__(kRedNT) void k_build(Dev d) {
-  if (lm_done(d) || (d.ctl && !d.ctl->lin)) return;
+__global__ __launch_bounds__(kRedNT) void k_build(Dev d0) {
+  if (lm_done(d0) || (d0.ctl && !d0.ctl->lin)) return;
+  const Dev d = lin_buf(d0, false);
   if ((int)blockIdx.x < d.np) poses_build_body(d, blockIdx.x);
   else points_build_body<false>(d, blockIdx.x - d.np, true);
 }
@@ -928,8 +965,9 @@ __device__ __forceinline__ void trial_push(const Dev& d, int q, int stride) {
 // One thread per (point, edge) entry of the point CSR: D = Hll + lambda I -> Dinv (cofactors,
 // recomputed per entry: identical bits), Y_e = Hpl_e Dinv; the first entry of each point
 // also stores Dinv and db = Dinv b_l.
-__global__ __launch_bounds__(256) void k_point_trial(Dev d) {
-  if (lm_done(d)) return;
+__global__ __launch_bounds__(256) void k_point_trial(Dev d0) {
+  if (lm_done(d0)) return;
+  const Dev d = lin_buf(d0, false);
   const int q = blockIdx.x * 256 + threadIdx.x;
   trial_push(d, q, gridDim.x * 256);
   if (q >= d.npe) return;
@@ -951,8 +989,9 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d) {
 // one launch -- the point quads go on from their H / b to Dinv, db and Y (same arithmetic,
 // same bits), every thread takes part in the push.  Step 0 keeps the two launches: lambda's
 // initial value needs the built diagonal first.
-__global__ __launch_bounds__(kRedNT) void k_build_trial(Dev d) {
-  if (lm_done(d)) return;
+__global__ __launch_bounds__(kRedNT) void k_build_trial(Dev d0) {
+  if (lm_done(d0)) return;
+  const Dev d = lin_buf(d0, false);
   const bool lin = d.ctl->lin != 0;
   trial_push(d, blockIdx.x * kRedNT + threadIdx.x, gridDim.x * kRedNT);
   if ((int)blockIdx.x < d.np) { if (lin) poses_build_body(d, blockIdx.x); }
@@ -988,8 +1027,9 @@ __device__ __forceinline__ void schur_write(const Dev& d, int bi, int bj, double
 }
 
 
-__global__ __launch_bounds__(256) void k_schur(Dev d) {
-  if (lm_done(d)) return;
+__global__ __launch_bounds__(256) void k_schur(Dev d0) {
+  if (lm_done(d0)) return;
+  const Dev d = lin_buf(d0, false);
   const double lam0 = lam0_of(d);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int it = blockIdx.x * 4 + w;
@@ -1088,8 +1128,9 @@ __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nblk) {
 // x_l = Dinv (b_l - sum_e Hpl_e^T x_p); point = backup + x_l; model-decrease terms:
 // red[k] (points, k < nl) and red[nl + i] (poses) summed separately (poses are replicated
 // across shards, points are not).
-__global__ __launch_bounds__(256) void k_update(Dev d) {
-  if (lm_done(d)) return;
+__global__ __launch_bounds__(256) void k_update(Dev d0) {
+  if (lm_done(d0)) return;
+  const Dev d = lin_buf(d0, false);
   const int gt = blockIdx.x * 256 + threadIdx.x;
   const double lam = lam_of(d);
   double spt = 0.0, sps = 0.0;   // this thread's point / pose model-decrease term
@@ -1306,6 +1347,13 @@ __global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges,
   for (int i = 0; i < 12; i++) d.jp[12 * e + i] = 0.0;
   for (int i = 0; i < 6; i++) d.jl[6 * e + i] = 0.0;
   for (int i = 0; i < 18; i++) { d.hpl[18 * e + i] = 0.0; d.y[18 * e + i] = 0.0; }
+  if (d.alt_err) {   // both linearisation buffers (a later run may flip to either)
+    d.alt_w[e] = 0.0;
+    d.alt_err[2 * e] = 0.0; d.alt_err[2 * e + 1] = 0.0;
+    for (int i = 0; i < 12; i++) d.alt_jp[12 * e + i] = 0.0;
+    for (int i = 0; i < 6; i++) d.alt_jl[6 * e + i] = 0.0;
+    for (int i = 0; i < 18; i++) d.alt_hpl[18 * e + i] = 0.0;
+  }
 }
 
 // the trial's pop (restore every pose and point from the backups) in one launch
@@ -1657,6 +1705,13 @@ struct Optimizer {
     d.npe = (int)s.pt_edges.size();
     d.err = dz(2 * (size_t)NE); d.w = dz(NE); d.jp = dz(12 * (size_t)NE); d.jl = dz(6 * (size_t)NE);
     d.hpl = dz(18 * (size_t)NE); d.y = dz(18 * (size_t)NE); d.chi = dz(NE); d.rchi = dz(NE);
+    // the second linearisation buffer (device-driven runs: speculative linearisation)
+    if (!sharded) {
+      d.alt_err = dz(2 * (size_t)NE); d.alt_w = dz(NE); d.alt_jp = dz(12 * (size_t)NE);
+      d.alt_jl = dz(6 * (size_t)NE); d.alt_hpl = dz(18 * (size_t)NE);
+    } else {
+      d.alt_err = d.alt_w = d.alt_jp = d.alt_jl = d.alt_hpl = nullptr;
+    }
     d.Hpp = dz(36 * (size_t)s.np); d.bp = dz(6 * (size_t)s.np);
     d.Hll = dz(9 * (size_t)s.nl); d.bl = dz(3 * (size_t)s.nl);
     d.Dinv = dz(9 * (size_t)s.nl); d.db = dz(3 * (size_t)s.nl);
@@ -2110,6 +2165,8 @@ struct Optimizer {
     h0.max_iterations = o->max_iterations; h0.max_trials = o->max_trials;
     h0.terminate_max_iter = o->terminate_max_iter;
     h0.lin = 1; h0.ni = 2;
+    h0.spec_lin = d.alt_err ? 1 : 0;   // k_edges_end linearises every trial (see k_edges_end)
+    h0.jbuf = 0;
     const bool empty = (s.np + nl_glob) == 0 || nae_glob == 0;
     h0.done = (empty || o->max_iterations <= 0 || *stop != 0) ? 1 : 0;
     c->lsig->ext_stop = *stop != 0;
@@ -2129,7 +2186,9 @@ struct Optimizer {
       hipLaunchKernelGGL(k_lm_start, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
     }
     auto enqueue_step = [&](int step) -> int {
-      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
+      // the first step linearises at the start; later steps find the accepted trial's
+      // linearisation (k_edges_end) already in place, or keep the iteration's after a reject
+      if (step == 0 || !h0.spec_lin) hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
       const unsigned g_build = (unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT);
       if (step == 0) {   // iteration 0 is always step 0: lambda from the max diagonal
         hipLaunchKernelGGL(k_build, dim3(g_build), dim3(kRedNT), 0, st, dd);
@@ -2149,12 +2208,12 @@ struct Optimizer {
           MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st, skip));
         }
       }
+      LmEnd le{d_scalar, (const int*)d_flag, c->lsig, ++c->lsig_seq};
       hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, dd);
       // the trial's evaluation, then (last workgroup) its three sums from the workgroup
       // partials of k_edges_end / k_update (a fixed order: partials in workgroup order, each a
       // fixed in-workgroup tree), the LM decision and the pop of a rejected trial
       Sum3 q{{dd.part_chi, dd.part_pt, dd.part_ps}, {(int)g_edg, (int)g_upd, (int)g_upd}};
-      LmEnd le{d_scalar, (const int*)d_flag, c->lsig, ++c->lsig_seq};
       hipLaunchKernelGGL(k_edges_end, dim3(g_edg), dim3(kRedNT), 0, st, dd, q, le);
       return hipGetLastError() == hipSuccess ? MCS_OK : MCS_ERR_HIP;
     };
