@@ -1193,103 +1193,56 @@ __global__ __launch_bounds__(256) void k_update(Dev d0) {
 // edges of P1 x the edges of P2 in edge order; points in order; then a stable radix sort by
 // block id (rocPRIM) makes the lists block-major with that order kept inside every block.
 
-// A point's active-pose edges as (pose, edge) sorted by pose, stable (edge order inside a
-// pose), in a private array; more than kPairK of them take the slow path below.
-constexpr int kPairK = 48;
-__device__ __forceinline__ int point_groups(const Dev& d, int l, int* hs, int* es) {
-  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
-  int k = 0;
-  for (int q = q0; q < q1; q++) {
-    const int h = d.pt_h[q];
-    if (h < 0) continue;
-    if (k == kPairK) return -1;
-    int i = k++;
-    while (i > 0 && hs[i - 1] > h) { hs[i] = hs[i - 1]; es[i] = es[i - 1]; i--; }
-    hs[i] = h;
-    es[i] = d.pt_edges[q];
-  }
-  return k;
+// The pairs of a point are {(a, b) : h(a) >= h(b) >= 0} over its active edges; after the
+// stable sort by block id only their order INSIDE a block matters, and there it is (a, b) in
+// edge order -- exactly the order of the plain double loop over the point's edges (pt_edges is
+// in edge order).  So every (point, edge a) entry counts and emits its own pairs in b order,
+// one thread per entry, at the offset the scan over the entries gives it: no per-point sort.
+__device__ __forceinline__ void entry_range(const Dev& d, int q, int* q0, int* q1) {
+  const int l = d.point_h[d.e_point[d.pt_edges[q]]];
+  *q0 = d.pt_ptr[l];
+  *q1 = d.pt_ptr[l + 1];
 }
-
-// pairs a point contributes: #{(a, b) : h(a) >= h(b) >= 0} over its active edges
 __global__ __launch_bounds__(256) void k_pair_count(Dev d, int32_t* cnt) {
-  const int l = blockIdx.x * 256 + threadIdx.x;
-  if (l > d.nl) return;
-  if (l == d.nl) { cnt[l] = 0; return; }   // the scan's total slot
-  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q > d.npe) return;
+  if (q == d.npe) { cnt[q] = 0; return; }   // the scan's total slot
+  const int ha = d.pt_h[q];
   int n = 0;
-  for (int a = q0; a < q1; a++) {
-    const int ha = d.pt_h[a];
-    if (ha < 0) continue;
+  if (ha >= 0) {
+    int q0, q1;
+    entry_range(d, q, &q0, &q1);
     for (int b = q0; b < q1; b++) {
       const int hb = d.pt_h[b];
       n += (hb >= 0 && hb <= ha) ? 1 : 0;
     }
   }
-  cnt[l] = n;
+  cnt[q] = n;
 }
 
 __global__ __launch_bounds__(256) void k_pair_emit(Dev d, const int32_t* off, uint32_t* keys,
                                                    uint2* vals, int64_t pmax, uint32_t pad_key) {
   const int64_t gt = (int64_t)blockIdx.x * 256 + threadIdx.x;
   // padding past the last pair: a key above every block, sorted to the end
-  const int64_t total = off[d.nl];
+  const int64_t total = off[d.npe];
   for (int64_t q = total + gt; q < pmax; q += (int64_t)gridDim.x * 256) {
     keys[q] = pad_key;
     vals[q] = make_uint2(0u, 0u);
   }
-  const int l = (int)gt;
-  if (l >= d.nl) return;
-  int64_t o = off[l];
-  int hs[kPairK], es[kPairK];
-  const int k = point_groups(d, l, hs, es);
-  if (k >= 0) {
-    for (int i0 = 0; i0 < k;) {          // group gi = [i0, i1) of pose P1
-      int i1 = i0 + 1;
-      while (i1 < k && hs[i1] == hs[i0]) i1++;
-      const int P1 = hs[i0];
-      for (int j0 = 0; j0 <= i0;) {      // group gj = [j0, j1) of pose P2 <= P1
-        int j1 = j0 + 1;
-        while (j1 < k && hs[j1] == hs[j0]) j1++;
-        const uint32_t blk = (uint32_t)((int64_t)P1 * (P1 + 1) / 2 + hs[j0]);
-        for (int a = i0; a < i1; a++)
-          for (int b = j0; b < j1; b++) {
-            keys[o] = blk;
-            vals[o] = make_uint2((uint32_t)es[a], (uint32_t)es[b]);
-            o++;
-          }
-        j0 = j1;
-      }
-      i0 = i1;
-    }
-    return;
-  }
-  // more than kPairK active edges: the same order from repeated minimum searches
-  const int q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
-  int p1 = -1;
-  for (;;) {   // distinct active poses of the point, ascending
-    int P1 = 0x7FFFFFFF;
-    for (int a = q0; a < q1; a++) { const int h = d.pt_h[a]; if (h > p1 && h < P1) P1 = h; }
-    if (P1 == 0x7FFFFFFF) break;
-    int p2 = -1;
-    for (;;) {
-      int P2 = 0x7FFFFFFF;
-      for (int b = q0; b < q1; b++) { const int h = d.pt_h[b]; if (h > p2 && h <= P1 && h < P2) P2 = h; }
-      if (P2 == 0x7FFFFFFF) break;
-      const uint32_t blk = (uint32_t)((int64_t)P1 * (P1 + 1) / 2 + P2);
-      for (int a = q0; a < q1; a++) {
-        if (d.pt_h[a] != P1) continue;
-        const uint32_t ea = (uint32_t)d.pt_edges[a];
-        for (int b = q0; b < q1; b++) {
-          if (d.pt_h[b] != P2) continue;
-          keys[o] = blk;
-          vals[o] = make_uint2(ea, (uint32_t)d.pt_edges[b]);
-          o++;
-        }
-      }
-      p2 = P2;
-    }
-    p1 = P1;
+  const int q = (int)gt;
+  if (q >= d.npe) return;
+  const int ha = d.pt_h[q];
+  if (ha < 0) return;
+  int q0, q1;
+  entry_range(d, q, &q0, &q1);
+  const uint32_t ea = (uint32_t)d.pt_edges[q];
+  int64_t o = off[q];
+  for (int b = q0; b < q1; b++) {
+    const int hb = d.pt_h[b];
+    if (hb < 0 || hb > ha) continue;
+    keys[o] = (uint32_t)((int64_t)ha * (ha + 1) / 2 + hb);
+    vals[o] = make_uint2(ea, (uint32_t)d.pt_edges[b]);
+    o++;
   }
 }
 
@@ -1720,12 +1673,14 @@ struct Optimizer {
     d.xp = dz((size_t)ldlt::TB * T);
     d.red = dz((size_t)NE + 6 * (size_t)s.np + s.nl + 16);
     // bounds of the device-built pair lists / items: a point with k active edges gives at most
-    // k (k + 1) / 2 pairs; a block at most 1 + pairs / CH + pose edges / CH chunks
+    // k^2 pairs (k (k + 1) / 2 when its edges have distinct poses, as the reference's one
+    // observation per keyframe makes them; the C-ABI takes any graph); a block at most
+    // 1 + pairs / CH + pose edges / CH chunks
     nblk = s.np * (s.np + 1) / 2;
     pmax = 0;
     for (int l = 0; l < s.nl; l++) {
       const int64_t k = s.pt_ptr[l + 1] - s.pt_ptr[l];
-      pmax += k * (k + 1) / 2;
+      pmax += k * k;
     }
     if (pmax > INT32_MAX) { set_error("BA: more than 2^31 Schur pairs"); return MCS_ERR_UNSUPPORTED; }
     items_max = (int)std::min<int64_t>(INT32_MAX, 2 * (int64_t)nblk + pmax / kSchurChunk +
@@ -1767,8 +1722,9 @@ struct Optimizer {
   // The Schur pair lists and k_schur items, built on the device (the kernels above), stream
   // ordered after the upload: nothing is read back.
   int enqueue_pairs() {
-    int32_t* cnt = (int32_t*)c->alloc(4 * (size_t)(s.nl + 1));
-    int32_t* off = (int32_t*)c->alloc(4 * (size_t)(s.nl + 1));
+    const int npe = (int)s.pt_edges.size();
+    int32_t* cnt = (int32_t*)c->alloc(4 * (size_t)(npe + 1));
+    int32_t* off = (int32_t*)c->alloc(4 * (size_t)(npe + 1));
     uint32_t* k_in = (uint32_t*)c->alloc(4 * (size_t)std::max<int64_t>(1, pmax));
     uint32_t* k_out = (uint32_t*)c->alloc(4 * (size_t)std::max<int64_t>(1, pmax));
     uint2* v_in = (uint2*)c->alloc(8 * (size_t)std::max<int64_t>(1, pmax));
@@ -1791,7 +1747,7 @@ struct Optimizer {
     const unsigned bits = nblk > 0 ? 32u - (unsigned)__builtin_clz((unsigned)nblk) : 1u;
     size_t b_scan1 = 0, b_scan2 = 0, b_sort = 0;
     auto plus = rocprim::plus<int32_t>();
-    MCS_HIP_CHECK(rocprim::exclusive_scan(nullptr, b_scan1, cnt, off, 0, (size_t)s.nl + 1, plus, st));
+    MCS_HIP_CHECK(rocprim::exclusive_scan(nullptr, b_scan1, cnt, off, 0, (size_t)npe + 1, plus, st));
     MCS_HIP_CHECK(rocprim::exclusive_scan(nullptr, b_scan2, nch, it_off, 0, (size_t)nblk + 1, plus, st));
     if (pmax > 0)
       MCS_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, b_sort, k_in, k_out, v_in, v_out, (size_t)pmax, 0u, bits, st));
@@ -1799,10 +1755,10 @@ struct Optimizer {
     void* tmp = c->alloc(tb);
     if (!tmp) { set_error("BA: out of device memory (scan storage)"); return MCS_ERR_HIP; }
     size_t b = tb;
-    hipLaunchKernelGGL(k_pair_count, dim3(gb(s.nl + 1)), dim3(256), 0, st, d, cnt);
-    MCS_HIP_CHECK(rocprim::exclusive_scan(tmp, b, cnt, off, 0, (size_t)s.nl + 1, plus, st));
+    hipLaunchKernelGGL(k_pair_count, dim3(gb(npe + 1)), dim3(256), 0, st, d, cnt);
+    MCS_HIP_CHECK(rocprim::exclusive_scan(tmp, b, cnt, off, 0, (size_t)npe + 1, plus, st));
     if (pmax > 0) {
-      const unsigned g = std::max(gb(s.nl), std::min(gb((int)std::min<int64_t>(pmax, INT32_MAX)), 4096u));
+      const unsigned g = std::max(gb(npe), std::min(gb((int)std::min<int64_t>(pmax, INT32_MAX)), 4096u));
       hipLaunchKernelGGL(k_pair_emit, dim3(g), dim3(256), 0, st, d, (const int32_t*)off, k_in, v_in, pmax,
                          (uint32_t)nblk);
       b = tb;
