@@ -2135,16 +2135,24 @@ struct Optimizer {
     dd.part_pt = dz(g_upd);
     dd.part_ps = dz(g_upd);
     if (he != hipSuccess) { set_hip_error(he, "BA partials", __FILE__, __LINE__); return MCS_ERR_HIP; }
-    if (!empty) {   // chi2 of the starting point (activeRobustChi2 before the first iteration)
-      Dev d0 = d;
-      hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d0, 0);
+    // the starting point's chi2 (activeRobustChi2 before the first iteration): from step 0's
+    // linearising pass when the loop will run (the same errors), else a plain evaluation
+    const bool lin0 = !empty && !h0.done;
+    if (!empty) {
+      if (lin0) {
+        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
+      } else {
+        Dev d0 = d;
+        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d0, 0);
+      }
       reduce_dev<false>(d.rchi, d.nae, d_scalar, d_part, st);
       hipLaunchKernelGGL(k_lm_start, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
     }
     auto enqueue_step = [&](int step) -> int {
       // the first step linearises at the start; later steps find the accepted trial's
       // linearisation (k_edges_end) already in place, or keep the iteration's after a reject
-      if (step == 0 || !h0.spec_lin) hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
+      if ((step == 0 && !lin0) || (step > 0 && !h0.spec_lin))
+        hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
       const unsigned g_build = (unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT);
       if (step == 0) {   // iteration 0 is always step 0: lambda from the max diagonal
         hipLaunchKernelGGL(k_build, dim3(g_build), dim3(kRedNT), 0, st, dd);
