@@ -805,6 +805,54 @@ __global__ __launch_bounds__(512) void k_tri_seq(
       const int q = __builtin_amdgcn_readlane(cur.x, i);
       const int o = __builtin_amdgcn_readlane(cur.y, i);
       const int c = __builtin_amdgcn_readlane(cur.z, i);
+      // Two short queries at once, one per 32-lane half, from one key read and one vbMatched2
+      // read: the second decides on the first's state plus the first's winner (its bit is
+      // cleared from the second's unmatched keys before its own best is taken), which is the
+      // sequential order.  Both must lie in the two resident windows.
+      if (todo && c > 0 && c <= 32) {
+        const int j = first_lane(todo);
+        const int c2 = __builtin_amdgcn_readlane(cur.z, j);
+        const int o2 = __builtin_amdgcn_readlane(cur.y, j);
+        if (c2 > 0 && c2 <= 32 && o2 + c2 - o <= kTriWin) {
+          todo &= todo - 1;
+          const int q2 = __builtin_amdgcn_readlane(cur.x, j);
+          ensure(o);
+          const bool hi = lane >= 32;
+          const int li = lane & 31;
+          const bool valid = li < (hi ? c2 : c);
+          const uint32_t key = valid ? key_at((hi ? o2 : o) + li) : 0u;
+          const uint32_t kid = key & 0xFFFFFu;
+          const bool unm = valid && !is_matched(kid);
+          const uint64_t bu = __ballot(unm);
+          uint32_t w1 = 0xFFFFFFFFu, w2 = 0xFFFFFFFFu;
+          const uint64_t b1 = bu & 0xFFFFFFFFull;
+          if (b1) {
+            const uint32_t best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b1)) & kTriKey;
+            const uint32_t th = 2u * (best >> 20);
+            const uint64_t bo = __ballot(!hi && unm && (key & kTriPass) && ((key & kTriKey) >> 20) <= th);
+            if (bo) w1 = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(bo)) & kTriKey;
+          }
+          const uint32_t r1k = w1 != 0xFFFFFFFFu ? (w1 & 0xFFFFFu) : 0xFFFFFFFFu;
+          const bool unm2 = hi && unm && kid != r1k;
+          const uint64_t b2 = __ballot(unm2);
+          if (b2) {
+            const uint32_t best = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(b2)) & kTriKey;
+            const uint32_t th = 2u * (best >> 20);
+            const uint64_t bo = __ballot(unm2 && (key & kTriPass) && ((key & kTriKey) >> 20) <= th);
+            if (bo) w2 = (uint32_t)__builtin_amdgcn_readlane((int)key, first_lane(bo)) & kTriKey;
+          }
+          const int r1 = w1 != 0xFFFFFFFFu ? (int)(w1 & 0xFFFFFu) : -1;
+          const int r2 = w2 != 0xFFFFFFFFu ? (int)(w2 & 0xFFFFFu) : -1;
+          if (lane == 0) {
+            m12[q] = r1;
+            m12[q2] = r2;
+            if (r1 >= 0) atomicOr(&matched2[r1 >> 5], 1u << (r1 & 31));
+            if (r2 >= 0) atomicOr(&matched2[r2 >> 5], 1u << (r2 & 31));
+          }
+          nm += (r1 >= 0) + (r2 >= 0);
+          continue;
+        }
+      }
       uint32_t wkey = 0xFFFFFFFFu;
       if (c > 0) {
         ensure(o);
