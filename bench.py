@@ -734,6 +734,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--multiframes", type=int, default=171, help="multi-frames per rank per step")
+    ap.add_argument("--split", type=int, default=2,
+                    help="2: extract the step's two halves on two streams, matching the first "
+                         "half beside the second's extraction (3: the second half starts after "
+                         "the first)")
     ap.add_argument("--unique", type=int, default=12, help="distinct rendered multi-frames")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--cpu-sample", type=int, default=12, help="multi-frames timed on the CPU")
@@ -802,17 +806,54 @@ def main():
 
     ev_m0 = torch.cuda.Event(enable_timing=True)
     ev_m1 = torch.cuda.Event(enable_timing=True)
+    # --split 2: the batch as two halves of multi-frames, each with its own extractor (its own
+    # workspace) on its own stream; the first half's pairs are matched as soon as it is
+    # extracted (MFMA work beside the second half's VALU-bound extraction), the second half's
+    # pairs (the boundary pair included) after both.  Same kernels, same outputs.
+    split = args.split > 1 and M >= 4
+    if split:
+        MA = M // 2
+        FA, FB = MA * NC, F - MA * NC
+        NPA = (MA - 1) * NC
+        ex2 = mcs_amd.Extractor(params, W, H, max_frames=FB, device=local_rank)
+        ex2.set_masks_device(d_mask.data_ptr(), NC, stream.cuda_stream)
+        s2 = torch.cuda.Stream(device=dev)
+        ev_a, ev_b, ev_go = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
 
-    def step(timed):
+    def match(p0, n, st):
+        rc = L.mcs_hamming_top2_batch_device(d_desc.data_ptr(), d_cnt.data_ptr(),
+                                             d_pairs.data_ptr() + 8 * p0, n, cap, 32,
+                                             *[t.data_ptr() + 4 * p0 * cap for t in d_m], st)
+        if rc != 0:
+            raise RuntimeError("matcher failed %d" % rc)
+
+    def step(timed, allow_split=True):
+        if split and allow_split:
+            ev_go.record(stream)
+            s2.wait_event(ev_go)
+            ex.extract_batch_device(d_img.data_ptr(), FA, d_midx.data_ptr(), d_kps.data_ptr(),
+                                    d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
+            ev_a.record(stream)
+            if args.split == 3:   # staggered: B's extraction starts once A's is done
+                s2.wait_event(ev_a)
+            ex2.extract_batch_device(d_img.data_ptr() + FA * W * H, FB, d_midx.data_ptr() + 4 * FA,
+                                     d_kps.data_ptr() + 4 * FA * cap * 7, d_cnt.data_ptr() + 4 * FA,
+                                     d_desc.data_ptr() + FA * cap * 32, s2.cuda_stream)
+            if timed:
+                ev_m0.record(stream)
+            match(0, NPA, stream.cuda_stream)
+            s2.wait_event(ev_a)
+            match(NPA, NP - NPA, s2.cuda_stream)
+            ev_b.record(s2)
+            stream.wait_event(ev_b)
+            if timed:
+                ev_m1.record(stream)
+            return
         ex.extract_batch_device(d_img.data_ptr(), F, d_midx.data_ptr(), d_kps.data_ptr(),
                                 d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
         if timed:
             ev_m0.record(stream)
-        rc = L.mcs_hamming_top2_batch_device(d_desc.data_ptr(), d_cnt.data_ptr(),
-                                             d_pairs.data_ptr(), NP, cap, 32,
-                                             *[t.data_ptr() for t in d_m], stream.cuda_stream)
-        if rc != 0:
-            raise RuntimeError("matcher failed %d" % rc)
+        match(0, NP, stream.cuda_stream)
         if timed:
             ev_m1.record(stream)
 
@@ -837,7 +878,7 @@ def main():
     if args.stage_timing:
         ex.enable_timing(True)
         for _ in range(max(2, min(5, args.steps))):
-            step(False)
+            step(False, False)   # the stages back to back on one stream, the whole batch
         torch.cuda.synchronize()
         stages, ncalls = ex.read_timing()
         ex.enable_timing(False)
@@ -947,7 +988,10 @@ def main():
                        "camera_frames_per_step_per_gpu": F,
                        "keypoints_per_step_per_gpu": kp_per_step,
                        "match_pairs_per_step_per_gpu": NP,
-                       "parallelism": "dp%d (independent multi-frame segments)" % world},
+                       "parallelism": "dp%d (independent multi-frame segments)" % world,
+                       "schedule": ("two halves of the step's multi-frames on two streams "
+                                    "(two extractors), each half's pairs matched after it"
+                                    if split else "one stream")},
             "roofline": roofline,
             "roofline_orient_desc": roofline_od,
             "roofline_octree": roofline_oct,
