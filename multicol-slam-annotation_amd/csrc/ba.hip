@@ -463,30 +463,34 @@ __device__ __forceinline__ void lm_publish(const LmCtl* c, const LmEnd& le) {
   __hip_atomic_store(&le.sig->iter, c->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&le.sig->seq, le.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// (blockDim >= 256: threads past 256 only take part in the barriers)
 __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
   static_assert(kRedNT == 256, "the tree below folds 1024 slots onto 256 threads");
   __shared__ double s[3][256];
   __shared__ int rej;
   LmCtl* c = d.ctl;
   const int t = threadIdx.x;
+  const bool act = t < 256;
   // slot ts = t + 256 u (u = 0..3) sums v[ts], v[ts + 1024], ... in order; the tree levels 512
   // and 256 (s[ts] += s[ts + o]) pair slots of one thread, so they run in registers; 128 and 64
   // cross waves (LDS); 32 .. 1 stay in wave 0 (shuffles).  Same additions in the same order.
   double a[3];
+  if (act) {
 #pragma unroll
-  for (int b = 0; b < 3; b++) {
-    const double* v = q.v[b];
-    double x[4];
+    for (int b = 0; b < 3; b++) {
+      const double* v = q.v[b];
+      double x[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      double acc = 0.0;
-      for (int i = t + 256 * u; i < q.n[b]; i += 1024) acc = acc + v[i];
-      x[u] = acc;
+      for (int u = 0; u < 4; u++) {
+        double acc = 0.0;
+        for (int i = t + 256 * u; i < q.n[b]; i += 1024) acc = acc + v[i];
+        x[u] = acc;
+      }
+      x[0] = x[0] + x[2];   // o = 512
+      x[1] = x[1] + x[3];
+      a[b] = x[0] + x[1];   // o = 256
+      s[b][t] = a[b];
     }
-    x[0] = x[0] + x[2];   // o = 512
-    x[1] = x[1] + x[3];
-    a[b] = x[0] + x[1];   // o = 256
-    s[b][t] = a[b];
   }
   __syncthreads();
   if (t < 128)
@@ -508,7 +512,7 @@ __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
     rej = c->restore;
   }
   __syncthreads();
-  if (rej) {   // pop: every pose and point back to the backups of the trial's push
+  if (rej && act) {   // pop: every pose and point back to the backups of the trial's push
     for (int i = t; i < d.n_pose_dbl; i += kRedNT) d.poses[i] = d.push_poses[i];
     for (int i = t; i < d.n_point_dbl; i += kRedNT) d.points[i] = d.push_points[i];
   }
@@ -519,8 +523,15 @@ __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
 // and the end of the step in one launch: each workgroup releases its partial and counts itself
 // in; the last one (device-scope counter, agent-scope acquire) closes the step.  A step past
 // the end still publishes its sequence number (workgroup 0), as the host waits for each.
-__global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d0, Sum3 q, LmEnd le) {
+// A workgroup holds 256 edges and 512 threads: waves 0-3 evaluate the error / robust chi2 / weight
+// of edge k (slot t), waves 4-7 its Jacobians (speculative linearisation), the two independent
+// halves of one edge's dependent chain side by side; Hpl = w Jp^T Jl follows once the weight
+// has crossed over in LDS.  Every value is the single-thread form's, bit for bit.
+constexpr int kEdgeEndNT = 512;
+__global__ __launch_bounds__(kEdgeEndNT) void k_edges_end(Dev d0, Sum3 q, LmEnd le) {
   __shared__ int last;
+  __shared__ double wsh[256];
+  __shared__ double sm[4];
   LmCtl* c = d0.ctl;
   if (c->done) {
     if (blockIdx.x == 0 && threadIdx.x == 0) lm_publish(c, le);
@@ -531,45 +542,66 @@ __global__ __launch_bounds__(kRedNT) void k_edges_end(Dev d0, Sum3 q, LmEnd le) 
   // (k_edges at the accepted state, the same arithmetic), and no linearising launch is needed
   const bool spec = c->spec_lin != 0;
   const Dev d = lin_buf(d0, spec);
-  const int k = blockIdx.x * kRedNT + threadIdx.x;
+  const int slot = threadIdx.x & 255;
+  const bool jac = threadIdx.x >= 256;   // wave-uniform
+  const int k = blockIdx.x * 256 + slot;
   double r0 = 0.0;
+  int e = 0, pi = 0, li = 0, ci = 0;
+  double jp[12], jl[6];
   if (k < d.nae) {
-    const int e = d.aedge ? d.aedge[k] : k;
-    const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
+    e = d.aedge ? d.aedge[k] : k;
+    pi = d.e_pose[e]; li = d.e_point[e]; ci = d.e_cam[e];
     const double* pose = d.poses + 6 * pi;
     const double* X = d.points + 3 * li;
-    double er[2];
-    edge_error(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
-    const double c2 = d.e_info[e] * (er[0] * er[0] + er[1] * er[1]);
-    double r1;
-    huber(c2, d.delta, d.dsqr, &r0, &r1);
-    d.err[2 * e] = er[0]; d.err[2 * e + 1] = er[1];
-    d.chi[e] = c2;
-    d.rchi[k] = r0;
-    if (spec) {
-      double jp[12], jl[6];
+    if (!jac) {
+      double er[2];
+      edge_error(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
+      const double c2 = d.e_info[e] * (er[0] * er[0] + er[1] * er[1]);
+      double r1;
+      huber(c2, d.delta, d.dsqr, &r0, &r1);
+      d.err[2 * e] = er[0]; d.err[2 * e + 1] = er[1];
+      d.chi[e] = c2;
+      d.rchi[k] = r0;
+      if (spec) {
+        const double w = r1 * d.e_info[e];
+        d.w[e] = w;
+        wsh[slot] = w;
+      }
+    } else if (spec) {
       edge_jac(pose, X, d.mc + 6 * ci, d.cam + 17 * ci, jp, jl);
       for (int i = 0; i < 12; i++) d.jp[12 * e + i] = jp[i];
       for (int i = 0; i < 6; i++) d.jl[6 * e + i] = jl[i];
-      const double w = r1 * d.e_info[e];
-      d.w[e] = w;
-      if (d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
-        for (int a = 0; a < 6; a++)
-          for (int bb = 0; bb < 3; bb++)
-            d.hpl[18 * e + 3 * a + bb] = w * (jp[a] * jl[bb] + jp[6 + a] * jl[3 + bb]);
-      }
     }
   }
-  const double sum = block_sum256(r0);
+  __syncthreads();
+  if (jac && spec && k < d.nae && d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
+    const double w = wsh[slot];
+    for (int a = 0; a < 6; a++)
+      for (int bb = 0; bb < 3; bb++)
+        d.hpl[18 * e + 3 * a + bb] = w * (jp[a] * jl[bb] + jp[6 + a] * jl[3 + bb]);
+  }
+  // block_sum256 over the error waves (0-3): the same butterfly and wave order
+  {
+    double v = r0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (!jac && (threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    d.part_chi[blockIdx.x] = sum;
+    d.part_chi[blockIdx.x] = ((sm[0] + sm[1]) + sm[2]) + sm[3];
     __threadfence();   // release the partial before counting in
     last = atomicAdd(&c->arrive, 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();     // acquire: every workgroup's partial
-  if (threadIdx.x == 0) __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
+  // acquire: every workgroup's partial (one lane; the barrier holds the rest until it is done)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
+  }
+  __syncthreads();
   lm_end_body(d0, q, le);
 }
 
@@ -1291,10 +1323,7 @@ __global__ __launch_bounds__(256) void k_block_items(int nblk, const int32_t* nc
 
 // edges that left the active set (LocalBA culling, Optimizer::remask): zero every per-edge term
 // a build kernel reads, so their contributions to Hll / b_l / Hpp / b_p / Schur are exact zeros
-__global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges, int n) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= n) return;
-  const int e = edges[k];
+__device__ __forceinline__ void zero_edge_terms(const Dev& d, int e) {
   d.w[e] = 0.0;
   d.err[2 * e] = 0.0; d.err[2 * e + 1] = 0.0;
   for (int i = 0; i < 12; i++) d.jp[12 * e + i] = 0.0;
@@ -1307,6 +1336,125 @@ __global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges,
     for (int i = 0; i < 6; i++) d.alt_jl[6 * e + i] = 0.0;
     for (int i = 0; i < 18; i++) d.alt_hpl[18 * e + i] = 0.0;
   }
+}
+__global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges, int n) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  zero_edge_terms(d, edges[k]);
+}
+
+// ---- LocalBA's culling on the device (mcs_local_ba_ex) -----------------------------------
+// The culling passes of LocalBundleAdjustment (src/cOptimizer.cpp:798-817 after round 1,
+// :830-849 after round 2) walk the edges in vpEdges order with per-point state: observations
+// left and the bad flag EraseObservation raises below two (src/cMapPoint.cpp:120-152).  A
+// point's decisions depend only on its own edges, in edge order, so one thread per active point
+// walks its point-CSR list (pt_edges is in edge order and, in round 1, holds every edge of the
+// point) and decides exactly as the sequential pass does.  Round 1 also moves the culled edges to
+// level 1 and zeroes their per-edge terms (what Optimizer::remask's k_zero_edges does); then one
+// workgroup compacts the active-edge list and checks that no active pose lost all its edges
+// (g2o would drop it from the system: the host then rebuilds from scratch).
+struct LbaState {
+  int32_t* obs_left; int32_t* edges_left; int32_t* edges_all;   // per point vertex
+  uint8_t* bad;                                                  // per point vertex
+  uint8_t* inlier; uint8_t* level;                               // per edge
+  const int32_t* extra;                                          // extra observations (nullable)
+  double* chi;                                                   // chi2 of every edge
+  double k2;                                                     // thHuber^2
+  int32_t* keep;                                                 // compacted active list
+  int32_t* res;                                                  // {nae, pose_left, nl_left}
+  uint8_t* pwrite;                                               // per point vertex (round 2)
+};
+
+__global__ __launch_bounds__(256) void k_lba_cull(Dev d, LbaState L, int round1) {
+  const int l = blockIdx.x * 256 + threadIdx.x;
+  if (l >= d.nl) return;
+  const int v = d.hpt_vtx[l], q0 = d.pt_ptr[l], q1 = d.pt_ptr[l + 1];
+  int ol, el;
+  bool bad;
+  if (round1) {
+    el = q1 - q0;
+    ol = el + (L.extra ? L.extra[v] : 0);
+    bad = false;
+    L.edges_all[v] = el;
+  } else {
+    ol = L.obs_left[v]; el = L.edges_left[v]; bad = L.bad[v] != 0;
+  }
+  for (int q = q0; q < q1; q++) {
+    const int e = d.pt_edges[q];
+    if (!L.inlier[e] || bad || !(L.chi[e] > L.k2)) continue;
+    L.inlier[e] = 0;
+    if (round1) { L.level[e] = 1; zero_edge_terms(d, e); }
+    el--;
+    if (--ol < 2) bad = true;
+  }
+  L.obs_left[v] = ol; L.edges_left[v] = el; L.bad[v] = bad ? 1 : 0;
+  // cOptimizer.cpp:885-902: not bad, TotalNrObservations() > 1, >= 2 vertex edges
+  if (!round1 && L.pwrite) L.pwrite[v] = !bad && el > 1 && L.edges_all[v] >= 2;
+}
+
+// the culling state before round 1: every edge an inlier at level 0, every point vertex clear
+__global__ __launch_bounds__(256) void k_lba_init(LbaState L, int ne, int npt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < ne) { L.inlier[i] = 1; L.level[i] = 0; }
+  if (i < npt) {
+    L.obs_left[i] = 0; L.edges_left[i] = 0; L.edges_all[i] = 0; L.bad[i] = 0;
+    if (L.pwrite) L.pwrite[i] = 0;
+  }
+}
+
+// exclusive prefix of v over a 1024-thread workgroup (and the total)
+__device__ __forceinline__ int block_excl_scan1024(int v, int* sm, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sm[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int t = sm[k];
+    base += k < w ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// the round-2 active list in edge order (stable), per-pose survivors, active points left
+__global__ __launch_bounds__(1024) void k_lba_compact(Dev d, LbaState L) {
+  __shared__ int hist[2048];
+  __shared__ int sm[16];
+  const int t = threadIdx.x, n = d.nae;
+  for (int h = t; h < d.np; h += 1024) hist[h] = 0;
+  __syncthreads();
+  const int chunk = (n + 1023) / 1024, k0 = min(n, t * chunk), k1 = min(n, k0 + chunk);
+  int cnt = 0;
+  for (int k = k0; k < k1; k++) {
+    const int e = d.aedge ? d.aedge[k] : k;
+    if (L.level[e]) continue;
+    cnt++;
+    const int h = d.pose_h[d.e_pose[e]];
+    if (h >= 0) atomicAdd(&hist[h], 1);
+  }
+  int total;
+  int o = block_excl_scan1024(cnt, sm, &total);
+  for (int k = k0; k < k1; k++) {
+    const int e = d.aedge ? d.aedge[k] : k;
+    if (!L.level[e]) L.keep[o++] = e;
+  }
+  int nl = 0;
+  for (int l = t; l < d.nl; l += 1024) nl += L.edges_left[d.hpt_vtx[l]] > 0 ? 1 : 0;
+  int left = 0;
+  for (int h = t; h < d.np; h += 1024) left |= hist[h] == 0 ? 1 : 0;
+  int nl_tot, left_any;
+  (void)block_excl_scan1024(nl, sm, &nl_tot);
+  (void)block_excl_scan1024(left, sm, &left_any);
+  if (t == 0) { L.res[0] = total; L.res[1] = left_any > 0 ? 1 : 0; L.res[2] = nl_tot; }
 }
 
 // the trial's pop (restore every pose and point from the backups) in one launch
@@ -1514,6 +1662,16 @@ struct Optimizer {
   unsigned g_state = 1;
   bool sig_path = false;
   hipError_t he = hipSuccess;
+  // LocalBA culling on the device (mcs_local_ba_ex with the device-driven LM): set lba and
+  // lba_extra before setup(); lba_tail picks what run_device does after the LM loop
+  bool lba = false;
+  const int32_t* lba_extra = nullptr;
+  LbaState L{};
+  int lba_tail = 0;   // 0 download; 1 round 1: cull + compaction, no download; 2 round 2: cull +
+                      // results; 3 round 2 without the cull (empty graph)
+  int32_t lba_res[3] = {0, 0, 0};   // round 1: active edges left, a pose left the system, points left
+  uint8_t* lba_inlier_out = nullptr;
+  uint8_t* lba_pwrite_out = nullptr;
 
   Optimizer(mcs_ba_ctx* c_, const mcs_ba_problem* p_, bool pf) : c(c_), p(p_), points_fixed(pf), s(c_->hs) {
     std::memset(&d, 0, sizeof(d));
@@ -1554,12 +1712,12 @@ struct Optimizer {
     if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
     HostClock hc;
     c->host_calls++;
-    for (int e = 0; e < p->n_edges; e++) {
-      if (p->edge_pose[e] < 0 || p->edge_pose[e] >= p->n_poses || p->edge_point[e] < 0 ||
-          p->edge_point[e] >= p->n_points || p->edge_cam[e] < 0 || p->edge_cam[e] >= p->n_cams) {
-        set_error("edge vertex index out of range");
-        return MCS_ERR_ARG;
-      }
+    // ---- structure, pass 1: the index checks, the active edges and their per-pose / per-point
+    // counts (+ active point / edge counts), all-reduced over the shards below
+    std::vector<double> cnt;
+    if (!scan_edges(*p, edge_level, points_fixed, s, cnt)) {
+      set_error("edge vertex index out of range");
+      return MCS_ERR_ARG;
     }
     MCS_HIP_CHECK(hipSetDevice(c->device));
     if (shard_in && shard_in->world > 1) {
@@ -1579,26 +1737,11 @@ struct Optimizer {
       sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
       if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
     }
-    // ---- structure: global pose activity (+ active point / edge counts)
+    // ---- global pose activity (+ active point / edge counts)
     int rc;
-    std::vector<double> cnt((size_t)p->n_poses + 2, 0.0);
-    {
-      int nae_l = 0;
-      std::vector<char> pt_seen(points_fixed ? 0 : p->n_points, 0);
-      int nl_l = 0;
-      for (int e = 0; e < p->n_edges; e++) {
-        if (edge_level && edge_level[e]) continue;
-        if (points_fixed && p->pose_fixed[p->edge_pose[e]]) continue;   // all vertices fixed
-        cnt[p->edge_pose[e]] += 1.0;
-        nae_l++;
-        if (!points_fixed && !pt_seen[p->edge_point[e]]) { pt_seen[p->edge_point[e]] = 1; nl_l++; }
-      }
-      cnt[p->n_poses] = nl_l;
-      cnt[p->n_poses + 1] = nae_l;
-      if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
-    }
+    if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
     hc.mark(c->host_ms, 0);
-    build_structure(*p, edge_level, points_fixed, cnt, s);
+    build_structure(*p, points_fixed, cnt, s);
     hc.mark(c->host_ms, 1);
     nl_glob = (int)cnt[p->n_poses];
     nae_glob = (int)cnt[p->n_poses + 1];
@@ -1648,6 +1791,7 @@ struct Optimizer {
       pk.add(&d.pt_ptr, s.pt_ptr); pk.add(&d.pt_edges, s.pt_edges); pk.add(&d.pt_h, s.pt_h);
       pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
       pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
+      if (lba && lba_extra) pk.add(&L.extra, lba_extra, (size_t)p->n_points);
       he = pk.flush(c);
     }
     d.delta = p->huber_delta;
@@ -1708,6 +1852,26 @@ struct Optimizer {
     d_scalar = dz(8);
     d_part = dz(kRedPartMax);
     d_flag = reinterpret_cast<int*>(d_scalar + 5);
+    if (lba) {
+      const size_t npt = (size_t)std::max(1, p->n_points), ne = (size_t)std::max(1, NE);
+      L.obs_left = (int32_t*)c->alloc(4 * npt);
+      L.edges_left = (int32_t*)c->alloc(4 * npt);
+      L.edges_all = (int32_t*)c->alloc(4 * npt);
+      L.bad = (uint8_t*)c->alloc(npt);
+      L.pwrite = (uint8_t*)c->alloc(npt);
+      L.inlier = (uint8_t*)c->alloc(ne);
+      L.level = (uint8_t*)c->alloc(ne);
+      L.keep = (int32_t*)c->alloc(4 * ne);
+      L.res = (int32_t*)c->alloc(16);
+      L.chi = d.chi;
+      L.k2 = p->huber_delta * p->huber_delta;
+      if (!L.obs_left || !L.edges_left || !L.edges_all || !L.bad || !L.pwrite || !L.inlier || !L.level ||
+          !L.keep || !L.res)
+        he = hipErrorOutOfMemory;
+      else
+        hipLaunchKernelGGL(k_lba_init, dim3(gb(std::max(NE, p->n_points))), dim3(256), 0, st, L, NE,
+                           p->n_points);
+    }
     if (he != hipSuccess) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
     d.push_poses = d_poses_bk; d.push_points = d_points_bk;
     d.n_pose_dbl = 6 * p->n_poses; d.n_point_dbl = 3 * p->n_points;
@@ -1834,6 +1998,92 @@ struct Optimizer {
     return MCS_OK;
   }
 
+  // Round 2 of a device-culled LocalBA: the compacted active list from round 1's tail (no host
+  // round trip: the culled edges' terms were zeroed by k_lba_cull)
+  void remask_device() {
+    d.aedge = L.keep;
+    d.nae = lba_res[0];
+    nae_glob = d.nae;
+    nl_glob = lba_res[2];
+    sig_path = !sharded && d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
+  }
+
+  // run_device's tail for LocalBA (lba_tail 1..3): chi2 of every edge at the final estimate,
+  // the culling pass, and either the round-2 active list (round 1: nothing is downloaded; the
+  // host reads three counts) or the results (round 2: poses, points, inlier flags, write-back)
+  int lba_finish(double* poses, double* points) {
+    HostClock hc;
+    if (lba_tail <= 2) {
+      Dev d2 = d;
+      d2.ctl = nullptr;
+      d2.aedge = nullptr;
+      d2.nae = NE;
+      d2.err = dz(2 * (size_t)NE);
+      d2.rchi = dz(NE);
+      if (he != hipSuccess) { set_hip_error(he, "BA chi2", __FILE__, __LINE__); return MCS_ERR_HIP; }
+      hipLaunchKernelGGL(k_edges, dim3(gb(NE)), dim3(256), 0, st, d2, 0);
+      hipLaunchKernelGGL(k_lba_cull, dim3(gb(s.nl)), dim3(256), 0, st, d, L, lba_tail == 1 ? 1 : 0);
+    }
+    if (lba_tail == 1) {
+      hipLaunchKernelGGL(k_lba_compact, dim3(1), dim3(1024), 0, st, d, L);
+      MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, L.res, 12, hipMemcpyDeviceToHost, st));
+      MCS_HIP_CHECK(spin_sync(st));
+      std::memcpy(lba_res, c->pinned_i, 12);
+      hc.mark(c->host_ms, 3);
+      MCS_HIP_CHECK(hipGetLastError());
+      return MCS_OK;
+    }
+    const size_t b_po = 48 * (size_t)p->n_poses, b_pt = 24 * (size_t)p->n_points;
+    const size_t b_in = (size_t)NE, b_pw = lba_pwrite_out ? (size_t)p->n_points : 0;
+    const size_t total = b_po + b_pt + b_in + b_pw + 64;
+    if (total > c->stage_cap) MCS_HIP_CHECK(hipStreamSynchronize(st));   // regrow
+    uint8_t* hst = c->stage_get(total);
+    if (!hst) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
+    if (b_po) MCS_HIP_CHECK(hipMemcpyAsync(hst, d_poses, b_po, hipMemcpyDeviceToHost, st));
+    if (b_pt) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po, d_points, b_pt, hipMemcpyDeviceToHost, st));
+    if (b_in) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt, L.inlier, b_in, hipMemcpyDeviceToHost, st));
+    if (b_pw) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt + b_in, L.pwrite, b_pw, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(spin_sync(st));
+    if (b_po) std::memcpy(poses, hst, b_po);
+    if (b_pt) std::memcpy(points, hst + b_po, b_pt);
+    if (b_in && lba_inlier_out) std::memcpy(lba_inlier_out, hst + b_po + b_pt, b_in);
+    if (b_pw) std::memcpy(lba_pwrite_out, hst + b_po + b_pt + b_in, b_pw);
+    hc.mark(c->host_ms, 3);
+    MCS_HIP_CHECK(hipGetLastError());
+    return MCS_OK;
+  }
+
+  // the round-1 state a host fallback needs (a pose left the system): the estimate, the levels
+  // and the per-point culling state
+  int lba_fetch(double* poses, double* points, uint8_t* level, uint8_t* inlier, int32_t* obs_left,
+                int32_t* edges_left, uint8_t* bad) {
+    const size_t npt = (size_t)p->n_points;
+    MCS_HIP_CHECK(hipMemcpyAsync(poses, d_poses, 48 * (size_t)p->n_poses, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(points, d_points, 24 * npt, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(level, L.level, (size_t)NE, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(inlier, L.inlier, (size_t)NE, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(obs_left, L.obs_left, 4 * npt, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(edges_left, L.edges_left, 4 * npt, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(bad, L.bad, npt, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    return MCS_OK;
+  }
+
+  // poses and points only (round 1 stopped by the caller's flag)
+  int fetch_state(double* poses, double* points) {
+    MCS_HIP_CHECK(hipMemcpyAsync(poses, d_poses, 48 * (size_t)p->n_poses, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipMemcpyAsync(points, d_points, 24 * (size_t)p->n_points, hipMemcpyDeviceToHost, st));
+    MCS_HIP_CHECK(hipStreamSynchronize(st));
+    return MCS_OK;
+  }
+
+  // the LM loop runs on the device (run_device) for these options
+  bool device_driven(const mcs_ba_options* o, const mcs_ba_report* rep) const {
+    const bool long_trace = rep && rep->trace_chi2 && rep->trace_cap > kLmTraceCap &&
+                            o->max_iterations > kLmTraceCap;
+    return !sharded && !c->timing && !long_trace;
+  }
+
   int run(const mcs_ba_options* o, double* poses, double* points, double* edge_chi2,
           volatile int32_t* stop_flag, mcs_ba_report* rep) {
     // one GPU and no per-stage timing: the LM control runs on the device (no per-trial
@@ -1841,9 +2091,7 @@ struct Optimizer {
     // (the device loop records the chi2 trace of its first kLmTraceCap iterations only: a
     // caller asking for a longer trace of a longer run gets the host-driven loop, which fills
     // up to trace_cap like every other path)
-    const bool long_trace = rep && rep->trace_chi2 && rep->trace_cap > kLmTraceCap &&
-                            o->max_iterations > kLmTraceCap;
-    if (!sharded && !c->timing && !long_trace)
+    if (device_driven(o, rep))
       return run_device(o, poses, points, edge_chi2, stop_flag, rep);
     auto rec = [&](int k) { if (c->timing) (void)hipEventRecord(c->ev[k], st); };
     auto ms = [&](int a, int b) { float f = 0.f; (void)hipEventElapsedTime(&f, c->ev[a], c->ev[b]); return (double)f; };
@@ -2178,7 +2426,7 @@ struct Optimizer {
       // partials of k_edges_end / k_update (a fixed order: partials in workgroup order, each a
       // fixed in-workgroup tree), the LM decision and the pop of a rejected trial
       Sum3 q{{dd.part_chi, dd.part_pt, dd.part_ps}, {(int)g_edg, (int)g_upd, (int)g_upd}};
-      hipLaunchKernelGGL(k_edges_end, dim3(g_edg), dim3(kRedNT), 0, st, dd, q, le);
+      hipLaunchKernelGGL(k_edges_end, dim3(g_edg), dim3(kEdgeEndNT), 0, st, dd, q, le);
       return hipGetLastError() == hipSuccess ? MCS_OK : MCS_ERR_HIP;
     };
     // progress word of the step whose k_edges_end published sequence `want`
@@ -2213,8 +2461,9 @@ struct Optimizer {
     }
     LmCtl* hc = (LmCtl*)c->pinned_ctl;
     MCS_HIP_CHECK(hipMemcpyAsync(hc, dctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
-    // per-edge chi2 of every edge at the final estimate, poses, points: the common tail
-    const int rtail = download(poses, points, edge_chi2);
+    // per-edge chi2 of every edge at the final estimate, poses, points: the common tail (or
+    // LocalBA's device culling)
+    const int rtail = lba_tail ? lba_finish(poses, points) : download(poses, points, edge_chi2);
     if (rtail) return rtail;
     if (hc->dev_err) {
       set_error("BA: the LDL^T solve's hand-off wait timed out (ldlt kFlagTimeout); optimisation aborted");
@@ -2436,6 +2685,53 @@ int mcs_local_ba_ex(mcs_ba_ctx* c, const mcs_ba_problem* p, const int32_t* point
   // round 1 builds the structure and uploads the problem; round 2 (the same graph with the
   // culled edges at level 1) reuses both (Optimizer::remask) unless a pose left the system
   Optimizer opt(c, p, false);
+  if (opt.device_driven(&o, r1) && opt.device_driven(&o, r2)) {
+    // The culling passes run on the device between and after the rounds (k_lba_cull): round 2
+    // follows round 1 without a download, and only the results come back.
+    opt.lba = true;
+    opt.lba_extra = point_extra_obs;
+    int rc = opt.setup(poses, points, level.data(), nullptr);
+    if (rc) return rc;
+    opt.lba_tail = 1;
+    rc = opt.run(&o, poses, points, nullptr, sf, r1);
+    if (rc) return rc;
+    if (r1->n_active_poses + r1->n_active_points == 0) return MCS_OK;   // :784-788 (nothing moved)
+    if (stop_flag && *stop_flag) return opt.fetch_state(poses, points);   // bDoMore = false (:790-794)
+    o.max_iterations = 15;                                    // :819-820
+    if (opt.lba_res[1]) {
+      // an active pose lost every edge: g2o's initializeOptimization drops it from the system, so
+      // round 2 rebuilds from scratch on the host's copy of round 1's state
+      std::vector<int32_t> obs_d(p->n_points), el_d(p->n_points);
+      if ((rc = opt.lba_fetch(poses, points, level.data(), edge_inlier, obs_d.data(), el_d.data(), pt_bad.data())))
+        return rc;
+      for (int i = 0; i < p->n_points; i++)
+        if (edges_left[i] > 0) { obs_left[i] = obs_d[i]; edges_left[i] = el_d[i]; }
+      rc = mcs_ba_optimize(c, p, &o, poses, points, level.data(), chi.data(), sf, r2);
+      if (rc) return rc;
+      if (r2->n_active_poses + r2->n_active_points == 0) return MCS_OK;
+      cull(false);
+    } else {
+      opt.remask_device();
+      // round 2's report counts (run_device) decide whether the final culling runs (:822-826)
+      const bool empty2 = (opt.s.np + opt.nl_glob) == 0;
+      opt.lba_tail = empty2 ? 3 : 2;
+      opt.lba_inlier_out = edge_inlier;
+      opt.lba_pwrite_out = empty2 ? nullptr : point_write;
+      rc = opt.run(&o, poses, points, nullptr, sf, r2);
+      if (rc) return rc;
+      if (r2->n_active_poses + r2->n_active_points == 0) return MCS_OK;   // :822-826
+      *write_back = 1;
+      return MCS_OK;
+    }
+    *write_back = 1;
+    if (point_write) {
+      std::vector<int32_t> edges_all(p->n_points, 0);
+      for (int e = 0; e < p->n_edges; e++) edges_all[p->edge_point[e]]++;
+      for (int i = 0; i < p->n_points; i++)
+        point_write[i] = !pt_bad[i] && edges_left[i] > 1 && edges_all[i] >= 2;
+    }
+    return MCS_OK;
+  }
   int rc = opt.setup(poses, points, level.data(), nullptr);
   if (rc) return rc;
   rc = opt.run(&o, poses, points, chi.data(), sf, r1);

@@ -24,63 +24,136 @@ struct HostStruct {
   std::vector<int32_t> aedge, pose_h, point_h, hpose_vtx, hpt_vtx, pt_ptr, pt_edges, ps_ptr,
       ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, it_nch;
   std::vector<int32_t> pt_h;   // Hessian index of the pose of every pt_edges entry (-1: fixed)
-  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_structure scratch
+  std::vector<int32_t> cnt_pt, cnt_pose, cursor;     // scan_edges / build_structure scratch
+  std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_pairs_host scratch
   int n_slots = 0;
   int np = 0, nl = 0;
 };
 
 // SparseOptimizer::initializeOptimization(0) + buildIndexMapping + BlockSolver::buildStructure
-// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295): active edges (level 0), active
-// non-fixed poses in vertex order (pose_cnt: number of active edges per pose over ALL shards),
-// active points in vertex order, CSR lists point -> edges and pose -> edges and the lower pose
-// blocks of the Schur complement, by counting sorts in edge order (deterministic).  The block
-// pairs themselves: build_pairs_host / the device build.
-inline void build_structure(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
-                            const std::vector<double>& pose_cnt, HostStruct& s) {
-  s.aedge.clear();
-  s.aedge.reserve(p.n_edges);
-  for (int e = 0; e < p.n_edges; e++)   // level 0 and not allVerticesFixed (:206-267)
-    if ((!level || level[e] == 0) && !(points_fixed && p.pose_fixed[p.edge_pose[e]])) s.aedge.push_back(e);
-  std::vector<char> lh(p.n_points, 0);
-  if (!points_fixed)
-    for (int e : s.aedge) lh[p.edge_point[e]] = 1;
-  s.pose_h.assign(p.n_poses, -1);
-  s.point_h.assign(p.n_points, -1);
-  s.hpose_vtx.clear(); s.hpt_vtx.clear();
-  s.np = s.nl = 0;
-  for (int i = 0; i < p.n_poses; i++)
-    if (pose_cnt[i] > 0 && !p.pose_fixed[i]) { s.pose_h[i] = s.np++; s.hpose_vtx.push_back(i); }
-  for (int i = 0; i < p.n_points; i++)
-    if (lh[i]) { s.point_h[i] = s.nl++; s.hpt_vtx.push_back(i); }
-  // CSR point -> edges, pose -> edges (counting sort, stable in edge order)
-  s.pt_ptr.assign(s.nl + 1, 0);
-  s.ps_ptr.assign(s.np + 1, 0);
-  for (int e : s.aedge) {
-    const int l = s.point_h[p.edge_point[e]];
-    if (l >= 0) s.pt_ptr[l + 1]++;
-    const int h = s.pose_h[p.edge_pose[e]];
-    if (h >= 0) s.ps_ptr[h + 1]++;
+// (sparse_optimizer.cpp:166-267, block_solver.hpp:143-295) in two passes over the edges.
+//
+// scan_edges: the vertex-index checks, the active edges (level 0 and not allVerticesFixed) in
+// edge order, and per pose / per point their numbers (cnt = the per-pose counts, then the
+// active point and edge counts: what the shards all-reduce).  Branch-free in the loop: the
+// edges come grouped by point, so a per-edge branch on the data mispredicts and a counter
+// chain through memory is the loop's critical path; one pass instead of the four of the
+// first version (config C: 0.35 -> 0.11 ms on this build host with build_structure).
+// Returns false when an edge names a vertex or camera out of range.
+inline bool scan_edges(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
+                       HostStruct& s, std::vector<double>& cnt) {
+  const int NE = p.n_edges, NP = p.n_poses, NL = p.n_points;
+  s.aedge.resize(NE);
+  s.cnt_pt.assign(NL, 0);
+  s.cnt_pose.assign(NP, 0);
+  int32_t* const ae = s.aedge.data();
+  int32_t* const cp = s.cnt_pt.data();
+  int32_t* const cpo = s.cnt_pose.data();
+  unsigned bad = 0;
+  int nae = 0;
+  for (int e = 0; e < NE; e++) {
+    const int pi = p.edge_pose[e], li = p.edge_point[e], ci = p.edge_cam[e];
+    const unsigned b = ((unsigned)pi >= (unsigned)NP) | ((unsigned)li >= (unsigned)NL) |
+                       ((unsigned)ci >= (unsigned)p.n_cams);
+    bad |= b;
+    if (b) continue;
+    const int act = !(level && level[e]) && !(points_fixed && p.pose_fixed[pi]);
+    ae[nae] = e;
+    nae += act;
+    cpo[pi] += act;
+    cp[li] += act;
   }
-  for (int l = 0; l < s.nl; l++) s.pt_ptr[l + 1] += s.pt_ptr[l];
-  for (int h = 0; h < s.np; h++) s.ps_ptr[h + 1] += s.ps_ptr[h];
-  s.pt_edges.assign(s.pt_ptr[s.nl], 0);
-  s.ps_edges.assign(s.ps_ptr[s.np], 0);
-  {
-    std::vector<int32_t> fp(s.pt_ptr.begin(), s.pt_ptr.end() - 1), fs(s.ps_ptr.begin(), s.ps_ptr.end() - 1);
-    for (int e : s.aedge) {
-      const int l = s.point_h[p.edge_point[e]];
-      if (l >= 0) s.pt_edges[fp[l]++] = e;
-      const int h = s.pose_h[p.edge_pose[e]];
-      if (h >= 0) s.ps_edges[fs[h]++] = e;
+  if (bad) return false;
+  s.aedge.resize(nae);
+  cnt.assign((size_t)NP + 2, 0.0);
+  for (int i = 0; i < NP; i++) cnt[i] = cpo[i];
+  int nl = 0;
+  if (!points_fixed)
+    for (int i = 0; i < NL; i++) nl += cp[i] > 0;
+  cnt[NP] = nl;
+  cnt[NP + 1] = nae;
+  return true;
+}
+
+// build_structure (after scan_edges on the same HostStruct): active non-fixed poses in vertex
+// order (pose_cnt: active edges per pose over ALL shards), active points in vertex order, CSR
+// lists point -> edges and pose -> edges in edge order (one fill pass, counting-sort cursors;
+// the fixed poses' edges go to a dropped tail run instead of a branch) and the lower pose
+// blocks of the Schur complement.  The block pairs themselves: build_pairs_host / the device.
+inline void build_structure(const mcs_ba_problem& p, bool points_fixed,
+                            const std::vector<double>& pose_cnt, HostStruct& s) {
+  const int NP = p.n_poses, NL = p.n_points;
+  const int nae = (int)s.aedge.size();
+  s.pose_h.resize(NP);
+  s.hpose_vtx.resize(NP);
+  int np = 0;
+  for (int i = 0; i < NP; i++) {
+    const bool a = pose_cnt[i] > 0 && !p.pose_fixed[i];
+    s.pose_h[i] = a ? np : -1;
+    if (a) s.hpose_vtx[np++] = i;
+  }
+  s.np = np;
+  s.hpose_vtx.resize(np);
+  const int32_t* const poh = s.pose_h.data();
+  const int32_t* const ae = s.aedge.data();
+  int32_t* const cp = s.cnt_pt.data();
+  // pose runs 0 .. np-1, then run np: the edges of fixed poses
+  s.ps_ptr.assign(np + 2, 0);
+  int32_t* const sp = s.ps_ptr.data();
+  for (int i = 0; i < NP; i++) sp[(poh[i] >= 0 ? poh[i] : np) + 1] += s.cnt_pose[i];
+  for (int h = 0; h <= np; h++) sp[h + 1] += sp[h];
+  s.point_h.resize(NL);
+  s.hpt_vtx.resize(NL);
+  s.pt_ptr.resize(NL + 1);
+  s.pt_ptr[0] = 0;
+  int nl = 0;
+  int32_t* const ph = s.point_h.data();
+  int32_t* const pp = s.pt_ptr.data();
+  int32_t* const hv = s.hpt_vtx.data();
+  if (!points_fixed) {
+    for (int i = 0; i < NL; i++) {
+      const int c = cp[i];
+      ph[i] = c > 0 ? nl : -1;
+      hv[nl] = i;                       // overwritten by the next point unless this one counts
+      pp[nl + 1] = pp[nl] + c;
+      cp[i] = pp[nl];                   // the point's fill cursor
+      nl += c > 0;
+    }
+  } else {
+    for (int i = 0; i < NL; i++) ph[i] = -1;
+  }
+  s.nl = nl;
+  s.hpt_vtx.resize(nl);
+  s.pt_ptr.resize(nl + 1);
+  s.pt_edges.resize(pp[nl]);
+  s.pt_h.resize(pp[nl]);
+  s.ps_edges.resize(nae);
+  int32_t* const pe = s.pt_edges.data();
+  int32_t* const pth = s.pt_h.data();
+  int32_t* const pse = s.ps_edges.data();
+  s.cursor.assign(sp, sp + np + 1);
+  int32_t* const fs = s.cursor.data();
+  if (!points_fixed) {
+    for (int k = 0; k < nae; k++) {
+      const int e = ae[k];
+      const int h = poh[p.edge_pose[e]];
+      const int r = cp[p.edge_point[e]]++;
+      pe[r] = e;
+      pth[r] = h;                       // the pose's Hessian index per entry (-1: fixed)
+      pse[fs[h >= 0 ? h : np]++] = e;
+    }
+  } else {
+    for (int k = 0; k < nae; k++) {
+      const int e = ae[k];
+      const int h = poh[p.edge_pose[e]];
+      pse[fs[h >= 0 ? h : np]++] = e;
     }
   }
-  s.pt_h.resize(s.pt_edges.size());
-  for (size_t q = 0; q < s.pt_edges.size(); q++) s.pt_h[q] = s.pose_h[p.edge_pose[s.pt_edges[q]]];
-  // lower pose blocks (i >= j), block id i(i+1)/2 + j, and their edge pairs in
-  // (point, e1, e2) order
-  const size_t nblk = (size_t)s.np * (s.np + 1) / 2;
+  s.ps_edges.resize(sp[np]);
+  s.ps_ptr.resize(np + 1);
+  const size_t nblk = (size_t)np * (np + 1) / 2;
   s.blk_i.resize(nblk); s.blk_j.resize(nblk);
-  for (int i = 0, b = 0; i < s.np; i++)
+  for (int i = 0, b = 0; i < np; i++)
     for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
 }
 

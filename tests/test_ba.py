@@ -241,3 +241,57 @@ def test_gpu_local_ba_bitwise_reproducible(gpu, problem):
     b = S.local_ba(problem)
     assert np.array_equal(a["poses"], b["poses"]) and np.array_equal(a["points"], b["points"])
     assert np.array_equal(a["edge_inlier"], b["edge_inlier"])
+
+
+def _pose_leaves_problem():
+    """Config-C-style small problem whose last local pose keeps 12 edges, all moved ~2000 px:
+    round 1's culling (cOptimizer.cpp:798-817) removes every one of them, so that pose leaves the
+    system of round 2 (g2o's initializeOptimization drops a vertex without active edges)."""
+    from mcs_amd import ba
+    pr = dict(ba.make_problem(n_local=4, n_fixed=1, n_points=300, target_edges=2000, seed=3))
+    rng = np.random.default_rng(0)
+    k = int(np.nonzero(pr["pose_fixed"] == 0)[0][-1])
+    ek = np.nonzero(pr["edge_pose"] == k)[0]
+    m = np.ones(len(pr["edge_pose"]), bool)
+    m[ek[12:]] = False
+    for key in ("edge_pose", "edge_point", "edge_cam", "edge_meas", "edge_info"):
+        pr[key] = pr[key][m]
+    ek = np.nonzero(pr["edge_pose"] == k)[0]
+    pr["edge_meas"] = pr["edge_meas"].copy()
+    pr["edge_meas"][ek] += rng.uniform(-2000.0, 2000.0, (len(ek), 2))
+    return pr, k
+
+
+def test_oracle_pose_leaves_after_culling():
+    pr, k = _pose_leaves_problem()
+    o = ob.local_ba(pr)
+    assert o["report1"].n_active_poses == 4 and o["report2"].n_active_poses == 3
+    assert o["edge_inlier"][pr["edge_pose"] == k].sum() == 0 and o["write_back"] == 1
+
+
+@pytest.mark.gpu
+def test_gpu_local_ba_pose_leaves_after_culling(gpu):
+    """The device-culled LocalBA (k_lba_cull / k_lba_compact between the rounds) finds that an
+    active pose lost every edge and runs round 2 from scratch on the host's copy of round 1's
+    state: the same rounds, inlier set and write-back as the oracle and as the host-culled flow
+    (timing on).  The left pose is fitted to 12 outliers only, so its estimate is compared
+    loosely; every other pose and the well-constrained points as in the config-C test."""
+    from mcs_amd import ba
+    pr, k = _pose_leaves_problem()
+    g = ba.Solver().local_ba(pr)
+    H = ba.Solver()
+    H.enable_timing(True)
+    h = H.local_ba(pr)
+    o = ob.local_ba(pr)
+    for r in (g, h):
+        assert r["report2"].n_active_poses == 3
+        assert r["write_back"] == o["write_back"]
+        assert r["report1"].iterations == o["report1"].iterations
+        assert r["report2"].iterations == o["report2"].iterations
+        assert np.array_equal(r["edge_inlier"], o["edge_inlier"])
+    keep = np.arange(len(pr["poses"])) != k
+    assert np.abs(g["poses"][keep] - o["poses"][keep]).max() < 1e-6
+    assert np.abs(g["poses"][k] - o["poses"][k]).max() < 1e-3
+    wc = _well_constrained(pr)
+    assert np.abs(g["points"][wc] - o["points"][wc]).max() < 1e-5
+    assert np.abs(g["poses"] - h["poses"]).max() < 1e-6

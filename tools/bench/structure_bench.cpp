@@ -26,14 +26,15 @@ int main(int argc, char** argv) {
   auto np = load<int32_t>(d + "/sizes.bin");
   mcs_ba_problem p{};
   p.n_poses = np[0]; p.n_points = np[1]; p.n_edges = (int)ep.size(); p.n_cams = 3;
-  p.edge_pose = ep.data(); p.edge_point = el.data(); p.pose_fixed = pf.data();
+  std::vector<int32_t> ec(ep.size(), 0);   // camera indices: only range-checked here
+  p.edge_pose = ep.data(); p.edge_point = el.data(); p.pose_fixed = pf.data(); p.edge_cam = ec.data();
   mcs::ba::HostStruct s;
   double best = 1e9;
   for (int r = 0; r < 50; r++) {
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<double> cnt(p.n_poses + 2, 0.0);
-    for (int e = 0; e < p.n_edges; e++) cnt[p.edge_pose[e]] += 1.0;
-    mcs::ba::build_structure(p, nullptr, false, cnt, s);
+    std::vector<double> cnt;
+    mcs::ba::scan_edges(p, nullptr, false, s, cnt);
+    mcs::ba::build_structure(p, false, cnt, s);
     mcs::ba::build_pairs_host(p, s);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     best = std::min(best, ms);
