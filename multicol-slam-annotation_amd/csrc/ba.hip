@@ -308,7 +308,12 @@ __device__ __forceinline__ double lam0_of(const Dev& d) { return d.ctl ? d.ctl->
 // a kernel of a device-driven step that is not needed (the loop has ended)
 __device__ __forceinline__ bool lm_done(const Dev& d) { return d.ctl && d.ctl->done; }
 
-constexpr int kRedNT = 256;   // k_build workgroup (1024 measured slower: 18.3 vs 12.9 us at config C)
+constexpr int kRedNT = 256;   // reduction workgroup (k_edges_end's LM tail, k_update partials)
+#ifndef MCS_BUILD_NT
+#define MCS_BUILD_NT 256
+#endif
+// k_build / k_build_trial workgroup (1024 measured slower: 18.3 vs 12.9 us at config C)
+constexpr int kBuildNT = MCS_BUILD_NT;
 
 // per active edge: error (+ robust chi2) and optionally Jacobians / weight / Hpl = w Jp^T Jl
 // (device-driven linearisation: only when the previous trial ended an iteration)
@@ -456,8 +461,15 @@ __host__ __device__ inline double cube_rn(double x) {
 // workgroups do: 1024 strided slots, then the LDS tree -- emulated here by kRedNT threads, so
 // the bits are the same), the LM control (lm_control) and the pop of a rejected trial.
 __device__ void lm_control(LmCtl* c, const double* sc, int flag, LmSig* sig);
-struct LmEnd { double* sc; const int* flag; LmSig* sig; uint64_t seq; };
+struct LmEnd { double* sc; const int* flag; LmSig* sig; uint64_t seq; LmCtl* host_ctl; };
+#ifndef MCS_LM_AHEAD
+#define MCS_LM_AHEAD 2      // LM steps the host keeps enqueued ahead of the device
+#endif
+#ifndef MCS_EXP_PUB_DONE
+#define MCS_EXP_PUB_DONE 0  // experiment builds: publish progress only once the run is done
+#endif
 __device__ __forceinline__ void lm_publish(const LmCtl* c, const LmEnd& le) {
+  if (MCS_EXP_PUB_DONE && !c->done) return;
   // relaxed: a stale `done` only costs the host one more (no-op) step
   __hip_atomic_store(&le.sig->done, c->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&le.sig->iter, c->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -515,6 +527,14 @@ __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
   if (rej && act) {   // pop: every pose and point back to the backups of the trial's push
     for (int i = t; i < d.n_pose_dbl; i += kRedNT) d.poses[i] = d.push_poses[i];
     for (int i = t; i < d.n_point_dbl; i += kRedNT) d.points[i] = d.push_points[i];
+  }
+  // the run's last step: the control block straight into host memory (the report), read by
+  // the host once the stream has drained -- no readback copy
+  if (le.host_ctl && c->done && act) {
+    constexpr int nw = (int)(sizeof(LmCtl) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(c);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(le.host_ctl);
+    for (int i = t; i < nw; i += kRedNT) dst[i] = src[i];
   }
   if (t == 0) lm_publish(c, le);
 }
@@ -621,6 +641,14 @@ __device__ __forceinline__ void lm_lambda0_body(LmCtl* c, double pt, double pose
   c->lambda = c->tau * fmax(pt, pose);
   c->ni = 2;
   c->nBad = 0;
+}
+// the LM control block of a run, by value (no pageable host copy on the stream)
+__global__ void k_ctl_init(LmCtl h0, LmCtl* c) {
+  constexpr int nw = (int)(sizeof(LmCtl) / 4);
+  static_assert(sizeof(LmCtl) % 4 == 0, "word copy");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&h0);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(c);
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
 }
 __global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
   if (threadIdx.x != 0 || c->done) return;
@@ -809,7 +837,7 @@ __global__ void k_point_block_eval(const double* H, double lam, const double* b,
 // iteration's stored Hll / b_l: a rejected trial re-solves the same linearisation)
 template <bool TRIAL>
 __device__ __forceinline__ void points_build_body(const Dev& d, int block, bool lin) {
-  const int gt = block * kRedNT + threadIdx.x;
+  const int gt = block * kBuildNT + threadIdx.x;
   const int l = gt >> 2, sub = gt & 3;
   const bool act = l < d.nl;
   double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
@@ -928,7 +956,7 @@ constexpr int kUpper6[21][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, 
 // workgroup's threads (fixed stride), block tree sum.  Also the diagonal and b_p into the
 // exchange area.
 __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
-  __shared__ double sm[27 * (kRedNT / 64)];
+  __shared__ double sm[27 * (kBuildNT / 64)];
   const int t = threadIdx.x;
   double acc[27];
 #pragma unroll
@@ -937,12 +965,15 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
   // before the first sum (the edge -> Jacobian gather is two dependent round trips, and a
   // pose has ~1500 edges at config C: one at a time the chain was the whole kernel).  Loads
   // past the list read the last edge (unconditional: no merge waits) and are not summed.
-  constexpr int kU = 4;
+#ifndef MCS_BUILD_KU
+#define MCS_BUILD_KU 4
+#endif
+  constexpr int kU = MCS_BUILD_KU;
   const int q0 = d.ps_ptr[i], q1 = d.ps_ptr[i + 1];
-  for (int qb = q0 + t; qb < q1; qb += kU * kRedNT) {
+  for (int qb = q0 + t; qb < q1; qb += kU * kBuildNT) {
     int e[kU];
 #pragma unroll
-    for (int u = 0; u < kU; u++) e[u] = d.ps_edges[min(qb + u * kRedNT, q1 - 1)];
+    for (int u = 0; u < kU; u++) e[u] = d.ps_edges[min(qb + u * kBuildNT, q1 - 1)];
     double j0[kU][6], j1[kU][6], w[kU], er0[kU], er1[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
@@ -955,7 +986,7 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
-      if (qb + u * kRedNT >= q1) break;
+      if (qb + u * kBuildNT >= q1) break;
       const double we0 = -w[u] * er0[u], we1 = -w[u] * er1[u];
 #pragma unroll
       for (int v = 0; v < 21; v++) {
@@ -966,7 +997,7 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
       for (int a = 0; a < 6; a++) acc[21 + a] += j0[u][a] * we0 + j1[u][a] * we1;
     }
   }
-  constexpr int NW = kRedNT / 64;
+  constexpr int NW = kBuildNT / 64;
   block_sum_vec<27, NW>(acc, sm);
   if (t < 21) {
     const int a = kUpper6[t][0], bb = kUpper6[t][1];
@@ -980,7 +1011,7 @@ __device__ __forceinline__ void poses_build_body(const Dev& d, int i) {
   }
 }
 // both builds in one launch: workgroups [0, np) per pose, the rest four lanes per point
-__global__ __launch_bounds__(kRedNT) void k_build(Dev d0) {
+__global__ __launch_bounds__(kBuildNT) void k_build(Dev d0) {
   if (lm_done(d0) || (d0.ctl && !d0.ctl->lin)) return;
   const Dev d = lin_buf(d0, false);
   if ((int)blockIdx.x < d.np) poses_build_body(d, blockIdx.x);
@@ -1021,11 +1052,11 @@ __global__ __launch_bounds__(256) void k_point_trial(Dev d0) {
 // one launch -- the point quads go on from their H / b to Dinv, db and Y (same arithmetic,
 // same bits), every thread takes part in the push.  Step 0 keeps the two launches: lambda's
 // initial value needs the built diagonal first.
-__global__ __launch_bounds__(kRedNT) void k_build_trial(Dev d0) {
+__global__ __launch_bounds__(kBuildNT) void k_build_trial(Dev d0) {
   if (lm_done(d0)) return;
   const Dev d = lin_buf(d0, false);
   const bool lin = d.ctl->lin != 0;
-  trial_push(d, blockIdx.x * kRedNT + threadIdx.x, gridDim.x * kRedNT);
+  trial_push(d, blockIdx.x * kBuildNT + threadIdx.x, gridDim.x * kBuildNT);
   if ((int)blockIdx.x < d.np) { if (lin) poses_build_body(d, blockIdx.x); }
   else points_build_body<true>(d, blockIdx.x - d.np, lin);
 }
@@ -1361,7 +1392,7 @@ struct LbaState {
   double* chi;                                                   // chi2 of every edge
   double k2;                                                     // thHuber^2
   int32_t* keep;                                                 // compacted active list
-  int32_t* res;                                                  // {nae, pose_left, nl_left}
+  int32_t* res;                                                  // {nae, pose_left, nl_left} (host memory)
   uint8_t* pwrite;                                               // per point vertex (round 2)
 };
 
@@ -1379,13 +1410,26 @@ __global__ __launch_bounds__(256) void k_lba_cull(Dev d, LbaState L, int round1)
   } else {
     ol = L.obs_left[v]; el = L.edges_left[v]; bad = L.bad[v] != 0;
   }
-  for (int q = q0; q < q1; q++) {
-    const int e = d.pt_edges[q];
-    if (!L.inlier[e] || bad || !(L.chi[e] > L.k2)) continue;
-    L.inlier[e] = 0;
-    if (round1) { L.level[e] = 1; zero_edge_terms(d, e); }
-    el--;
-    if (--ol < 2) bad = true;
+  // the point's edges eight at a time: their indices, then their flags and chi2 all in flight,
+  // then the sequential decisions in edge order from registers
+  for (int qb = q0; qb < q1; qb += 8) {
+    int ev[8];
+    bool in[8];
+    double ch[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) ev[j] = d.pt_edges[min(qb + j, q1 - 1)];
+#pragma unroll
+    for (int j = 0; j < 8; j++) { in[j] = L.inlier[ev[j]] != 0; ch[j] = L.chi[ev[j]]; }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (qb + j >= q1) break;
+      const int e = ev[j];
+      if (!in[j] || bad || !(ch[j] > L.k2)) continue;
+      L.inlier[e] = 0;
+      if (round1) { L.level[e] = 1; zero_edge_terms(d, e); }
+      el--;
+      if (--ol < 2) bad = true;
+    }
   }
   L.obs_left[v] = ol; L.edges_left[v] = el; L.bad[v] = bad ? 1 : 0;
   // cOptimizer.cpp:885-902: not bad, TotalNrObservations() > 1, >= 2 vertex edges
@@ -1400,6 +1444,23 @@ __global__ __launch_bounds__(256) void k_lba_init(LbaState L, int ne, int npt) {
     L.obs_left[i] = 0; L.edges_left[i] = 0; L.edges_all[i] = 0; L.bad[i] = 0;
     if (L.pwrite) L.pwrite[i] = 0;
   }
+}
+
+// per-thread contiguous chunks of the one-workgroup kernels below: up to this many elements
+// are loaded into registers with every load in flight before the first use
+constexpr int kChunkMax = 32;
+
+// LocalBA's round-2 results into host memory: [poses | points | inlier flags | write-back flags]
+__global__ __launch_bounds__(256) void k_lba_out(const double* poses, int npo, const double* points, int npt,
+                                                 const uint8_t* inl, int ne, const uint8_t* pw, int npw,
+                                                 uint8_t* host) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  double* hd = reinterpret_cast<double*>(host);
+  if (i < npo) hd[i] = poses[i];
+  else if (i < npo + npt) hd[i] = points[i - npo];
+  uint8_t* hb = host + 8 * (size_t)(npo + npt);
+  if (i < ne) hb[i] = inl[i];
+  if (i < npw) hb[ne + i] = pw[i];
 }
 
 // exclusive prefix of v over a 1024-thread workgroup (and the total)
@@ -1426,31 +1487,74 @@ __device__ __forceinline__ int block_excl_scan1024(int v, int* sm, int* total) {
 }
 
 // the round-2 active list in edge order (stable), per-pose survivors, active points left
+// (the per-pose survivors as bit sets: OR-reduced per wave, one LDS atomicOr per wave and word;
+// per-edge LDS atomics on ten counters serialised the workgroup: 38 us)
 __global__ __launch_bounds__(1024) void k_lba_compact(Dev d, LbaState L) {
-  __shared__ int hist[2048];
+  constexpr int kPW = 2048 / 32;          // words of the pose bit set (np <= 2048)
+  __shared__ unsigned kept[kPW];
   __shared__ int sm[16];
   const int t = threadIdx.x, n = d.nae;
-  for (int h = t; h < d.np; h += 1024) hist[h] = 0;
+  for (int h = t; h < kPW; h += 1024) kept[h] = 0u;
   __syncthreads();
   const int chunk = (n + 1023) / 1024, k0 = min(n, t * chunk), k1 = min(n, k0 + chunk);
   int cnt = 0;
-  for (int k = k0; k < k1; k++) {
-    const int e = d.aedge ? d.aedge[k] : k;
-    if (L.level[e]) continue;
-    cnt++;
-    const int h = d.pose_h[d.e_pose[e]];
-    if (h >= 0) atomicAdd(&hist[h], 1);
-  }
-  int total;
-  int o = block_excl_scan1024(cnt, sm, &total);
-  for (int k = k0; k < k1; k++) {
-    const int e = d.aedge ? d.aedge[k] : k;
-    if (!L.level[e]) L.keep[o++] = e;
+  int total, o;
+  if (chunk <= kChunkMax) {
+    // the chunk's index loads, then its level / pose loads, all in flight together (one
+    // workgroup is latency-bound: one dependent chain per edge was 42 us at 20k edges)
+    int ev[kChunkMax], hv[kChunkMax];
+    bool kv[kChunkMax];
+#pragma unroll
+    for (int j = 0; j < kChunkMax; j++) {
+      const int k = min(k0 + j, max(k1 - 1, 0));
+      ev[j] = d.aedge ? d.aedge[k] : k;
+    }
+#pragma unroll
+    for (int j = 0; j < kChunkMax; j++) { kv[j] = k0 + j < k1 && !L.level[ev[j]]; hv[j] = d.e_pose[ev[j]]; }
+    // poses of this thread's kept edges: the first 64 Hessian indices as a bit set (LocalBA
+    // sizes), the rest one atomic each
+    uint64_t pm = 0;
+#pragma unroll
+    for (int j = 0; j < kChunkMax; j++) hv[j] = kv[j] ? d.pose_h[hv[j]] : -1;
+#pragma unroll
+    for (int j = 0; j < kChunkMax; j++) {
+      if (!kv[j]) continue;
+      cnt++;
+      const int h = hv[j];
+      if (h >= 0 && h < 64) pm |= 1ull << h;
+      else if (h >= 64) atomicOr(&kept[h >> 5], 1u << (h & 31));
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) pm |= __shfl_xor(pm, o2);
+    if ((t & 63) == 0 && pm) { atomicOr(&kept[0], (unsigned)pm); atomicOr(&kept[1], (unsigned)(pm >> 32)); }
+    o = block_excl_scan1024(cnt, sm, &total);
+#pragma unroll
+    for (int j = 0; j < kChunkMax; j++)
+      if (kv[j]) L.keep[o++] = ev[j];
+  } else {
+    for (int k = k0; k < k1; k++) {
+      const int e = d.aedge ? d.aedge[k] : k;
+      if (L.level[e]) continue;
+      cnt++;
+      const int h = d.pose_h[d.e_pose[e]];
+      if (h >= 0) atomicOr(&kept[h >> 5], 1u << (h & 31));
+    }
+    o = block_excl_scan1024(cnt, sm, &total);
+    for (int k = k0; k < k1; k++) {
+      const int e = d.aedge ? d.aedge[k] : k;
+      if (!L.level[e]) L.keep[o++] = e;
+    }
   }
   int nl = 0;
-  for (int l = t; l < d.nl; l += 1024) nl += L.edges_left[d.hpt_vtx[l]] > 0 ? 1 : 0;
+  for (int l0 = t; l0 < d.nl; l0 += 4096) {
+    int vx[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) vx[u] = d.hpt_vtx[min(l0 + 1024 * u, d.nl - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; u++) nl += (l0 + 1024 * u < d.nl && L.edges_left[vx[u]] > 0) ? 1 : 0;
+  }
   int left = 0;
-  for (int h = t; h < d.np; h += 1024) left |= hist[h] == 0 ? 1 : 0;
+  for (int h = t; h < d.np; h += 1024) left |= ((kept[h >> 5] >> (h & 31)) & 1u) ? 0 : 1;
   int nl_tot, left_any;
   (void)block_excl_scan1024(nl, sm, &nl_tot);
   (void)block_excl_scan1024(left, sm, &left_any);
@@ -1495,7 +1599,8 @@ struct mcs_ba_ctx {
       if (stage) (void)hipHostFree(stage);
       stage = nullptr; stage_cap = 0;
       const size_t cap = std::max(bytes, (size_t)1 << 20);
-      if (hipHostMalloc((void**)&stage, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+      // mapped: k_lba_out writes LocalBA's results into it directly
+      if (hipHostMalloc((void**)&stage, cap, hipHostMallocMapped) != hipSuccess) return nullptr;
       stage_cap = cap;
     }
     return stage;
@@ -1862,7 +1967,7 @@ struct Optimizer {
       L.inlier = (uint8_t*)c->alloc(ne);
       L.level = (uint8_t*)c->alloc(ne);
       L.keep = (int32_t*)c->alloc(4 * ne);
-      L.res = (int32_t*)c->alloc(16);
+      L.res = c->pinned_i;   // written by k_lba_compact straight into host memory
       L.chi = d.chi;
       L.k2 = p->huber_delta * p->huber_delta;
       if (!L.obs_left || !L.edges_left || !L.edges_all || !L.bad || !L.pwrite || !L.inlier || !L.level ||
@@ -2026,7 +2131,6 @@ struct Optimizer {
     }
     if (lba_tail == 1) {
       hipLaunchKernelGGL(k_lba_compact, dim3(1), dim3(1024), 0, st, d, L);
-      MCS_HIP_CHECK(hipMemcpyAsync(c->pinned_i, L.res, 12, hipMemcpyDeviceToHost, st));
       MCS_HIP_CHECK(spin_sync(st));
       std::memcpy(lba_res, c->pinned_i, 12);
       hc.mark(c->host_ms, 3);
@@ -2039,10 +2143,12 @@ struct Optimizer {
     if (total > c->stage_cap) MCS_HIP_CHECK(hipStreamSynchronize(st));   // regrow
     uint8_t* hst = c->stage_get(total);
     if (!hst) { set_error("BA: out of pinned host memory"); return MCS_ERR_HIP; }
-    if (b_po) MCS_HIP_CHECK(hipMemcpyAsync(hst, d_poses, b_po, hipMemcpyDeviceToHost, st));
-    if (b_pt) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po, d_points, b_pt, hipMemcpyDeviceToHost, st));
-    if (b_in) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt, L.inlier, b_in, hipMemcpyDeviceToHost, st));
-    if (b_pw) MCS_HIP_CHECK(hipMemcpyAsync(hst + b_po + b_pt + b_in, L.pwrite, b_pw, hipMemcpyDeviceToHost, st));
+    // one kernel writes the four results into the pinned staging buffer (host memory the device
+    // reaches directly): no readback copies
+    const int nmax = (int)std::max<size_t>({b_po / 8 + b_pt / 8, b_in, b_pw, 1});
+    hipLaunchKernelGGL(k_lba_out, dim3(gb(nmax)), dim3(256), 0, st, (const double*)d_poses,
+                       (int)(b_po / 8), (const double*)d_points, (int)(b_pt / 8), (const uint8_t*)L.inlier,
+                       (int)b_in, (const uint8_t*)L.pwrite, (int)b_pw, hst);
     MCS_HIP_CHECK(spin_sync(st));
     if (b_po) std::memcpy(poses, hst, b_po);
     if (b_pt) std::memcpy(points, hst + b_po, b_pt);
@@ -2219,7 +2325,7 @@ struct Optimizer {
         // the first iteration reads anything back (the max diagonal for lambda's init).
         rec(0);
         hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, d, 1);
-        hipLaunchKernelGGL(k_build, dim3((unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT)), dim3(kRedNT), 0, st, d);
+        hipLaunchKernelGGL(k_build, dim3((unsigned)s.np + (unsigned)((4 * s.nl + kBuildNT - 1) / kBuildNT)), dim3(kBuildNT), 0, st, d);
         rec(1);
         c->n_iter++;
         bool lin_pending = c->timing;
@@ -2374,7 +2480,8 @@ struct Optimizer {
     const bool empty = (s.np + nl_glob) == 0 || nae_glob == 0;
     h0.done = (empty || o->max_iterations <= 0 || *stop != 0) ? 1 : 0;
     c->lsig->ext_stop = *stop != 0;
-    MCS_HIP_CHECK(hipMemcpyAsync(dctl, &h0, sizeof(h0), hipMemcpyHostToDevice, st));
+    c->lsig->done = 0;   // this run's `done` (the previous run's stream has drained)
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(256), 0, st, h0, dctl);
     Dev dd = d;
     dd.ctl = dctl;
     const int* skip = &dctl->done;
@@ -2401,15 +2508,15 @@ struct Optimizer {
       // linearisation (k_edges_end) already in place, or keep the iteration's after a reject
       if ((step == 0 && !lin0) || (step > 0 && !h0.spec_lin))
         hipLaunchKernelGGL(k_edges, dim3(gb(d.nae)), dim3(256), 0, st, dd, 1);
-      const unsigned g_build = (unsigned)s.np + (unsigned)((4 * s.nl + kRedNT - 1) / kRedNT);
+      const unsigned g_build = (unsigned)s.np + (unsigned)((4 * s.nl + kBuildNT - 1) / kBuildNT);
       if (step == 0) {   // iteration 0 is always step 0: lambda from the max diagonal
-        hipLaunchKernelGGL(k_build, dim3(g_build), dim3(kRedNT), 0, st, dd);
+        hipLaunchKernelGGL(k_build, dim3(g_build), dim3(kBuildNT), 0, st, dd);
         reduce_dev<true>(d.red, s.nl, d_scalar + 1, d_part, st);
         reduce_dev<true>(d.hdiag, 6 * s.np, d_scalar + 2, d_part, st);
         hipLaunchKernelGGL(k_lm_lambda0, dim3(1), dim3(64), 0, st, dctl, (const double*)d_scalar);
         hipLaunchKernelGGL(k_point_trial, dim3(std::max(gb(d.npe), g_state)), dim3(256), 0, st, dd);
       } else {
-        hipLaunchKernelGGL(k_build_trial, dim3(g_build), dim3(kRedNT), 0, st, dd);
+        hipLaunchKernelGGL(k_build_trial, dim3(g_build), dim3(kBuildNT), 0, st, dd);
       }
       if (s.np) {
         hipLaunchKernelGGL(k_schur, dim3((unsigned)((items_max + 3) / 4)), dim3(256), 0, st, dd);
@@ -2420,7 +2527,7 @@ struct Optimizer {
           MCS_HIP_CHECK(ldlt::solve(d.S, d.bs, d.xp, T, lw, d_flag, st, skip));
         }
       }
-      LmEnd le{d_scalar, (const int*)d_flag, c->lsig, ++c->lsig_seq};
+      LmEnd le{d_scalar, (const int*)d_flag, c->lsig, ++c->lsig_seq, (LmCtl*)c->pinned_ctl};
       hipLaunchKernelGGL(k_update, dim3(gb(4 * s.nl + s.np)), dim3(256), 0, st, dd);
       // the trial's evaluation, then (last workgroup) its three sums from the workgroup
       // partials of k_edges_end / k_update (a fixed order: partials in workgroup order, each a
@@ -2451,8 +2558,8 @@ struct Optimizer {
       const uint64_t base = c->lsig_seq;
       const int max_steps = o->max_iterations * std::max(1, o->max_trials);
       for (int step = 0; step < max_steps; step++) {
-        if (step >= 2) {   // keep two steps in flight: wait for the one before the last
-          if ((rc = wait_seq(base + (uint64_t)step - 1))) return rc;
+        if (step >= MCS_LM_AHEAD) {   // keep MCS_LM_AHEAD steps in flight
+          if ((rc = wait_seq(base + (uint64_t)step - (MCS_LM_AHEAD - 1)))) return rc;
           c->lsig->ext_stop = *stop != 0;
           if (c->lsig->done) break;
         }
@@ -2460,7 +2567,10 @@ struct Optimizer {
       }
     }
     LmCtl* hc = (LmCtl*)c->pinned_ctl;
-    MCS_HIP_CHECK(hipMemcpyAsync(hc, dctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
+    // the step that ended the run wrote the control block to hc (k_edges_end); otherwise (no
+    // step ran, or the host stopped at max_steps before seeing `done`) read it back
+    const bool ctl_written = !h0.done && __atomic_load_n(&c->lsig->done, __ATOMIC_ACQUIRE) != 0;
+    if (!ctl_written) MCS_HIP_CHECK(hipMemcpyAsync(hc, dctl, sizeof(LmCtl), hipMemcpyDeviceToHost, st));
     // per-edge chi2 of every edge at the final estimate, poses, points: the common tail (or
     // LocalBA's device culling)
     const int rtail = lba_tail ? lba_finish(poses, points) : download(poses, points, edge_chi2);
@@ -2524,11 +2634,11 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   }
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
-  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocDefault));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocMapped));   // k_lba_compact writes it
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->sig, sizeof(TrialSig), hipHostMallocCoherent | hipHostMallocMapped));
   std::memset((void*)c->sig, 0, sizeof(TrialSig));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->lsig, sizeof(LmSig), hipHostMallocCoherent | hipHostMallocMapped));
-  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_ctl, sizeof(LmCtl), hipHostMallocDefault));
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_ctl, sizeof(LmCtl), hipHostMallocMapped));   // k_edges_end writes it
   std::memset((void*)c->lsig, 0, sizeof(LmSig));
   *out = c;
   return MCS_OK;
