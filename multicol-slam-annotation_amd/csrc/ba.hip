@@ -250,6 +250,7 @@ struct Dev {
   double* poses; double* points; const double* poses_bk; const double* points_bk;
   // active structure
   const int32_t* aedge; int nae;
+  const uint8_t* elevel;   // per edge: 1 = level 1 (LocalBA round 2 keeps round 1's list), null = none
   const int32_t* pose_h; const int32_t* point_h;      // hessian index per vertex (-1 inactive)
   const int32_t* hpose_vtx; const int32_t* hpt_vtx;   // vertex id per hessian index
   int np, nl;
@@ -323,8 +324,10 @@ __global__ __launch_bounds__(256) void k_edges(Dev d0, int linearize) {
   const Dev d = lin_buf(d0, false);
   if (!linearize && d.part_chi) {   // trial chi2 of a device-driven step: + workgroup partial
     double r0 = 0.0;
-    if (k < d.nae) {
-      const int e = d.aedge ? d.aedge[k] : k;
+    const int e = k < d.nae ? (d.aedge ? d.aedge[k] : k) : 0;
+    if (k < d.nae && d.elevel && d.elevel[e]) {
+      d.rchi[k] = 0.0;   // level 1: outside the graph
+    } else if (k < d.nae) {
       const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
       double er[2];
       edge_error(d.poses + 6 * pi, d.points + 3 * li, d.mc + 6 * ci, d.cam + 17 * ci, d.e_meas + 2 * e, er);
@@ -341,6 +344,7 @@ __global__ __launch_bounds__(256) void k_edges(Dev d0, int linearize) {
   }
   if (k >= d.nae) return;
   const int e = d.aedge ? d.aedge[k] : k;   // null: every edge
+  if (d.elevel && d.elevel[e]) { d.rchi[k] = 0.0; return; }   // level 1: terms stay zero
   const int pi = d.e_pose[e], li = d.e_point[e], ci = d.e_cam[e];
   const double* pose = d.poses + 6 * pi;
   const double* X = d.points + 3 * li;
@@ -568,8 +572,15 @@ __global__ __launch_bounds__(kEdgeEndNT) void k_edges_end(Dev d0, Sum3 q, LmEnd 
   double r0 = 0.0;
   int e = 0, pi = 0, li = 0, ci = 0;
   double jp[12], jl[6];
-  if (k < d.nae) {
+  bool live = k < d.nae;
+  if (live) {
     e = d.aedge ? d.aedge[k] : k;
+    if (d.elevel && d.elevel[e]) {   // level 1: outside the graph, terms stay zero
+      live = false;
+      if (!jac) d.rchi[k] = 0.0;
+    }
+  }
+  if (live) {
     pi = d.e_pose[e]; li = d.e_point[e]; ci = d.e_cam[e];
     const double* pose = d.poses + 6 * pi;
     const double* X = d.points + 3 * li;
@@ -594,7 +605,7 @@ __global__ __launch_bounds__(kEdgeEndNT) void k_edges_end(Dev d0, Sum3 q, LmEnd 
     }
   }
   __syncthreads();
-  if (jac && spec && k < d.nae && d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
+  if (jac && spec && live && d.hpl && d.pose_h[pi] >= 0 && d.point_h[li] >= 0) {
     const double w = wsh[slot];
     for (int a = 0; a < 6; a++)
       for (int bb = 0; bb < 3; bb++)
@@ -1381,9 +1392,11 @@ __global__ __launch_bounds__(256) void k_zero_edges(Dev d, const int32_t* edges,
 // point's decisions depend only on its own edges, in edge order, so one thread per active point
 // walks its point-CSR list (pt_edges is in edge order and, in round 1, holds every edge of the
 // point) and decides exactly as the sequential pass does.  Round 1 also moves the culled edges to
-// level 1 and zeroes their per-edge terms (what Optimizer::remask's k_zero_edges does); then one
-// workgroup compacts the active-edge list and checks that no active pose lost all its edges
-// (g2o would drop it from the system: the host then rebuilds from scratch).
+// level 1 and zeroes their per-edge terms (what Optimizer::remask's k_zero_edges does), counts
+// the culled edges per pose and the points left, and its last workgroup reports whether an
+// active pose lost all its edges (g2o would drop it from the system: the host then rebuilds from
+// scratch).  Round 2 keeps round 1's active list; k_edges / k_edges_end skip its level-1 edges
+// (Dev::elevel), whose terms stay zero.  (A one-workgroup compaction of the list took 39 us.)
 struct LbaState {
   int32_t* obs_left; int32_t* edges_left; int32_t* edges_all;   // per point vertex
   uint8_t* bad;                                                  // per point vertex
@@ -1391,7 +1404,8 @@ struct LbaState {
   const int32_t* extra;                                          // extra observations (nullable)
   double* chi;                                                   // chi2 of every edge
   double k2;                                                     // thHuber^2
-  int32_t* keep;                                                 // compacted active list
+  int32_t* pose_cnt;                                             // active edges per active pose
+  uint32_t* ctr;                                                 // {culled edges, points left, arrivals}
   int32_t* res;                                                  // {nae, pose_left, nl_left} (host memory)
   uint8_t* pwrite;                                               // per point vertex (round 2)
 };
@@ -1436,19 +1450,67 @@ __global__ __launch_bounds__(256) void k_lba_cull(Dev d, LbaState L, int round1)
   if (!round1 && L.pwrite) L.pwrite[v] = !bad && el > 1 && L.edges_all[v] >= 2;
 }
 
+// round 1's bookkeeping after k_lba_cull's decisions: per-pose survivors (one atomic per culled
+// edge, integer counts), culled edges and points left (one atomic per wave); the last
+// workgroup writes the three counts into host memory
+__global__ __launch_bounds__(256) void k_lba_count(Dev d, LbaState L) {
+  __shared__ int last;
+  const int l = blockIdx.x * 256 + threadIdx.x;
+  int culled = 0, alive = 0;
+  if (l < d.nl) {
+    const int v = d.hpt_vtx[l];
+    const int el = L.edges_left[v];
+    alive = el > 0 ? 1 : 0;
+    culled = L.edges_all[v] - el;
+    if (culled) {
+      for (int q = d.pt_ptr[l]; q < d.pt_ptr[l + 1]; q++) {
+        const int e = d.pt_edges[q];
+        const int h = d.pt_h[q];
+        if (L.level[e] && h >= 0) atomicSub(&L.pose_cnt[h], 1);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { culled += __shfl_xor(culled, o); alive += __shfl_xor(alive, o); }
+  if ((threadIdx.x & 63) == 0) {
+    if (culled) atomicAdd(&L.ctr[0], (unsigned)culled);
+    if (alive) atomicAdd(&L.ctr[1], (unsigned)alive);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();   // release this workgroup's counts before counting in
+    last = atomicAdd(&L.ctr[2], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  int left = 0;
+  for (int h = threadIdx.x; h < d.np; h += 256) left |= __hip_atomic_load(&L.pose_cnt[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0 ? 1 : 0;
+  left = __syncthreads_or(left);
+  if (threadIdx.x == 0) {
+    const unsigned c0 = __hip_atomic_load(&L.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned c1 = __hip_atomic_load(&L.ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.res[0] = d.nae - (int)c0;
+    L.res[1] = left;
+    L.res[2] = (int)c1;
+  }
+}
+
 // the culling state before round 1: every edge an inlier at level 0, every point vertex clear
-__global__ __launch_bounds__(256) void k_lba_init(LbaState L, int ne, int npt) {
+__global__ __launch_bounds__(256) void k_lba_init(Dev d, LbaState L, int ne, int npt) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < ne) { L.inlier[i] = 1; L.level[i] = 0; }
+  if (i < d.np) L.pose_cnt[i] = d.ps_ptr[i + 1] - d.ps_ptr[i];
+  if (i < 4) L.ctr[i] = 0u;
   if (i < npt) {
     L.obs_left[i] = 0; L.edges_left[i] = 0; L.edges_all[i] = 0; L.bad[i] = 0;
     if (L.pwrite) L.pwrite[i] = 0;
   }
 }
-
-// per-thread contiguous chunks of the one-workgroup kernels below: up to this many elements
-// are loaded into registers with every load in flight before the first use
-constexpr int kChunkMax = 32;
 
 // LocalBA's round-2 results into host memory: [poses | points | inlier flags | write-back flags]
 __global__ __launch_bounds__(256) void k_lba_out(const double* poses, int npo, const double* points, int npt,
@@ -1461,104 +1523,6 @@ __global__ __launch_bounds__(256) void k_lba_out(const double* poses, int npo, c
   uint8_t* hb = host + 8 * (size_t)(npo + npt);
   if (i < ne) hb[i] = inl[i];
   if (i < npw) hb[ne + i] = pw[i];
-}
-
-// exclusive prefix of v over a 1024-thread workgroup (and the total)
-__device__ __forceinline__ int block_excl_scan1024(int v, int* sm, int* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sm[w] = x;
-  __syncthreads();
-  int base = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int t = sm[k];
-    base += k < w ? t : 0;
-    tot += t;
-  }
-  __syncthreads();
-  *total = tot;
-  return base + x - v;
-}
-
-// the round-2 active list in edge order (stable), per-pose survivors, active points left
-// (the per-pose survivors as bit sets: OR-reduced per wave, one LDS atomicOr per wave and word;
-// per-edge LDS atomics on ten counters serialised the workgroup: 38 us)
-__global__ __launch_bounds__(1024) void k_lba_compact(Dev d, LbaState L) {
-  constexpr int kPW = 2048 / 32;          // words of the pose bit set (np <= 2048)
-  __shared__ unsigned kept[kPW];
-  __shared__ int sm[16];
-  const int t = threadIdx.x, n = d.nae;
-  for (int h = t; h < kPW; h += 1024) kept[h] = 0u;
-  __syncthreads();
-  const int chunk = (n + 1023) / 1024, k0 = min(n, t * chunk), k1 = min(n, k0 + chunk);
-  int cnt = 0;
-  int total, o;
-  if (chunk <= kChunkMax) {
-    // the chunk's index loads, then its level / pose loads, all in flight together (one
-    // workgroup is latency-bound: one dependent chain per edge was 42 us at 20k edges)
-    int ev[kChunkMax], hv[kChunkMax];
-    bool kv[kChunkMax];
-#pragma unroll
-    for (int j = 0; j < kChunkMax; j++) {
-      const int k = min(k0 + j, max(k1 - 1, 0));
-      ev[j] = d.aedge ? d.aedge[k] : k;
-    }
-#pragma unroll
-    for (int j = 0; j < kChunkMax; j++) { kv[j] = k0 + j < k1 && !L.level[ev[j]]; hv[j] = d.e_pose[ev[j]]; }
-    // poses of this thread's kept edges: the first 64 Hessian indices as a bit set (LocalBA
-    // sizes), the rest one atomic each
-    uint64_t pm = 0;
-#pragma unroll
-    for (int j = 0; j < kChunkMax; j++) hv[j] = kv[j] ? d.pose_h[hv[j]] : -1;
-#pragma unroll
-    for (int j = 0; j < kChunkMax; j++) {
-      if (!kv[j]) continue;
-      cnt++;
-      const int h = hv[j];
-      if (h >= 0 && h < 64) pm |= 1ull << h;
-      else if (h >= 64) atomicOr(&kept[h >> 5], 1u << (h & 31));
-    }
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) pm |= __shfl_xor(pm, o2);
-    if ((t & 63) == 0 && pm) { atomicOr(&kept[0], (unsigned)pm); atomicOr(&kept[1], (unsigned)(pm >> 32)); }
-    o = block_excl_scan1024(cnt, sm, &total);
-#pragma unroll
-    for (int j = 0; j < kChunkMax; j++)
-      if (kv[j]) L.keep[o++] = ev[j];
-  } else {
-    for (int k = k0; k < k1; k++) {
-      const int e = d.aedge ? d.aedge[k] : k;
-      if (L.level[e]) continue;
-      cnt++;
-      const int h = d.pose_h[d.e_pose[e]];
-      if (h >= 0) atomicOr(&kept[h >> 5], 1u << (h & 31));
-    }
-    o = block_excl_scan1024(cnt, sm, &total);
-    for (int k = k0; k < k1; k++) {
-      const int e = d.aedge ? d.aedge[k] : k;
-      if (!L.level[e]) L.keep[o++] = e;
-    }
-  }
-  int nl = 0;
-  for (int l0 = t; l0 < d.nl; l0 += 4096) {
-    int vx[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) vx[u] = d.hpt_vtx[min(l0 + 1024 * u, d.nl - 1)];
-#pragma unroll
-    for (int u = 0; u < 4; u++) nl += (l0 + 1024 * u < d.nl && L.edges_left[vx[u]] > 0) ? 1 : 0;
-  }
-  int left = 0;
-  for (int h = t; h < d.np; h += 1024) left |= ((kept[h >> 5] >> (h & 31)) & 1u) ? 0 : 1;
-  int nl_tot, left_any;
-  (void)block_excl_scan1024(nl, sm, &nl_tot);
-  (void)block_excl_scan1024(left, sm, &left_any);
-  if (t == 0) { L.res[0] = total; L.res[1] = left_any > 0 ? 1 : 0; L.res[2] = nl_tot; }
 }
 
 // the trial's pop (restore every pose and point from the backups) in one launch
@@ -1966,15 +1930,16 @@ struct Optimizer {
       L.pwrite = (uint8_t*)c->alloc(npt);
       L.inlier = (uint8_t*)c->alloc(ne);
       L.level = (uint8_t*)c->alloc(ne);
-      L.keep = (int32_t*)c->alloc(4 * ne);
-      L.res = c->pinned_i;   // written by k_lba_compact straight into host memory
+      L.pose_cnt = (int32_t*)c->alloc(4 * (size_t)std::max(1, s.np));
+      L.ctr = (uint32_t*)c->alloc(16);
+      L.res = c->pinned_i;   // written by k_lba_count straight into host memory
       L.chi = d.chi;
       L.k2 = p->huber_delta * p->huber_delta;
       if (!L.obs_left || !L.edges_left || !L.edges_all || !L.bad || !L.pwrite || !L.inlier || !L.level ||
-          !L.keep || !L.res)
+          !L.pose_cnt || !L.ctr)
         he = hipErrorOutOfMemory;
       else
-        hipLaunchKernelGGL(k_lba_init, dim3(gb(std::max(NE, p->n_points))), dim3(256), 0, st, L, NE,
+        hipLaunchKernelGGL(k_lba_init, dim3(gb(std::max(NE, p->n_points))), dim3(256), 0, st, d, L, NE,
                            p->n_points);
     }
     if (he != hipSuccess) { set_hip_error(he, "BA upload", __FILE__, __LINE__); return MCS_ERR_HIP; }
@@ -2103,25 +2068,25 @@ struct Optimizer {
     return MCS_OK;
   }
 
-  // Round 2 of a device-culled LocalBA: the compacted active list from round 1's tail (no host
-  // round trip: the culled edges' terms were zeroed by k_lba_cull)
+  // Round 2 of a device-culled LocalBA: round 1's active list with its level-1 edges skipped
+  // (no host round trip: the culled edges' terms were zeroed by k_lba_cull)
   void remask_device() {
-    d.aedge = L.keep;
-    d.nae = lba_res[0];
-    nae_glob = d.nae;
+    d.elevel = L.level;   // round 1's list; its level-1 edges are skipped (terms zeroed)
+    nae_glob = lba_res[0];
     nl_glob = lba_res[2];
     sig_path = !sharded && d.nae <= 32768 && s.nl <= 32768 && s.np <= 32768;
   }
 
   // run_device's tail for LocalBA (lba_tail 1..3): chi2 of every edge at the final estimate,
-  // the culling pass, and either the round-2 active list (round 1: nothing is downloaded; the
-  // host reads three counts) or the results (round 2: poses, points, inlier flags, write-back)
+  // the culling pass, and either round 2's counts (round 1: nothing is downloaded; the host
+  // reads three counts) or the results (round 2: poses, points, inlier flags, write-back)
   int lba_finish(double* poses, double* points) {
     HostClock hc;
     if (lba_tail <= 2) {
       Dev d2 = d;
       d2.ctl = nullptr;
       d2.aedge = nullptr;
+      d2.elevel = nullptr;
       d2.nae = NE;
       d2.err = dz(2 * (size_t)NE);
       d2.rchi = dz(NE);
@@ -2130,7 +2095,7 @@ struct Optimizer {
       hipLaunchKernelGGL(k_lba_cull, dim3(gb(s.nl)), dim3(256), 0, st, d, L, lba_tail == 1 ? 1 : 0);
     }
     if (lba_tail == 1) {
-      hipLaunchKernelGGL(k_lba_compact, dim3(1), dim3(1024), 0, st, d, L);
+      hipLaunchKernelGGL(k_lba_count, dim3(gb(s.nl)), dim3(256), 0, st, d, L);
       MCS_HIP_CHECK(spin_sync(st));
       std::memcpy(lba_res, c->pinned_i, 12);
       hc.mark(c->host_ms, 3);
@@ -2430,6 +2395,7 @@ struct Optimizer {
       Dev d2 = d;
       d2.ctl = nullptr;
       d2.aedge = nullptr;
+      d2.elevel = nullptr;
       d2.nae = NE;
       d2.err = dz(2 * (size_t)NE);
       d2.rchi = dz(NE);
@@ -2634,7 +2600,7 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   }
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
-  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocMapped));   // k_lba_compact writes it
+  MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocMapped));   // k_lba_count writes it
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->sig, sizeof(TrialSig), hipHostMallocCoherent | hipHostMallocMapped));
   std::memset((void*)c->sig, 0, sizeof(TrialSig));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->lsig, sizeof(LmSig), hipHostMallocCoherent | hipHostMallocMapped));
