@@ -499,7 +499,11 @@ __device__ void lm_end_body(const Dev& d, const Sum3& q, const LmEnd& le) {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         double acc = 0.0;
-        for (int i = t + 256 * u; i < q.n[b]; i += 1024) acc = acc + v[i];
+        // sc1 loads: k_edges_end's partials arrive write-through, without an acquire
+        for (int i = t + 256 * u; i < q.n[b]; i += 1024)
+          acc = acc + __longlong_as_double((long long)__hip_atomic_load(
+                          (const __attribute__((address_space(1))) unsigned long long*)(v + i), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT));
         x[u] = acc;
       }
       x[0] = x[0] + x[2];   // o = 512
@@ -619,20 +623,20 @@ __global__ __launch_bounds__(kEdgeEndNT) void k_edges_end(Dev d0, Sum3 q, LmEnd 
     if (!jac && (threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
   }
   __syncthreads();
+  // The partial goes write-through (sc1 store), its wait drains before the arrival add, and the
+  // last workgroup reads every partial with sc1 loads (lm_end_body): the hand-off of
+  // MI355X_MICROARCH.md's first table row, with no L2 write-back (a __threadfence per workgroup
+  // wrote back the ~6 MB of Jacobians this kernel leaves dirty) and no acquire.
   if (threadIdx.x == 0) {
-    d.part_chi[blockIdx.x] = ((sm[0] + sm[1]) + sm[2]) + sm[3];
-    __threadfence();   // release the partial before counting in
-    last = atomicAdd(&c->arrive, 1u) == gridDim.x - 1;
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(d.part_chi + blockIdx.x),
+                       (unsigned long long)__double_as_longlong(((sm[0] + sm[1]) + sm[2]) + sm[3]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(&c->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  // acquire: every workgroup's partial (one lane; the barrier holds the rest until it is done)
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
-  }
-  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&c->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
   lm_end_body(d0, q, le);
 }
 
