@@ -261,6 +261,7 @@ struct Dev {
   const int32_t* it_blk; const int32_t* it_chunk; const int32_t* it_slot;  // k_schur items
   const int32_t* blk_nch; const int32_t* blk_slot0;  // chunks / first partial slot per block
   double* schur_part;                                 // [slots][42]
+  uint32_t* blk_arrive;                               // per block: chunks arrived (fused fin; null: k_schur_fin)
   double lam, lam0;                                   // lambda; lambda on rank 0, 0 elsewhere
   const int32_t* pr_ptr; const uint2* pr;             // edge pairs (e1, e2) per block
   const int32_t* nitem;                               // k_schur items (device-built count)
@@ -658,12 +659,15 @@ __device__ __forceinline__ void lm_lambda0_body(LmCtl* c, double pt, double pose
   c->nBad = 0;
 }
 // the LM control block of a run, by value (no pageable host copy on the stream)
-__global__ void k_ctl_init(LmCtl h0, LmCtl* c) {
+// (+ the per-block chunk counters of k_schur's fused fin, zeroed)
+__global__ void k_ctl_init(LmCtl h0, LmCtl* c, uint32_t* blk_arrive, int nblk) {
   constexpr int nw = (int)(sizeof(LmCtl) / 4);
   static_assert(sizeof(LmCtl) % 4 == 0, "word copy");
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&h0);
   uint32_t* dst = reinterpret_cast<uint32_t*>(c);
   for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+  if (blk_arrive)
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) blk_arrive[i] = 0u;
 }
 __global__ void k_lm_lambda0(LmCtl* c, const double* sc) {
   if (threadIdx.x != 0 || c->done) return;
@@ -1166,9 +1170,46 @@ __global__ __launch_bounds__(256) void k_schur(Dev d0) {
   // sum, bit for bit, as a full xor butterfly forms for every value), so 44 exchanges instead
   // of 6 x 42, and sum v ends in one lane (wave_halve_all), which writes it
   const int v = wave_halve_all<42>(acc, lane);
-  if (v < 0) return;
-  if (slot < 0) schur_write(d, bi, bj, lam0, v, acc[0]);
-  else d.schur_part[(size_t)slot * 42 + v] = acc[0];
+  if (slot < 0) {
+    if (v >= 0) schur_write(d, bi, bj, lam0, v, acc[0]);
+    return;
+  }
+  if (!d.blk_arrive) {   // k_schur_fin adds the slots
+    if (v >= 0) d.schur_part[(size_t)slot * 42 + v] = acc[0];
+    return;
+  }
+  // Fused fin (one-tile systems): the slot goes write-through (sc1), the wave's stores drain, one
+  // lane counts the chunk in; the wave whose chunk arrives last adds the block's slots in chunk
+  // order with sc1 loads (k_schur_fin's order and bits) and writes S / bschur.  Each wave hands
+  // off for itself (MI355X_MICROARCH.md, first table row): no fence, no extra launch.
+  if (v >= 0)
+    __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)(d.schur_part + (size_t)slot * 42 + v),
+                       (unsigned long long)__double_as_longlong(acc[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int n = d.blk_nch[blk];
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(&d.blk_arrive[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __builtin_amdgcn_readfirstlane(prev);
+  if ((int)prev != n - 1) return;
+  if (lane == 0) __hip_atomic_store(&d.blk_arrive[blk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next step
+  const int s0 = d.blk_slot0[blk];
+  double sum = 0.0;
+  if (lane < 42) {
+    const __attribute__((address_space(1))) unsigned long long* P =
+        (const __attribute__((address_space(1))) unsigned long long*)(d.schur_part + (size_t)s0 * 42 + lane);
+    int cc = 0;
+    for (; cc + 8 <= n; cc += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        t[u] = __longlong_as_double((long long)__hip_atomic_load(P + (size_t)(cc + u) * 42, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+      for (int u = 0; u < 8; u++) sum += t[u];
+    }
+    for (; cc < n; cc++)
+      sum += __longlong_as_double((long long)__hip_atomic_load(P + (size_t)cc * 42, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  schur_write(d, bi, bj, lam0, lane, sum);
 }
 
 // blocks split into several chunks: sum the chunk slots in chunk order, then write (one wave
@@ -1176,7 +1217,7 @@ __global__ __launch_bounds__(256) void k_schur(Dev d0) {
 // k_schur by the wave whose chunk arrives last (agent release / atomic / acquire): equal at
 // config C, 2.6x slower k_schur at config E, whose 199 diagonal blocks split 16 ways.
 __global__ __launch_bounds__(256) void k_schur_fin(Dev d, int nblk) {
-  if (lm_done(d)) return;
+  if (lm_done(d) || d.blk_arrive) return;
   const double lam0 = lam0_of(d);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + w;
@@ -2451,9 +2492,11 @@ struct Optimizer {
     h0.done = (empty || o->max_iterations <= 0 || *stop != 0) ? 1 : 0;
     c->lsig->ext_stop = *stop != 0;
     c->lsig->done = 0;   // this run's `done` (the previous run's stream has drained)
-    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(256), 0, st, h0, dctl);
     Dev dd = d;
     dd.ctl = dctl;
+    // one-tile systems (LocalBA): k_schur adds a split block's chunk slots itself (fused fin)
+    dd.blk_arrive = (T == 1 && nblk > 0) ? (uint32_t*)c->alloc(4 * (size_t)nblk) : nullptr;
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(256), 0, st, h0, dctl, dd.blk_arrive, nblk);
     const int* skip = &dctl->done;
     const unsigned g_upd = gb(4 * s.nl + s.np), g_edg = gb(d.nae);
     dd.part_chi = dz(g_edg);
@@ -2490,7 +2533,8 @@ struct Optimizer {
       }
       if (s.np) {
         hipLaunchKernelGGL(k_schur, dim3((unsigned)((items_max + 3) / 4)), dim3(256), 0, st, dd);
-        hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, dd, nblk);
+        if (!dd.blk_arrive)
+          hipLaunchKernelGGL(k_schur_fin, dim3((unsigned)((nblk + 3) / 4)), dim3(256), 0, st, dd, nblk);
         if (T == 1) MCS_HIP_CHECK(ldlt::solve_one_tile(d.S, d.bs, d.xp, n, 1.0, d_flag, st, skip));
         else {
           MCS_HIP_CHECK(ldlt::pad(d.S, d.bs, n, T, 1.0, st, skip));
