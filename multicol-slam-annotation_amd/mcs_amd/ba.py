@@ -51,17 +51,35 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+_PROBLEM_FIELDS = (("poses", np.float64), ("pose_fixed", np.uint8), ("points", np.float64),
+                   ("mc", np.float64), ("cam", np.float64), ("edge_pose", np.int32),
+                   ("edge_point", np.int32), ("edge_cam", np.int32), ("edge_meas", np.float64),
+                   ("edge_info", np.float64))
+
+
+_STRUCT_CACHE = []   # (arrays, huber_delta, BAProblem), most recent last, a few entries
+
+
 def as_struct(pr):
-    """numpy problem dict -> BAProblem (keeps references alive in the dict)."""
-    for k, dt in (("poses", np.float64), ("pose_fixed", np.uint8), ("points", np.float64),
-                  ("mc", np.float64), ("cam", np.float64), ("edge_pose", np.int32),
-                  ("edge_point", np.int32), ("edge_cam", np.int32), ("edge_meas", np.float64),
-                  ("edge_info", np.float64)):
-        pr[k] = np.ascontiguousarray(pr[k], dtype=dt)
+    """numpy problem dict -> BAProblem (keeps references alive in the dict).  A dict whose
+    arrays are the same objects as at an earlier call (values may have changed in place) gets
+    that call's struct back: the addresses are the same, and reading ten array addresses cost
+    ~30 us of a ~2.3 ms LocalBA call."""
+    arrs = tuple(pr[k] for k, _ in _PROBLEM_FIELDS)
+    hd = float(pr["huber_delta"])
+    for ent in _STRUCT_CACHE:
+        if ent[1] == hd and all(x is y for x, y in zip(ent[0], arrs)):
+            return ent[2]
+    addr = []
+    for k, dt in _PROBLEM_FIELDS:
+        a = pr[k]
+        if not (isinstance(a, np.ndarray) and a.dtype == dt and a.flags.c_contiguous):
+            a = pr[k] = np.ascontiguousarray(a, dtype=dt)
+        addr.append(a.__array_interface__["data"][0])
     s = BAProblem(len(pr["poses"]), len(pr["points"]), len(pr["edge_pose"]), len(pr["mc"]),
-                  _p(pr["poses"]), _p(pr["pose_fixed"]), _p(pr["points"]), _p(pr["mc"]),
-                  _p(pr["cam"]), _p(pr["edge_pose"]), _p(pr["edge_point"]), _p(pr["edge_cam"]),
-                  _p(pr["edge_meas"]), _p(pr["edge_info"]), float(pr["huber_delta"]))
+                  *addr, hd)
+    _STRUCT_CACHE.append((tuple(pr[k] for k, _ in _PROBLEM_FIELDS), hd, s))
+    del _STRUCT_CACHE[:-4]
     return s
 
 
