@@ -1521,18 +1521,14 @@ __global__ __launch_bounds__(256) void k_lba_count(Dev d, LbaState L) {
     if (culled) atomicAdd(&L.ctr[0], (unsigned)culled);
     if (alive) atomicAdd(&L.ctr[1], (unsigned)alive);
   }
+  // every count is an atomic (performed in device-coherent memory): each wave drains its own,
+  // then one lane counts the workgroup in; the last one reads them with atomic loads
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();   // release this workgroup's counts before counting in
-    last = atomicAdd(&L.ctr[2], 1u) == gridDim.x - 1;
-  }
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&L.ctr[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   int left = 0;
   for (int h = threadIdx.x; h < d.np; h += 256) left |= __hip_atomic_load(&L.pose_cnt[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0 ? 1 : 0;
   left = __syncthreads_or(left);
@@ -1897,9 +1893,12 @@ struct Optimizer {
       pk.add(&d.e_info, p->edge_info, (size_t)NE);
       pk.add(&d_poses, poses, 6 * (size_t)p->n_poses);
       pk.add(&d_points, points, 3 * (size_t)p->n_points);
-      pk.add(&d_poses_bk, poses, 6 * (size_t)p->n_poses);
-      pk.add(&d_points_bk, points, 3 * (size_t)p->n_points);
-      pk.add(&d.aedge, s.aedge);
+      // the trial backups are written by every trial's push before anything reads them: space only
+      pk.add(&d_poses_bk, static_cast<const double*>(nullptr), 6 * (size_t)p->n_poses);
+      pk.add(&d_points_bk, static_cast<const double*>(nullptr), 3 * (size_t)p->n_points);
+      // every edge active (LocalBA round 1, GlobalBA): no list, the kernels index edges directly
+      if ((int)s.aedge.size() != NE) pk.add(&d.aedge, s.aedge);
+      else d.aedge = nullptr;
       pk.add(&d.pose_h, s.pose_h); pk.add(&d.point_h, s.point_h);
       pk.add(&d.hpose_vtx, s.hpose_vtx); pk.add(&d.hpt_vtx, s.hpt_vtx);
       pk.add(&d.pt_ptr, s.pt_ptr); pk.add(&d.pt_edges, s.pt_edges); pk.add(&d.pt_h, s.pt_h);
