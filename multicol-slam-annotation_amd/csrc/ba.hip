@@ -2494,7 +2494,9 @@ struct Optimizer {
     Dev dd = d;
     dd.ctl = dctl;
     // one-tile systems (LocalBA): k_schur adds a split block's chunk slots itself (fused fin)
-    dd.blk_arrive = (T == 1 && nblk > 0) ? (uint32_t*)c->alloc(4 * (size_t)nblk) : nullptr;
+    static const int fuse_env = [] { const char* e = std::getenv("MCS_FUSE_FIN"); return e ? std::atoi(e) : -1; }();
+    const bool fuse = fuse_env >= 0 ? fuse_env != 0 : T == 1;
+    dd.blk_arrive = (fuse && nblk > 0) ? (uint32_t*)c->alloc(4 * (size_t)nblk) : nullptr;
     hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(256), 0, st, h0, dctl, dd.blk_arrive, nblk);
     const int* skip = &dctl->done;
     const unsigned g_upd = gb(4 * s.nl + s.np), g_edg = gb(d.nae);
