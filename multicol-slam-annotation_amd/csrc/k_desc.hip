@@ -299,8 +299,9 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   // any lane of the wave is that close takes the double form for every lane (rare), so every
   // offset is the double form's, bit for bit.  (Software-pipelining several pairs per wave
   // was measured slower: 0.71 -> 0.94-1.13 ms per step, fewer waves per SIMD; cos / sin in
-  // float with the double pair only for the rare exact rounds: 0.72 -> 0.77 ms; the two points
-  // of a test in packed f32: 0.72 -> 0.72 ms.)
+  // float with the double pair only for the rare exact rounds: 0.72 -> 0.77 ms, also with the
+  // double pair formed lazily inside that branch (OCML sincosf costs about what the double
+  // sincos does); the two points of a test in packed f32: 0.72 -> 0.72 ms.)
   const float caf = (float)ca, saf = (float)sa;
   auto near_half = [](float v, float rv) { return fabsf(v - rv) > 0.5f - 1e-5f; };
   for (int r = 0; r < nw; r++) {
