@@ -1,0 +1,44 @@
+// Host structure of one BA call (ba_structure.hpp: scan_edges + build_structure), dumped as
+// text for tests/test_ba_structure_host.py.  Input (stdin): n_poses n_points n_edges n_cams
+// points_fixed has_level, then pose_fixed[n_poses], then per edge: pose point cam level.
+#include <cstdio>
+#include <vector>
+#include "../../multicol-slam-annotation_amd/csrc/ba_structure.hpp"
+
+static void dump(const char* name, const std::vector<int32_t>& v) {
+  std::printf("%s %zu", name, v.size());
+  for (int32_t x : v) std::printf(" %d", x);
+  std::printf("\n");
+}
+
+int main() {
+  int np, npt, ne, nc, pf, hl;
+  if (std::scanf("%d %d %d %d %d %d", &np, &npt, &ne, &nc, &pf, &hl) != 6) return 2;
+  std::vector<uint8_t> fixed(np), level(ne);
+  std::vector<int32_t> ep(ne), el(ne), ec(ne);
+  for (int i = 0; i < np; i++) { int v; if (std::scanf("%d", &v) != 1) return 2; fixed[i] = (uint8_t)v; }
+  for (int e = 0; e < ne; e++) {
+    int lv;
+    if (std::scanf("%d %d %d %d", &ep[e], &el[e], &ec[e], &lv) != 4) return 2;
+    level[e] = (uint8_t)lv;
+  }
+  mcs_ba_problem p{};
+  p.n_poses = np; p.n_points = npt; p.n_edges = ne; p.n_cams = nc;
+  p.edge_pose = ep.data(); p.edge_point = el.data(); p.edge_cam = ec.data(); p.pose_fixed = fixed.data();
+  mcs::ba::HostStruct s;
+  std::vector<double> cnt;
+  // twice on one HostStruct: capacities are reused across calls, the result must not depend on it
+  for (int rep = 0; rep < 2; rep++) {
+    if (!mcs::ba::scan_edges(p, hl ? level.data() : nullptr, pf != 0, s, cnt)) { std::printf("bad\n"); return 0; }
+    mcs::ba::build_structure(p, pf != 0, cnt, s);
+  }
+  std::printf("np %d nl %d\n", s.np, s.nl);
+  std::vector<int32_t> ci(cnt.size());
+  for (size_t i = 0; i < cnt.size(); i++) ci[i] = (int32_t)cnt[i];
+  dump("cnt", ci);
+  dump("aedge", s.aedge); dump("pose_h", s.pose_h); dump("point_h", s.point_h);
+  dump("hpose_vtx", s.hpose_vtx); dump("hpt_vtx", s.hpt_vtx); dump("pt_ptr", s.pt_ptr);
+  dump("pt_edges", s.pt_edges); dump("pt_h", s.pt_h); dump("ps_ptr", s.ps_ptr); dump("ps_edges", s.ps_edges);
+  dump("blk_i", s.blk_i); dump("blk_j", s.blk_j);
+  return 0;
+}
