@@ -738,31 +738,6 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// k_pipe's consumers read every handed-off byte with sc1 loads (buffer / global, never flat):
-// with the producers' sc1 stores, drained waits and one-lane flags this is the hand-off of
-// MI355X_MICROARCH.md's first visibility row, which needs no acquire fence after a wait (the
-// fence is ~1.7 us per wait, two waits on the diagonal chain per step).  Default (0): plain
-// loads behind an agent-scope acquire; MCS_LDLT_SC1=1 builds the sc1 form (A/B variant).
-#ifndef MCS_LDLT_SC1
-#define MCS_LDLT_SC1 0
-#endif
-__device__ __forceinline__ void fetch_tile_h(d2 (&v)[8], const double* __restrict__ g) {
-  if (MCS_LDLT_SC1) {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g), 0, TB * TB * 8, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-      v[i] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (threadIdx.x + 256 * i), 0, 16));
-  } else {
-    fetch_tile(v, g);
-  }
-}
-__device__ __forceinline__ double ld_h(const double* p) {
-  if (MCS_LDLT_SC1)
-    return __longlong_as_double((long long)__hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  return *p;
-}
-
 // 64x64 tile from LDS (stride LS) to global (row-major), write-through, 16 B per store
 __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, TB * TB * 8, 0x00020000);
@@ -778,7 +753,7 @@ __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
 // outcome (false: timed out here or elsewhere).
 __device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const unsigned* w1, unsigned v1,
                                      const unsigned* w2, unsigned v2, unsigned* err, int* sh_ok,
-                                     long long ticks, bool acquire = true) {
+                                     long long ticks) {
   if (threadIdx.x == 0) {
     int ok = 1;
     const long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -788,7 +763,7 @@ __device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const u
       if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { pl_store(err, 1u); ok = 0; break; }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (ok && acquire) {
+    if (ok) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -886,7 +861,7 @@ __device__ __forceinline__ void load_acc(double (&a)[4][4], const double* Aij) {
 #pragma unroll
   for (int q = 0; q < 4; q++)
 #pragma unroll
-    for (int r = 0; r < 4; r++) a[q][r] = ld_h(Aij + (16 * q + k4 + 4 * r) * TB + col);
+    for (int r = 0; r < 4; r++) a[q][r] = Aij[(16 * q + k4 + 4 * r) * TB + col];
 }
 
 // the 10 lower and 6 strict-upper 16x16 blocks of a diagonal tile
@@ -922,13 +897,12 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     DSTAMP(k, 0);
     // A_kk after products 0 .. k-2 (UPDATE tasks), then product k-1 from the tiles this
     // workgroup formed at step k-1 (still in sX / sY, u_{k-1} in su)
-    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks,
-                           !MCS_LDLT_SC1)) break;
+    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
     DSTAMP(k, 1);
     // A_kk -= L_{k,k-1} W_{k,k-1}^T on the 10 lower 16x16 blocks only (the upper ones are
     // not read by the factorisation), 3 / 3 / 2 / 2 blocks per wave; each block is the same
     // MFMA chain (k ascending) as the full gemm_xyt, so the bits are the full product's
-    double bv = ld_h(g.b + k * TB + (t >> 2));
+    double bv = g.b[k * TB + (t >> 2)];
     {
       const double* Akk = g.A + toff(k, k, T);
       const int nb = w < 2 ? 3 : 2, b0 = w < 2 ? 3 * w : 6 + 2 * (w - 2);
@@ -938,7 +912,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
         if (q < nb) {
           const int bi = kLowBi[b0 + q], bj = kLowBj[b0 + q];
 #pragma unroll
-          for (int r = 0; r < 4; r++) a[q][r] = ld_h(Akk + (16 * bi + k4 + 4 * r) * TB + 16 * bj + r16);
+          for (int r = 0; r < 4; r++) a[q][r] = Akk[(16 * bi + k4 + 4 * r) * TB + 16 * bj + r16];
         }
       }
       if (k >= 1) bv -= gemv_row(sX, su);
@@ -992,12 +966,11 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     DSTAMP(k, 4);
     if (k + 1 < T) {
       // the next panel tile: A_{k+1,k} after products 0 .. k-1
-      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks,
-                   !MCS_LDLT_SC1)) break;
+      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
       DSTAMP(k, 5);
       {
         d2 v[8];
-        fetch_tile_h(v, g.A + toff(k + 1, k, T));
+        fetch_tile(v, g.A + toff(k + 1, k, T));
         put_tile(sX, v);
       }
       if (t < TB) sv[t] = sK[t * LS + t];
@@ -1023,14 +996,13 @@ __device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_o
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
   unsigned* dg = pan + g.ntile;
-  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok, g.wait_ticks, !MCS_LDLT_SC1))
-    return false;
+  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok, g.wait_ticks)) return false;
   TSTAMP(tk, 1);
   {
     d2 vx[8], vi[8];
-    fetch_tile_h(vx, g.A + toff(i, k, T));
-    fetch_tile_h(vi, g.Linv + (size_t)k * TB * TB);
-    if (t < TB) sv[t] = ld_h(g.du + (size_t)k * 128 + t);
+    fetch_tile(vx, g.A + toff(i, k, T));
+    fetch_tile(vi, g.Linv + (size_t)k * TB * TB);
+    if (t < TB) sv[t] = g.du[(size_t)k * 128 + t];
     put_tile(sX, vx);
     put_tile(sI, vi);
   }
@@ -1051,20 +1023,19 @@ __device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, 
   unsigned* err = g.sync + 1;
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
-  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok, g.wait_ticks,
-               !MCS_LDLT_SC1))
+  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok, g.wait_ticks))
     return false;
   TSTAMP(tk, 1);
   double a[4][4];
   double bv = 0.0;
   {
     d2 vx[8], vy[8];
-    fetch_tile_h(vx, g.L + toff(i, k, T));
-    fetch_tile_h(vy, g.W + toff(j, k, T));
+    fetch_tile(vx, g.L + toff(i, k, T));
+    fetch_tile(vy, g.W + toff(j, k, T));
     load_acc(a, g.A + toff(i, j, T));
     if (i == j) {
-      bv = ld_h(g.b + i * TB + (t >> 2));
-      if (t < TB) su[t] = ld_h(g.du + (size_t)k * 128 + TB + t);
+      bv = g.b[i * TB + (t >> 2)];
+      if (t < TB) su[t] = g.du[(size_t)k * 128 + TB + t];
     }
     put_tile(sX, vx);
     put_tile(sY, vy);
