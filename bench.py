@@ -349,12 +349,14 @@ def run_global_ba(args, rank, world, local_rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    solver.read_host_timing(reset=True)
     t0 = time.perf_counter()
     iters = 0
     for _ in range(args.gba_calls):
         r = solver.global_ba(sub, exchange=xch)
         iters += r["report"].iterations
     tg = time.perf_counter() - t0
+    host_ms, _ = solver.read_host_timing(reset=True)
     # stage breakdown from one more call with per-stage HIP events (that call synchronises per
     # trial, so it is not part of the timed calls above)
     solver.enable_timing(True)
@@ -379,6 +381,7 @@ def run_global_ba(args, rank, world, local_rank, dev):
            "problem": "config E: %d MKF (1 fixed), %d points, %d edges, 8 cams 1024^2" % (
                len(pr["poses"]), len(pr["points"]), len(pr["edge_pose"])),
            "stage_ms_per_trial": {k: round(v / max(1, n_tr), 4) for k, v in st.items()},
+           "host_ms_per_call": {k: round(v / args.gba_calls, 4) for k, v in host_ms.items()},
            "trials": n_tr,
            "roofline_solve": {"kernel": "ldlt k_pipe (pipelined factorisation, one launch) + k_bwd (n=%d)" % n, "bound": "mfma",
                               "achieved": None if achieved is None else round(achieved, 4),

@@ -25,7 +25,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <new>
+#include <thread>
 #include <vector>
 #include <string.h>
 #include <rocprim/rocprim.hpp>
@@ -1583,6 +1585,20 @@ using namespace mcs::ba;
 struct mcs_ba_ctx {
   int device = 0;
   HostStruct hs;
+  // host threads for config-E-sized calls (structure build, staging copy); made on the first
+  // call with at least kParMinEdges edges.  MCS_HOST_THREADS: their number (default 8, 1: off)
+  std::unique_ptr<mcs::HostPool> pool;
+  mcs::HostPool* pool_for(int n_edges) {
+    if (n_edges < kParMinEdges) return nullptr;
+    if (!pool) {
+      const char* e = std::getenv("MCS_HOST_THREADS");
+      int t = e ? std::atoi(e) : 8;
+      const int hw = (int)std::thread::hardware_concurrency();
+      if (hw > 0) t = std::min(t, hw);
+      pool.reset(new mcs::HostPool(std::max(1, std::min(t, 16))));
+    }
+    return pool->size() > 1 ? pool.get() : nullptr;
+  }
   hipStream_t st = nullptr;
   // Device buffers are cached across calls: the driver requests them in the same order
   // every call, so request k reuses slot k when it is large enough (grow-only).
@@ -1687,16 +1703,27 @@ struct Packer {
   }
   template <typename D, typename T>
   void add(D** dst, const std::vector<T>& v) { add(dst, v.data(), v.size()); }
-  hipError_t flush(mcs_ba_ctx* c) {
+  hipError_t flush(mcs_ba_ctx* c, mcs::HostPool* pool = nullptr) {
     uint8_t* d = (uint8_t*)c->alloc(std::max<size_t>(total, 256));
     if (!d) return hipErrorOutOfMemory;
     hipError_t e = spin_sync(c->st);   // the staging buffer is free again
     if (e != hipSuccess) return e;
     uint8_t* h = c->stage_get(std::max<size_t>(total, 256));
     if (!h) return hipErrorOutOfMemory;
-    for (const Item& it : items) {
-      if (it.bytes) std::memcpy(h + it.off, it.src, it.bytes);
-      *it.dst = d + it.off;
+    for (const Item& it : items) *it.dst = d + it.off;
+    if (pool && total >= ((size_t)4 << 20)) {
+      // config E packs ~20 MB: the staging copy split by byte range over the host threads
+      const int T = pool->size();
+      pool->run([&](int t) {
+        const size_t lo = total * t / T, hi = total * (t + 1) / T;
+        for (const Item& it : items) {
+          const size_t a = std::max(lo, it.off), b = std::min(hi, it.off + it.bytes);
+          if (a < b) std::memcpy(h + a, (const uint8_t*)it.src + (a - it.off), b - a);
+        }
+      });
+    } else {
+      for (const Item& it : items)
+        if (it.bytes) std::memcpy(h + it.off, it.src, it.bytes);
     }
     return total ? hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, c->st) : hipSuccess;
   }
@@ -1825,7 +1852,8 @@ struct Optimizer {
     // ---- structure, pass 1: the index checks, the active edges and their per-pose / per-point
     // counts (+ active point / edge counts), all-reduced over the shards below
     std::vector<double> cnt;
-    if (!scan_edges(*p, edge_level, points_fixed, s, cnt)) {
+    mcs::HostPool* const pool = c->pool_for(p->n_edges);
+    if (!scan_edges(*p, edge_level, points_fixed, s, cnt, pool)) {
       set_error("edge vertex index out of range");
       return MCS_ERR_ARG;
     }
@@ -1851,7 +1879,7 @@ struct Optimizer {
     int rc;
     if ((rc = allreduce_host(cnt.data(), p->n_poses + 2, MCS_REDUCE_SUM, 0))) return rc;
     hc.mark(c->host_ms, 0);
-    build_structure(*p, points_fixed, cnt, s);
+    build_structure(*p, points_fixed, cnt, s, pool);
     hc.mark(c->host_ms, 1);
     nl_glob = (int)cnt[p->n_poses];
     nae_glob = (int)cnt[p->n_poses + 1];
@@ -1905,7 +1933,7 @@ struct Optimizer {
       pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
       pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
       if (lba && lba_extra) pk.add(&L.extra, lba_extra, (size_t)p->n_points);
-      he = pk.flush(c);
+      he = pk.flush(c, pool);
     }
     d.delta = p->huber_delta;
     d.dsqr = huber_dsqr(p->huber_delta);

@@ -6,9 +6,11 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 #include "../../include/mcs_ba.h"
+#include "host_pool.hpp"
 
 namespace mcs {
 namespace ba {
@@ -25,6 +27,10 @@ struct HostStruct {
       ps_edges, blk_i, blk_j, pr_ptr, pr_e1, pr_e2, it_blk, it_chunk, it_slot, it_nch;
   std::vector<int32_t> pt_h;   // Hessian index of the pose of every pt_edges entry (-1: fixed)
   std::vector<int32_t> cnt_pt, cnt_pose, cursor;     // scan_edges / build_structure scratch
+  // the threaded path (HostPool): edge chunk bounds, per-chunk active counts and their
+  // compacted edges, per-chunk per-vertex counts (turned into per-chunk fill cursors)
+  std::vector<int32_t> par_begin, par_nae, par_off, par_ae, par_pt, par_pose;
+  int par_T = 0;   // chunks of the last scan_edges (0: the one-thread path ran)
   std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_pairs_host scratch
   int n_slots = 0;
   int np = 0, nl = 0;
@@ -40,8 +46,17 @@ struct HostStruct {
 // chain through memory is the loop's critical path; one pass instead of the four of the
 // first version (config C: 0.35 -> 0.11 ms on this build host with build_structure).
 // Returns false when an edge names a vertex or camera out of range.
+inline bool scan_edges_par(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
+                           HostStruct& s, std::vector<double>& cnt, HostPool& pool);
+// systems at least this large take the threaded path when a pool is given
+constexpr int kParMinEdges = 65536;
+
 inline bool scan_edges(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
-                       HostStruct& s, std::vector<double>& cnt) {
+                       HostStruct& s, std::vector<double>& cnt, HostPool* pool = nullptr,
+                       int par_min = kParMinEdges) {
+  if (pool && pool->size() > 1 && p.n_edges >= par_min)
+    return scan_edges_par(p, level, points_fixed, s, cnt, *pool);
+  s.par_T = 0;
   const int NE = p.n_edges, NP = p.n_poses, NL = p.n_points;
   s.aedge.resize(NE);
   s.cnt_pt.assign(NL, 0);
@@ -80,8 +95,11 @@ inline bool scan_edges(const mcs_ba_problem& p, const uint8_t* level, bool point
 // lists point -> edges and pose -> edges in edge order (one fill pass, counting-sort cursors;
 // the fixed poses' edges go to a dropped tail run instead of a branch) and the lower pose
 // blocks of the Schur complement.  The block pairs themselves: build_pairs_host / the device.
+inline void build_structure_fill_par(const mcs_ba_problem& p, bool points_fixed, HostStruct& s,
+                                    HostPool& pool);
+
 inline void build_structure(const mcs_ba_problem& p, bool points_fixed,
-                            const std::vector<double>& pose_cnt, HostStruct& s) {
+                            const std::vector<double>& pose_cnt, HostStruct& s, HostPool* pool = nullptr) {
   const int NP = p.n_poses, NL = p.n_points;
   const int nae = (int)s.aedge.size();
   s.pose_h.resize(NP);
@@ -131,6 +149,9 @@ inline void build_structure(const mcs_ba_problem& p, bool points_fixed,
   int32_t* const pe = s.pt_edges.data();
   int32_t* const pth = s.pt_h.data();
   int32_t* const pse = s.ps_edges.data();
+  if (pool && s.par_T > 0 && s.par_T == pool->size()) {
+    build_structure_fill_par(p, points_fixed, s, *pool);
+  } else {
   s.cursor.assign(sp, sp + np + 1);
   int32_t* const fs = s.cursor.data();
   if (!points_fixed) {
@@ -149,12 +170,166 @@ inline void build_structure(const mcs_ba_problem& p, bool points_fixed,
       pse[fs[h >= 0 ? h : np]++] = e;
     }
   }
+  }
   s.ps_edges.resize(sp[np]);
   s.ps_ptr.resize(np + 1);
   const size_t nblk = (size_t)np * (np + 1) / 2;
   s.blk_i.resize(nblk); s.blk_j.resize(nblk);
   for (int i = 0, b = 0; i < np; i++)
     for (int j = 0; j <= i; j++, b++) { s.blk_i[b] = i; s.blk_j[b] = j; }
+}
+
+// ---- the threaded path (config-E-sized systems) ----------------------------------------
+// scan_edges over T contiguous edge chunks: each chunk compacts its active edges and counts
+// them per pose and per point on its own; the chunks' lists are then concatenated in chunk
+// order (= edge order) and the counts summed.  build_structure's fill pass runs over the same
+// chunks with per-chunk cursors: chunk t's edges of a vertex go after those of chunks < t, so
+// every list is in edge order exactly as the one-thread pass leaves it (the outputs are equal,
+// tests/test_ba_structure_host.py).
+inline bool scan_edges_par(const mcs_ba_problem& p, const uint8_t* level, bool points_fixed,
+                           HostStruct& s, std::vector<double>& cnt, HostPool& pool) {
+  const int NE = p.n_edges, NP = p.n_poses, NL = p.n_points, T = pool.size();
+  s.par_T = T;
+  s.par_begin.resize(T + 1);
+  for (int t = 0; t <= T; t++) s.par_begin[t] = (int)((int64_t)NE * t / T);
+  s.par_nae.assign(T, 0);
+  s.par_off.assign(T + 1, 0);
+  s.par_ae.resize(NE);
+  s.par_pt.resize((size_t)T * NL);
+  s.par_pose.resize((size_t)T * NP);
+  std::vector<unsigned> bad(T, 0u);
+  const int32_t* const epo = p.edge_pose;
+  const int32_t* const ept = p.edge_point;
+  const int32_t* const eca = p.edge_cam;
+  const uint8_t* const pfx = p.pose_fixed;
+  const unsigned ncam = (unsigned)p.n_cams;
+  pool.run([&, epo, ept, eca, pfx, ncam, level, points_fixed, NP, NL](int t) {
+    int32_t* const cp = s.par_pt.data() + (size_t)t * NL;
+    int32_t* const cpo = s.par_pose.data() + (size_t)t * NP;
+    std::memset(cp, 0, (size_t)NL * 4);
+    std::memset(cpo, 0, (size_t)NP * 4);
+    const int e0 = s.par_begin[t], e1 = s.par_begin[t + 1];
+    int32_t* const out = s.par_ae.data() + e0;
+    unsigned b = 0;
+    int n = 0;
+    for (int e = e0; e < e1; e++) {
+      const int pi = epo[e], li = ept[e], ci = eca[e];
+      const unsigned bb = ((unsigned)pi >= (unsigned)NP) | ((unsigned)li >= (unsigned)NL) |
+                          ((unsigned)ci >= ncam);
+      b |= bb;
+      if (bb) continue;
+      const int act = !(level && level[e]) && !(points_fixed && pfx[pi]);
+      out[n] = e;
+      n += act;
+      cpo[pi] += act;
+      cp[li] += act;
+    }
+    s.par_nae[t] = n;
+    bad[t] = b;
+  });
+  for (int t = 0; t < T; t++)
+    if (bad[t]) return false;
+  for (int t = 0; t < T; t++) s.par_off[t + 1] = s.par_off[t] + s.par_nae[t];
+  const int nae = s.par_off[T];
+  s.aedge.resize(nae);
+  s.cnt_pt.resize(NL);
+  s.cnt_pose.resize(NP);
+  std::vector<int> nl_part(T, 0);
+  pool.run([&](int t) {
+    std::memcpy(s.aedge.data() + s.par_off[t], s.par_ae.data() + s.par_begin[t], (size_t)s.par_nae[t] * 4);
+    // per-vertex totals over the chunks, vertices split over the threads
+    const int v0 = (int)((int64_t)NL * t / T), v1 = (int)((int64_t)NL * (t + 1) / T);
+    int nl = 0;
+    for (int v = v0; v < v1; v++) {
+      int c = 0;
+      for (int u = 0; u < T; u++) c += s.par_pt[(size_t)u * NL + v];
+      s.cnt_pt[v] = c;
+      nl += c > 0;
+    }
+    nl_part[t] = nl;
+  });
+  for (int i = 0; i < NP; i++) {
+    int c = 0;
+    for (int u = 0; u < T; u++) c += s.par_pose[(size_t)u * NP + i];
+    s.cnt_pose[i] = c;
+  }
+  cnt.assign((size_t)NP + 2, 0.0);
+  for (int i = 0; i < NP; i++) cnt[i] = s.cnt_pose[i];
+  int nl = 0;
+  if (!points_fixed)
+    for (int t = 0; t < T; t++) nl += nl_part[t];
+  cnt[NP] = nl;
+  cnt[NP + 1] = nae;
+  return true;
+}
+
+// build_structure's fill pass over scan_edges_par's chunks (pose_h, point_h, pt_ptr and ps_ptr
+// are already set): per-chunk cursors from the per-chunk counts, then each chunk writes its
+// active edges into the point and pose lists
+inline void build_structure_fill_par(const mcs_ba_problem& p, bool points_fixed, HostStruct& s,
+                                     HostPool& pool) {
+  const int NP = p.n_poses, NL = p.n_points, T = s.par_T;
+  const int np = s.np;
+  const int32_t* const poh = s.pose_h.data();
+  const int32_t* const ph = s.point_h.data();
+  const int32_t* const pp = s.pt_ptr.data();
+  const int32_t* const sp = s.ps_ptr.data();
+  // pose cursors per (chunk, pose vertex): active poses fill their run, fixed poses the dropped
+  // tail run np
+  {
+    int tail = sp[np];
+    for (int i = 0; i < NP; i++) {
+      int base = poh[i] >= 0 ? sp[poh[i]] : tail;
+      for (int u = 0; u < T; u++) {
+        int32_t& c = s.par_pose[(size_t)u * NP + i];
+        const int n = c;
+        c = base;
+        base += n;
+      }
+      if (poh[i] < 0) tail = base;
+    }
+  }
+  int32_t* const pe = s.pt_edges.data();
+  int32_t* const pth = s.pt_h.data();
+  int32_t* const pse = s.ps_edges.data();
+  pool.run([&](int t) {
+    if (!points_fixed) {   // point cursors per (chunk, point vertex), vertices split over threads
+      const int v0 = (int)((int64_t)NL * t / T), v1 = (int)((int64_t)NL * (t + 1) / T);
+      for (int v = v0; v < v1; v++) {
+        if (ph[v] < 0) continue;
+        int base = pp[ph[v]];
+        for (int u = 0; u < T; u++) {
+          int32_t& c = s.par_pt[(size_t)u * NL + v];
+          const int n = c;
+          c = base;
+          base += n;
+        }
+      }
+    }
+  });
+  pool.run([&](int t) {
+    int32_t* const cp = s.par_pt.data() + (size_t)t * NL;
+    int32_t* const cpo = s.par_pose.data() + (size_t)t * NP;
+    const int32_t* const ae = s.aedge.data() + s.par_off[t];
+    const int n = s.par_nae[t];
+    if (!points_fixed) {
+      for (int k = 0; k < n; k++) {
+        const int e = ae[k];
+        const int pv = p.edge_pose[e];
+        const int r = cp[p.edge_point[e]]++;
+        pe[r] = e;
+        pth[r] = poh[pv];
+        pse[cpo[pv]++] = e;
+      }
+    } else {
+      for (int k = 0; k < n; k++) {
+        const int e = ae[k];
+        const int pv = p.edge_pose[e];
+        pse[cpo[pv]++] = e;
+      }
+    }
+  });
+  (void)np;
 }
 
 // The edge pairs of every lower block in (point, e1, e2) order and the k_schur work items, on

@@ -1,7 +1,10 @@
 // Host structure of one BA call (ba_structure.hpp: scan_edges + build_structure), dumped as
 // text for tests/test_ba_structure_host.py.  Input (stdin): n_poses n_points n_edges n_cams
 // points_fixed has_level, then pose_fixed[n_poses], then per edge: pose point cam level.
+// argv[1] (optional): host threads; > 1 runs the threaded path (scan_edges_par + the chunked
+// fill) whatever the size, which must give the same output as the one-thread path.
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "../../multicol-slam-annotation_amd/csrc/ba_structure.hpp"
 
@@ -11,7 +14,9 @@ static void dump(const char* name, const std::vector<int32_t>& v) {
   std::printf("\n");
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
+  mcs::HostPool pool(threads);
   int np, npt, ne, nc, pf, hl;
   if (std::scanf("%d %d %d %d %d %d", &np, &npt, &ne, &nc, &pf, &hl) != 6) return 2;
   std::vector<uint8_t> fixed(np), level(ne);
@@ -29,8 +34,8 @@ int main() {
   std::vector<double> cnt;
   // twice on one HostStruct: capacities are reused across calls, the result must not depend on it
   for (int rep = 0; rep < 2; rep++) {
-    if (!mcs::ba::scan_edges(p, hl ? level.data() : nullptr, pf != 0, s, cnt)) { std::printf("bad\n"); return 0; }
-    mcs::ba::build_structure(p, pf != 0, cnt, s);
+    if (!mcs::ba::scan_edges(p, hl ? level.data() : nullptr, pf != 0, s, cnt, &pool, 1)) { std::printf("bad\n"); return 0; }
+    mcs::ba::build_structure(p, pf != 0, cnt, s, &pool);
   }
   std::printf("np %d nl %d\n", s.np, s.nl);
   std::vector<int32_t> ci(cnt.size());

@@ -18,16 +18,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def exe(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("bs") / "structure_dump")
     subprocess.check_call(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "tests", "cpp", "structure_dump.cpp"),
-                           "-o", out])
+                           "-pthread", "-o", out])
     return out
 
 
-def _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, ncam=3):
+def _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, ncam=3, threads=1):
     lines = ["%d %d %d %d %d %d" % (npose, npt, len(ep), ncam, int(points_fixed), int(level is not None)),
              " ".join(str(int(x)) for x in fixed)]
     lv = level if level is not None else np.zeros(len(ep), np.uint8)
     lines += ["%d %d %d %d" % (a, b, c, d) for a, b, c, d in zip(ep, el, ec, lv)]
-    out = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True,
+    out = subprocess.run([exe, str(threads)], input="\n".join(lines) + "\n", capture_output=True, text=True,
                          timeout=60, check=True).stdout.split("\n")
     if out[0].strip() == "bad":
         return None
@@ -78,8 +78,9 @@ def _restated(npose, npt, ep, el, fixed, level, points_fixed):
                 blk_i=blk_i, blk_j=blk_j)
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
 @pytest.mark.parametrize("seed", range(8))
-def test_host_structure_matches_restatement(exe, seed):
+def test_host_structure_matches_restatement(exe, seed, threads):
     rng = np.random.default_rng(seed)
     npose, npt = int(rng.integers(1, 12)), int(rng.integers(1, 60))
     ne = int(rng.integers(0, 300))
@@ -92,7 +93,7 @@ def test_host_structure_matches_restatement(exe, seed):
     fixed = (rng.random(npose) < 0.3).astype(np.uint8)
     level = (rng.random(ne) < 0.2).astype(np.uint8) if seed % 3 else None
     points_fixed = seed in (5, 7)
-    got = _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed)
+    got = _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, threads=threads)
     want = _restated(npose, npt, ep.tolist(), el.tolist(), fixed.tolist(),
                      None if level is None else level.tolist(), points_fixed)
     for k, v in want.items():
@@ -103,5 +104,21 @@ def test_host_structure_rejects_out_of_range(exe):
     ep, el, ec = np.array([0, 1, 2]), np.array([0, 1, 0]), np.array([0, 0, 0])
     fixed = np.zeros(2, np.uint8)
     assert _run(exe, 2, 2, ep, el, ec, fixed, None, False) is None            # pose 2 of 2
+    assert _run(exe, 2, 2, ep, el, ec, fixed, None, False, threads=2) is None
     assert _run(exe, 3, 2, ep, np.array([0, 1, 2]), ec, np.zeros(3, np.uint8), None, False) is None
     assert _run(exe, 3, 2, ep, el, np.array([0, 3, 0]), np.zeros(3, np.uint8), None, False) is None
+
+
+@pytest.mark.parametrize("points_fixed", [False, True])
+def test_host_structure_threaded_equals_one_thread(exe, points_fixed):
+    """The threaded path (HostPool chunks) on a larger graph: identical output to one thread."""
+    rng = np.random.default_rng(11)
+    npose, npt, ne = 40, 3000, 20000
+    el = np.sort(rng.integers(0, npt, ne))
+    ep = rng.integers(0, npose, ne)
+    ec = rng.integers(0, 3, ne)
+    fixed = (rng.random(npose) < 0.2).astype(np.uint8)
+    level = (rng.random(ne) < 0.1).astype(np.uint8)
+    one = _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed)
+    for t in (2, 5, 8):
+        assert _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, threads=t) == one

@@ -103,3 +103,17 @@ def test_gpu_config_e_sharded_lockstep(gpu, eproblem, egpu, world, ordered):
     cnt = np.bincount(eproblem["edge_point"], minlength=len(eproblem["points"]))
     wc = cnt >= 3
     assert np.abs(pts[wc] - full["points"][wc]).max() < 1e-5
+
+
+@pytest.mark.gpu
+def test_gpu_config_e_host_threads_identical(gpu, eproblem, egpu, monkeypatch):
+    """Config E takes the threaded host path (structure build + staging copy over a HostPool,
+    ba_structure.hpp scan_edges_par); with MCS_HOST_THREADS=1 it takes the one-thread path.
+    Both must give bit-identical results (the structure lists are equal by construction)."""
+    from mcs_amd import ba
+    monkeypatch.setenv("MCS_HOST_THREADS", "1")
+    one = ba.Solver().global_ba(eproblem, trace=20)
+    assert one["report"].iterations == egpu["report"].iterations
+    assert np.array_equal(one["poses"], egpu["poses"])
+    assert np.array_equal(one["points"], egpu["points"])
+    assert np.array_equal(one["trace"], egpu["trace"])
