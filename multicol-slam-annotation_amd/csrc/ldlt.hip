@@ -717,7 +717,8 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
 // payload stored write-through (sc1: 16-B buffer stores from LDS, 8-B stores from registers),
 // every storing wave drains vmcnt, a workgroup barrier, ONE lane stores the flag / counter
 // (relaxed, agent scope); the consumer's lane 0 polls relaxed with s_sleep, then ONE agent-scope
-// acquire + vmcnt drain before the workgroup barrier, then plain loads.  Flag words are zeroed
+// acquire + vmcnt drain before the workgroup barrier, then plain loads (MCS_PIPE_SC1 builds read
+// with sc1 loads instead, see kSc1Consume below).  Flag words are zeroed
 // by a memset on the stream before every launch.
 namespace {
 
@@ -749,6 +750,40 @@ __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
   }
 }
 
+// Consumer side of the hand-offs.  Every byte k_pipe hands off is stored sc1 (write-through,
+// 16-B tiles / 8-B words) by a workgroup whose every storing wave drained vmcnt before ONE lane's
+// sc1 flag store, the waiting lane polls that flag with sc1 loads and the other waves join it at
+// a barrier, one workgroup per CU (LDS), hipMalloc memory: MI355X_MICROARCH.md's hand-off table,
+// first row.  So the consumer reads the handed-off bytes with sc1 loads (16-B buffer loads for
+// tiles, 8-B global loads for words) and skips the agent acquire after each wait (an L2
+// invalidate on the diagonal chain twice per step).  Built with MCS_PIPE_SC1 (A/B variant until
+// it is measured on the device); the default keeps the acquire form.
+#ifdef MCS_PIPE_SC1
+constexpr bool kSc1Consume = true;
+#else
+constexpr bool kSc1Consume = false;
+#endif
+__device__ __forceinline__ double ld_h(const double* p) {
+  if (!kSc1Consume) return *p;
+  return __longlong_as_double((long long)__hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void fetch_tile_h(d2 (&v)[8], const double* g) {
+  if (!kSc1Consume) { fetch_tile(v, g); return; }
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(g), 0, TB * TB * 8, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    v[i] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (threadIdx.x + 256 * i), 0, 16));
+}
+__device__ __forceinline__ void load_acc_h(double (&a)[4][4], const double* Aij) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = l & 15, k4 = l >> 4;
+  const int col = 16 * w + r16;
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) a[q][r] = ld_h(&Aij[(16 * q + k4 + 4 * r) * TB + col]);
+}
+
 // Lane 0 waits until *w_i >= v_i for every non-null word (bounded in time), then acquires; all threads get the
 // outcome (false: timed out here or elsewhere).
 __device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const unsigned* w1, unsigned v1,
@@ -763,7 +798,7 @@ __device__ __forceinline__ bool wg_wait(const unsigned* w0, unsigned v0, const u
       if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { pl_store(err, 1u); ok = 0; break; }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (ok) {
+    if (ok && !kSc1Consume) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -854,16 +889,6 @@ __device__ __forceinline__ void trsm_to_lds(double* sX, double* sY, const double
   __syncthreads();
 }
 
-// A_kk's entries in the accumulator layout (rows 16q + k4 + 4r, column 16w + r16)
-__device__ __forceinline__ void load_acc(double (&a)[4][4], const double* Aij) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, r16 = l & 15, k4 = l >> 4;
-  const int col = 16 * w + r16;
-#pragma unroll
-  for (int q = 0; q < 4; q++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) a[q][r] = Aij[(16 * q + k4 + 4 * r) * TB + col];
-}
-
 // the 10 lower and 6 strict-upper 16x16 blocks of a diagonal tile
 __constant__ int kLowBi[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
 __constant__ int kLowBj[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
@@ -902,7 +927,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     // A_kk -= L_{k,k-1} W_{k,k-1}^T on the 10 lower 16x16 blocks only (the upper ones are
     // not read by the factorisation), 3 / 3 / 2 / 2 blocks per wave; each block is the same
     // MFMA chain (k ascending) as the full gemm_xyt, so the bits are the full product's
-    double bv = g.b[k * TB + (t >> 2)];
+    double bv = ld_h(&g.b[k * TB + (t >> 2)]);
     {
       const double* Akk = g.A + toff(k, k, T);
       const int nb = w < 2 ? 3 : 2, b0 = w < 2 ? 3 * w : 6 + 2 * (w - 2);
@@ -912,7 +937,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
         if (q < nb) {
           const int bi = kLowBi[b0 + q], bj = kLowBj[b0 + q];
 #pragma unroll
-          for (int r = 0; r < 4; r++) a[q][r] = Akk[(16 * bi + k4 + 4 * r) * TB + 16 * bj + r16];
+          for (int r = 0; r < 4; r++) a[q][r] = ld_h(&Akk[(16 * bi + k4 + 4 * r) * TB + 16 * bj + r16]);
         }
       }
       if (k >= 1) bv -= gemv_row(sX, su);
@@ -970,7 +995,7 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
       DSTAMP(k, 5);
       {
         d2 v[8];
-        fetch_tile(v, g.A + toff(k + 1, k, T));
+        fetch_tile_h(v, g.A + toff(k + 1, k, T));
         put_tile(sX, v);
       }
       if (t < TB) sv[t] = sK[t * LS + t];
@@ -1000,9 +1025,9 @@ __device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_o
   TSTAMP(tk, 1);
   {
     d2 vx[8], vi[8];
-    fetch_tile(vx, g.A + toff(i, k, T));
-    fetch_tile(vi, g.Linv + (size_t)k * TB * TB);
-    if (t < TB) sv[t] = g.du[(size_t)k * 128 + t];
+    fetch_tile_h(vx, g.A + toff(i, k, T));
+    fetch_tile_h(vi, g.Linv + (size_t)k * TB * TB);
+    if (t < TB) sv[t] = ld_h(&g.du[(size_t)k * 128 + t]);
     put_tile(sX, vx);
     put_tile(sI, vi);
   }
@@ -1030,12 +1055,12 @@ __device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, 
   double bv = 0.0;
   {
     d2 vx[8], vy[8];
-    fetch_tile(vx, g.L + toff(i, k, T));
-    fetch_tile(vy, g.W + toff(j, k, T));
-    load_acc(a, g.A + toff(i, j, T));
+    fetch_tile_h(vx, g.L + toff(i, k, T));
+    fetch_tile_h(vy, g.W + toff(j, k, T));
+    load_acc_h(a, g.A + toff(i, j, T));
     if (i == j) {
-      bv = g.b[i * TB + (t >> 2)];
-      if (t < TB) su[t] = g.du[(size_t)k * 128 + TB + t];
+      bv = ld_h(&g.b[i * TB + (t >> 2)]);
+      if (t < TB) su[t] = ld_h(&g.du[(size_t)k * 128 + TB + t]);
     }
     put_tile(sX, vx);
     put_tile(sY, vy);
