@@ -31,6 +31,9 @@ struct HostStruct {
   // compacted edges, per-chunk per-vertex counts (turned into per-chunk fill cursors)
   std::vector<int32_t> par_begin, par_nae, par_off, par_ae, par_pt, par_pose;
   int par_T = 0;   // chunks of the last scan_edges (0: the one-thread path ran)
+  // the edges come in non-decreasing point order (LocalBA and GlobalBA build them so): the
+  // point lists are then the active-edge list itself, and the fill pass needs no point cursors
+  bool pt_sorted = false;
   std::vector<int32_t> tmp_e, tmp_g, tmp_p, tmp_f;   // build_pairs_host scratch
   int n_slots = 0;
   int np = 0, nl = 0;
@@ -64,13 +67,15 @@ inline bool scan_edges(const mcs_ba_problem& p, const uint8_t* level, bool point
   int32_t* const ae = s.aedge.data();
   int32_t* const cp = s.cnt_pt.data();
   int32_t* const cpo = s.cnt_pose.data();
-  unsigned bad = 0;
-  int nae = 0;
+  unsigned bad = 0, uns = 0;
+  int nae = 0, prev = 0;
   for (int e = 0; e < NE; e++) {
     const int pi = p.edge_pose[e], li = p.edge_point[e], ci = p.edge_cam[e];
     const unsigned b = ((unsigned)pi >= (unsigned)NP) | ((unsigned)li >= (unsigned)NL) |
                        ((unsigned)ci >= (unsigned)p.n_cams);
     bad |= b;
+    uns |= (unsigned)(li < prev);
+    prev = li;
     if (b) continue;
     const int act = !(level && level[e]) && !(points_fixed && p.pose_fixed[pi]);
     ae[nae] = e;
@@ -79,6 +84,7 @@ inline bool scan_edges(const mcs_ba_problem& p, const uint8_t* level, bool point
     cp[li] += act;
   }
   if (bad) return false;
+  s.pt_sorted = uns == 0;
   s.aedge.resize(nae);
   cnt.assign((size_t)NP + 2, 0.0);
   for (int i = 0; i < NP; i++) cnt[i] = cpo[i];
@@ -154,7 +160,17 @@ inline void build_structure(const mcs_ba_problem& p, bool points_fixed,
   } else {
   s.cursor.assign(sp, sp + np + 1);
   int32_t* const fs = s.cursor.data();
-  if (!points_fixed) {
+  if (!points_fixed && s.pt_sorted) {
+    // point order = edge order: pt_edges is the active-edge list (no counter chain through
+    // the point cursors, which consecutive edges of one point would serialise on)
+    if (nae) std::memcpy(pe, ae, (size_t)nae * 4);
+    for (int k = 0; k < nae; k++) {
+      const int e = ae[k];
+      const int h = poh[p.edge_pose[e]];
+      pth[k] = h;
+      pse[fs[h >= 0 ? h : np]++] = e;
+    }
+  } else if (!points_fixed) {
     for (int k = 0; k < nae; k++) {
       const int e = ae[k];
       const int h = poh[p.edge_pose[e]];
@@ -210,13 +226,15 @@ inline bool scan_edges_par(const mcs_ba_problem& p, const uint8_t* level, bool p
     std::memset(cpo, 0, (size_t)NP * 4);
     const int e0 = s.par_begin[t], e1 = s.par_begin[t + 1];
     int32_t* const out = s.par_ae.data() + e0;
-    unsigned b = 0;
-    int n = 0;
+    unsigned b = 0, uns = 0;
+    int n = 0, prev = e0 > 0 ? ept[e0 - 1] : 0;
     for (int e = e0; e < e1; e++) {
       const int pi = epo[e], li = ept[e], ci = eca[e];
       const unsigned bb = ((unsigned)pi >= (unsigned)NP) | ((unsigned)li >= (unsigned)NL) |
                           ((unsigned)ci >= ncam);
       b |= bb;
+      uns |= (unsigned)(li < prev);
+      prev = li;
       if (bb) continue;
       const int act = !(level && level[e]) && !(points_fixed && pfx[pi]);
       out[n] = e;
@@ -225,10 +243,14 @@ inline bool scan_edges_par(const mcs_ba_problem& p, const uint8_t* level, bool p
       cp[li] += act;
     }
     s.par_nae[t] = n;
-    bad[t] = b;
+    bad[t] = b | (uns << 1);
   });
-  for (int t = 0; t < T; t++)
-    if (bad[t]) return false;
+  unsigned uns_all = 0;
+  for (int t = 0; t < T; t++) {
+    if (bad[t] & 1u) return false;
+    uns_all |= bad[t];
+  }
+  s.pt_sorted = uns_all == 0;
   for (int t = 0; t < T; t++) s.par_off[t + 1] = s.par_off[t] + s.par_nae[t];
   const int nae = s.par_off[T];
   s.aedge.resize(nae);
@@ -292,7 +314,8 @@ inline void build_structure_fill_par(const mcs_ba_problem& p, bool points_fixed,
   int32_t* const pe = s.pt_edges.data();
   int32_t* const pth = s.pt_h.data();
   int32_t* const pse = s.ps_edges.data();
-  pool.run([&](int t) {
+  const bool sorted = s.pt_sorted;
+  if (!sorted) pool.run([&](int t) {
     if (!points_fixed) {   // point cursors per (chunk, point vertex), vertices split over threads
       const int v0 = (int)((int64_t)NL * t / T), v1 = (int)((int64_t)NL * (t + 1) / T);
       for (int v = v0; v < v1; v++) {
@@ -312,7 +335,17 @@ inline void build_structure_fill_par(const mcs_ba_problem& p, bool points_fixed,
     int32_t* const cpo = s.par_pose.data() + (size_t)t * NP;
     const int32_t* const ae = s.aedge.data() + s.par_off[t];
     const int n = s.par_nae[t];
-    if (!points_fixed) {
+    if (!points_fixed && sorted) {
+      int32_t* const pek = pe + s.par_off[t];
+      int32_t* const phk = pth + s.par_off[t];
+      if (n) std::memcpy(pek, ae, (size_t)n * 4);
+      for (int k = 0; k < n; k++) {
+        const int e = ae[k];
+        const int pv = p.edge_pose[e];
+        phk[k] = poh[pv];
+        pse[cpo[pv]++] = e;
+      }
+    } else if (!points_fixed) {
       for (int k = 0; k < n; k++) {
         const int e = ae[k];
         const int pv = p.edge_pose[e];

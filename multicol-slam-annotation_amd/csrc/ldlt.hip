@@ -717,9 +717,9 @@ __global__ __launch_bounds__(kBwdNT) void k_backward(const double* __restrict__ 
 // payload stored write-through (sc1: 16-B buffer stores from LDS, 8-B stores from registers),
 // every storing wave drains vmcnt, a workgroup barrier, ONE lane stores the flag / counter
 // (relaxed, agent scope); the consumer's lane 0 polls relaxed with s_sleep, then ONE agent-scope
-// acquire + vmcnt drain before the workgroup barrier, then plain loads (MCS_PIPE_SC1 builds read
-// with sc1 loads instead, see kSc1Consume below).  Flag words are zeroed
-// by a memset on the stream before every launch.
+// acquire + vmcnt drain before the workgroup barrier, then plain loads -- the MCS_PIPE_ACQUIRE
+// build; by default the consumers read with sc1 loads instead (kSc1Consume below).  Flag words
+// are zeroed by a memset on the stream before every launch.
 namespace {
 
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -756,12 +756,13 @@ __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
 // a barrier, one workgroup per CU (LDS), hipMalloc memory: MI355X_MICROARCH.md's hand-off table,
 // first row.  So the consumer reads the handed-off bytes with sc1 loads (16-B buffer loads for
 // tiles, 8-B global loads for words) and skips the agent acquire after each wait (an L2
-// invalidate on the diagonal chain twice per step).  Built with MCS_PIPE_SC1 (A/B variant until
-// it is measured on the device); the default keeps the acquire form.
-#ifdef MCS_PIPE_SC1
-constexpr bool kSc1Consume = true;
-#else
+// invalidate on the diagonal chain twice per step).  Config E (n = 1194, 19 tile steps): solve
+// 0.395 -> 0.390 ms per trial, parity tests green (tools/gpu/host_threads_ab.sh, round 5).
+// MCS_PIPE_ACQUIRE builds the acquire form.
+#ifdef MCS_PIPE_ACQUIRE
 constexpr bool kSc1Consume = false;
+#else
+constexpr bool kSc1Consume = true;
 #endif
 __device__ __forceinline__ double ld_h(const double* p) {
   if (!kSc1Consume) return *p;

@@ -109,16 +109,23 @@ def test_host_structure_rejects_out_of_range(exe):
     assert _run(exe, 3, 2, ep, el, np.array([0, 3, 0]), np.zeros(3, np.uint8), None, False) is None
 
 
+@pytest.mark.parametrize("sorted_points", [True, False])
 @pytest.mark.parametrize("points_fixed", [False, True])
-def test_host_structure_threaded_equals_one_thread(exe, points_fixed):
-    """The threaded path (HostPool chunks) on a larger graph: identical output to one thread."""
+def test_host_structure_threaded_equals_one_thread(exe, points_fixed, sorted_points):
+    """The threaded path (HostPool chunks) on a larger graph: identical output to one thread,
+    with the edges in point order (the point lists are the edge list) and in random order."""
     rng = np.random.default_rng(11)
     npose, npt, ne = 40, 3000, 20000
-    el = np.sort(rng.integers(0, npt, ne))
+    el = rng.integers(0, npt, ne)
+    if sorted_points:
+        el = np.sort(el)
     ep = rng.integers(0, npose, ne)
     ec = rng.integers(0, 3, ne)
     fixed = (rng.random(npose) < 0.2).astype(np.uint8)
     level = (rng.random(ne) < 0.1).astype(np.uint8)
     one = _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed)
+    want = _restated(npose, npt, ep.tolist(), el.tolist(), fixed.tolist(), level.tolist(), points_fixed)
+    for k, v in want.items():
+        assert one[k] == v, k
     for t in (2, 5, 8):
         assert _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, threads=t) == one
