@@ -1626,6 +1626,20 @@ struct mcs_ba_ctx {
     }
     return stage;
   }
+  // second staging buffer (threaded calls): the structure arrays, filled while the problem
+  // arrays' copy out of `stage` may still be in flight
+  uint8_t* stage2 = nullptr;
+  size_t stage2_cap = 0;
+  uint8_t* stage2_get(size_t bytes) {
+    if (bytes > stage2_cap) {
+      if (stage2) (void)hipHostFree(stage2);
+      stage2 = nullptr; stage2_cap = 0;
+      const size_t cap = std::max(bytes, (size_t)1 << 20);
+      if (hipHostMalloc((void**)&stage2, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+      stage2_cap = cap;
+    }
+    return stage2;
+  }
   // optional stage timing (mcs_ba_enable_timing): HIP events on st around each stage,
   // accumulated after the per-trial synchronisation the LM control needs anyway
   bool timing = false;
@@ -1703,12 +1717,16 @@ struct Packer {
   }
   template <typename D, typename T>
   void add(D** dst, const std::vector<T>& v) { add(dst, v.data(), v.size()); }
-  hipError_t flush(mcs_ba_ctx* c, mcs::HostPool* pool = nullptr) {
+  // second: into stage2, behind a first flush of this call (whose spin_sync already found the
+  // previous call's copies done; the first flush's own copy may still be running)
+  hipError_t flush(mcs_ba_ctx* c, mcs::HostPool* pool = nullptr, bool second = false) {
     uint8_t* d = (uint8_t*)c->alloc(std::max<size_t>(total, 256));
     if (!d) return hipErrorOutOfMemory;
-    hipError_t e = spin_sync(c->st);   // the staging buffer is free again
-    if (e != hipSuccess) return e;
-    uint8_t* h = c->stage_get(std::max<size_t>(total, 256));
+    if (!second) {
+      const hipError_t e = spin_sync(c->st);   // the staging buffer is free again
+      if (e != hipSuccess) return e;
+    }
+    uint8_t* h = second ? c->stage2_get(std::max<size_t>(total, 256)) : c->stage_get(std::max<size_t>(total, 256));
     if (!h) return hipErrorOutOfMemory;
     for (const Item& it : items) *it.dst = d + it.off;
     if (pool && total >= ((size_t)4 << 20)) {
@@ -1844,6 +1862,23 @@ struct Optimizer {
     return MCS_OK;
   }
 
+  // the problem's own arrays (and the trial backups' space) into a packed upload
+  void add_problem(Packer& pk, const double* poses, const double* points, double** poses_bk,
+                   double** points_bk) {
+    pk.add(&d.mc, p->mc, 6 * (size_t)p->n_cams);
+    pk.add(&d.cam, p->cam, 17 * (size_t)p->n_cams);
+    pk.add(&d.e_pose, p->edge_pose, (size_t)NE);
+    pk.add(&d.e_point, p->edge_point, (size_t)NE);
+    pk.add(&d.e_cam, p->edge_cam, (size_t)NE);
+    pk.add(&d.e_meas, p->edge_meas, 2 * (size_t)NE);
+    pk.add(&d.e_info, p->edge_info, (size_t)NE);
+    pk.add(&d_poses, poses, 6 * (size_t)p->n_poses);
+    pk.add(&d_points, points, 3 * (size_t)p->n_points);
+    // the trial backups are written by every trial's push before anything reads them: space only
+    pk.add(poses_bk, static_cast<const double*>(nullptr), 6 * (size_t)p->n_poses);
+    pk.add(points_bk, static_cast<const double*>(nullptr), 3 * (size_t)p->n_points);
+  }
+
   int setup(const double* poses, const double* points, const uint8_t* edge_level,
             const mcs_ba_shard* shard_in) {
     if (p->n_poses < 0 || p->n_points < 0 || p->n_edges < 0 || p->n_cams < 1) return MCS_ERR_ARG;
@@ -1874,6 +1909,15 @@ struct Optimizer {
     if (!sharded) {
       sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
       if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
+    }
+    // ---- threaded (config-E-sized) calls: the problem arrays go up now, their copy overlapping
+    // the structure build; the structure arrays follow from the second staging buffer
+    NE = p->n_edges;
+    double *d_poses_bk = nullptr, *d_points_bk = nullptr;
+    if (pool) {
+      Packer pk;
+      add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
+      if ((he = pk.flush(c, pool)) != hipSuccess) MCS_HIP_CHECK(he);
     }
     // ---- global pose activity (+ active point / edge counts)
     int rc;
@@ -1908,22 +1952,9 @@ struct Optimizer {
       if ((rc = allreduce_host(&wd, 1, MCS_REDUCE_MAX, X.sc))) return rc;
       xs_count = (size_t)ldlt::TB * T + ldlt::band_tiles((int)wd + 1, T) * ldlt::TB * ldlt::TB;
     }
-    NE = p->n_edges;
-    double *d_poses_bk = nullptr, *d_points_bk = nullptr;
     {
       Packer pk;
-      pk.add(&d.mc, p->mc, 6 * (size_t)p->n_cams);
-      pk.add(&d.cam, p->cam, 17 * (size_t)p->n_cams);
-      pk.add(&d.e_pose, p->edge_pose, (size_t)NE);
-      pk.add(&d.e_point, p->edge_point, (size_t)NE);
-      pk.add(&d.e_cam, p->edge_cam, (size_t)NE);
-      pk.add(&d.e_meas, p->edge_meas, 2 * (size_t)NE);
-      pk.add(&d.e_info, p->edge_info, (size_t)NE);
-      pk.add(&d_poses, poses, 6 * (size_t)p->n_poses);
-      pk.add(&d_points, points, 3 * (size_t)p->n_points);
-      // the trial backups are written by every trial's push before anything reads them: space only
-      pk.add(&d_poses_bk, static_cast<const double*>(nullptr), 6 * (size_t)p->n_poses);
-      pk.add(&d_points_bk, static_cast<const double*>(nullptr), 3 * (size_t)p->n_points);
+      if (!pool) add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
       // every edge active (LocalBA round 1, GlobalBA): no list, the kernels index edges directly
       if ((int)s.aedge.size() != NE) pk.add(&d.aedge, s.aedge);
       else d.aedge = nullptr;
@@ -1933,7 +1964,7 @@ struct Optimizer {
       pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
       pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
       if (lba && lba_extra) pk.add(&L.extra, lba_extra, (size_t)p->n_points);
-      he = pk.flush(c, pool);
+      he = pk.flush(c, pool, pool != nullptr);
     }
     d.delta = p->huber_delta;
     d.dsqr = huber_dsqr(p->huber_delta);
@@ -2698,6 +2729,7 @@ void mcs_ba_destroy(mcs_ba_ctx* c) {
   if (c->lsig) (void)hipHostFree(c->lsig);
   if (c->pinned_ctl) (void)hipHostFree(c->pinned_ctl);
   if (c->stage) (void)hipHostFree(c->stage);
+  if (c->stage2) (void)hipHostFree(c->stage2);
   if (c->st) (void)hipStreamDestroy(c->st);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   delete c;
