@@ -1910,11 +1910,14 @@ struct Optimizer {
       sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
       if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
     }
-    // ---- threaded (config-E-sized) calls: the problem arrays go up now, their copy overlapping
-    // the structure build; the structure arrays follow from the second staging buffer
+    // ---- threaded (config-E-sized) calls with MCS_SPLIT_UPLOAD=1: the problem arrays go up
+    // now, their copy overlapping the structure build; the structure arrays follow from the
+    // second staging buffer (written, not yet measured on the device: off by default)
     NE = p->n_edges;
     double *d_poses_bk = nullptr, *d_points_bk = nullptr;
-    if (pool) {
+    static const bool split_env = [] { const char* e = std::getenv("MCS_SPLIT_UPLOAD"); return e && e[0] == '1'; }();
+    const bool split = pool && split_env;
+    if (split) {
       Packer pk;
       add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
       if ((he = pk.flush(c, pool)) != hipSuccess) MCS_HIP_CHECK(he);
@@ -1954,7 +1957,7 @@ struct Optimizer {
     }
     {
       Packer pk;
-      if (!pool) add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
+      if (!split) add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
       // every edge active (LocalBA round 1, GlobalBA): no list, the kernels index edges directly
       if ((int)s.aedge.size() != NE) pk.add(&d.aedge, s.aedge);
       else d.aedge = nullptr;
@@ -1964,7 +1967,7 @@ struct Optimizer {
       pk.add(&d.ps_ptr, s.ps_ptr); pk.add(&d.ps_edges, s.ps_edges);
       pk.add(&d.blk_i, s.blk_i); pk.add(&d.blk_j, s.blk_j);
       if (lba && lba_extra) pk.add(&L.extra, lba_extra, (size_t)p->n_points);
-      he = pk.flush(c, pool, pool != nullptr);
+      he = pk.flush(c, pool, split);
     }
     d.delta = p->huber_delta;
     d.dsqr = huber_dsqr(p->huber_delta);
