@@ -129,3 +129,12 @@ def test_host_structure_threaded_equals_one_thread(exe, points_fixed, sorted_poi
         assert one[k] == v, k
     for t in (2, 5, 8):
         assert _run(exe, npose, npt, ep, el, ec, fixed, level, points_fixed, threads=t) == one
+
+
+def test_host_pool_runs_every_index_once(tmp_path):
+    """csrc/host_pool.hpp: each run(f) calls f(0..n-1) once and waits for all of them."""
+    out = str(tmp_path / "host_pool_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread",
+                           os.path.join(ROOT, "tests", "cpp", "host_pool_check.cpp"), "-o", out])
+    r = subprocess.run([out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
