@@ -11,6 +11,8 @@ pixel noise sigma = 0.5*1.2^octave, a few outliers, perturbed initial poses / po
 """
 import ctypes
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -57,19 +59,24 @@ _PROBLEM_FIELDS = (("poses", np.float64), ("pose_fixed", np.uint8), ("points", n
                    ("edge_info", np.float64))
 
 
-_STRUCT_CACHE = []   # (arrays, huber_delta, BAProblem), most recent last, a few entries
+_STRUCT_CACHE = []   # (weakrefs to the arrays, huber_delta, BAProblem), most recent last
+_STRUCT_CACHE_LOCK = threading.Lock()
+_STRUCT_CACHE_SIZE = 2
 
 
 def as_struct(pr):
     """numpy problem dict -> BAProblem (keeps references alive in the dict).  A dict whose
     arrays are the same objects as at an earlier call (values may have changed in place) gets
     that call's struct back: the addresses are the same, and reading ten array addresses cost
-    ~30 us of a ~2.3 ms LocalBA call."""
+    ~30 us of a ~2.3 ms LocalBA call.  The cache holds weak references only, so a problem the
+    caller drops is freed (a dead reference never matches: a new array at a reused address is
+    a cache miss), and at most two entries."""
     arrs = tuple(pr[k] for k, _ in _PROBLEM_FIELDS)
     hd = float(pr["huber_delta"])
-    for ent in _STRUCT_CACHE:
-        if ent[1] == hd and all(x is y for x, y in zip(ent[0], arrs)):
-            return ent[2]
+    with _STRUCT_CACHE_LOCK:
+        for ent in _STRUCT_CACHE:
+            if ent[1] == hd and all(r() is y for r, y in zip(ent[0], arrs)):
+                return ent[2]
     addr = []
     for k, dt in _PROBLEM_FIELDS:
         a = pr[k]
@@ -78,8 +85,11 @@ def as_struct(pr):
         addr.append(a.__array_interface__["data"][0])
     s = BAProblem(len(pr["poses"]), len(pr["points"]), len(pr["edge_pose"]), len(pr["mc"]),
                   *addr, hd)
-    _STRUCT_CACHE.append((tuple(pr[k] for k, _ in _PROBLEM_FIELDS), hd, s))
-    del _STRUCT_CACHE[:-4]
+    refs = tuple(weakref.ref(pr[k]) for k, _ in _PROBLEM_FIELDS)
+    with _STRUCT_CACHE_LOCK:
+        _STRUCT_CACHE[:] = [e for e in _STRUCT_CACHE if all(r() is not None for r in e[0])]
+        _STRUCT_CACHE.append((refs, hd, s))
+        del _STRUCT_CACHE[:-_STRUCT_CACHE_SIZE]
     return s
 
 

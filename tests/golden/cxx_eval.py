@@ -913,6 +913,9 @@ class FuncTranslator:
                 return e.code
         if isinstance(to, Cls) and to.name == "Mat" and fr == Cls("MatExpr"):
             return e.code
+        if to == Cls("Point2d") and fr == Cls("Vec", (DOUBLE, 2)):
+            # cv::Point_<double>(const Vec<double, 2>&): x = v[0], y = v[1] [ext, OpenCV types.hpp]
+            return "_Point2d_vec(%s)" % e.code
         raise Unsupported("conversion %r -> %r of %s" % (fr, to, e.code))
 
     def store(self, lv, code):

@@ -689,6 +689,15 @@ def Point2f(x=0.0, y=0.0):
     return _struct("Point2f", x=f32(x), y=f32(y))
 
 
+def Point2d(x=0.0, y=0.0):
+    return _struct("Point2d", x=dbl(x), y=dbl(y))
+
+
+def point2d_from_vec(v):
+    """cv::Point_<double>(const Vec<double, 2>& v): (v[0], v[1])."""
+    return Point2d(v.v[0], v.v[1])
+
+
 def KeyPoint():
     return _struct("KeyPoint", pt=Point2f(), size=0.0, angle=-1.0, response=0.0, octave=0, class_id=-1)
 
@@ -863,6 +872,6 @@ def env():
         "_cp": cp, "_assign": assign, "_deref": deref, "_inc": inc, "_dec": dec,
         "_addr": addr, "_addr_elem": addr_elem, "_Pair": Pair, "_Cell": Cell,
         "_sort": std_sort, "_copy": std_copy, "_back_inserter": back_inserter, "_remove": std_remove,
-        "_point_imul": point_imul, "_PointView": PointView,
+        "_point_imul": point_imul, "_PointView": PointView, "_Point2d_vec": point2d_from_vec,
         "_range": range, "_len": len,
     }
