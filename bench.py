@@ -337,8 +337,9 @@ def run_global_ba(args, rank, world, local_rank, dev):
     import torch
     import torch.distributed as dist
     from mcs_amd import ba as mba
-    pr = mba.make_global_problem(n_kf=args.gba_kf, n_points=args.gba_points,
-                                 target_edges=args.gba_edges, seed=7)
+    # the map -> graph assembly of BundleAdjustment (mcs_global_ba_select), as a caller would
+    pr = mba.config_e_problem(n_kf=args.gba_kf, n_points=args.gba_points,
+                              target_edges=args.gba_edges, seed=7)
     xch = None
     sub = pr
     if world > 1:

@@ -152,6 +152,92 @@ typedef struct mcs_lba_graph {
 int mcs_local_ba_select(const mcs_lba_map* m, int32_t cur_kf, const int32_t* covis,
                         int32_t n_covis, mcs_lba_graph* g);
 
+/* ---- BundleAdjustment graph assembly (src/cOptimizer.cpp:101-234, write-back :240-259) -----
+ * cOptimizer::GlobalBundleAdjustment (:59-69) calls BundleAdjustment(pMap->GetAllKeyFrames(),
+ * pMap->GetAllMapPoints(), ...).  The two lists as flat arrays, in the caller's order (the
+ * reference's std::set pointer order); each point's observations in its std::map<cMultiKeyFrame*,
+ * vector<size_t>> iteration order (keyframe, then the image points of that keyframe). */
+typedef struct mcs_gba_map {
+  int32_t n_kf;               /* vpKFs.size() */
+  const int64_t* kf_id;       /* [n_kf] mnId */
+  const uint8_t* kf_bad;      /* [n_kf] isBad() */
+  int32_t n_points;           /* vpMP.size() */
+  const int64_t* pt_id;       /* [n_points] mnId (the key of mapPointId_to_cont_g2oId, :163-176) */
+  const uint8_t* pt_bad;      /* [n_points] isBad() */
+  const int32_t* pt_obs_off;  /* [n_points + 1] CSR offsets into obs_kf */
+  const int32_t* obs_kf;      /* observing keyframe of every observation: index into vpKFs */
+  int32_t n_cams;             /* vpKFs[0]->camSystem.GetNrCams() */
+} mcs_gba_map;
+
+/* Outputs (caller-allocated; counts written back).  Vertex ids are g2o's: keyframe mnId, then
+ * the Mc, IO and point vertices from currVertexIdx = maxKF + 1 on (:103-176). */
+typedef struct mcs_gba_graph {
+  int32_t* pose_kf;           /* [n_kf] vpKFs index of every pose vertex (addVertex order) */
+  uint8_t* pose_fixed;        /* [n_kf] setFixed: mnId == 0 (:119-120) */
+  int32_t n_poses;
+  int32_t* points;            /* [n_points] vpMP index of every point vertex (addVertex order) */
+  int64_t* point_vertex_id;   /* [n_points] nullable: the g2o id of every point vertex */
+  int32_t n_points;
+  int64_t mc_vertex_id0;      /* id of camera 0's Mc vertex (maxMcid - nrCams); IO follows */
+  int64_t io_vertex_id0;      /* id of camera 0's IO vertex (maxIOid - nrCams) */
+  int32_t* kf_slot;           /* [n_kf] write-back (:242-249): pose slot of vpKFs[i], -1 if it has
+                                 no pose vertex (a bad keyframe: the reference dereferences NULL) */
+  int32_t* pt_slot;           /* [n_points] write-back (:252-259): point slot of vpMP[i] via
+                                 mapPointId_to_cont_g2oId[mnId] (the last good point of that mnId),
+                                 -1 if none (a bad point: the reference dereferences end()) */
+  int32_t* edge_obs;          /* [edge_cap] observation index of every edge (addEdge order) */
+  int32_t* edge_pose;         /* [edge_cap] pose slot */
+  int32_t* edge_point;        /* [edge_cap] point slot */
+  int32_t n_edges;
+  int32_t edge_cap;
+  int64_t collision_id;       /* out: first vertex id registered twice, -1 = none */
+} mcs_gba_graph;
+
+/* Pose vertices: every non-bad keyframe, in list order, id = mnId, fixed iff mnId == 0.  The
+ * reference's `maxKF` rule (:104-132): `if (pKF->mnId > maxKFid) maxKF = pKF->mnId;` with
+ * maxKFid never updated (0), so maxKF is the mnId of the LAST non-bad keyframe with mnId > 0
+ * (0 if none) and the Mc / IO / point ids start at maxKF + 1 -- not at max(mnId) + 1.  When the
+ * list is not id-ordered these ids can equal a keyframe's mnId; g2o's addVertex then refuses
+ * the second vertex ("FATAL, a vertex with ID .. has already been registered", optimizable_
+ * graph.cpp:243-250) and the edges bind whatever vertex holds the id: this returns
+ * MCS_ERR_ARG with collision_id set and the message, and builds no edges.  Point vertices:
+ * every non-bad point in list order (one id each, also for points without an edge), Huber
+ * delta sqrt(5.991) and information I are the caller's (:161, :209).  Edges: one per
+ * observation from a non-bad keyframe (:189-231); an observing keyframe without a pose vertex
+ * is rejected (the reference would bind a NULL vertex).  An empty vpKFs is rejected
+ * (the reference reads vpKFs[0]).  MCS_ERR_CAPACITY when n_edges > edge_cap (counts written). */
+int mcs_global_ba_select(const mcs_gba_map* m, mcs_gba_graph* g);
+
+/* ---- PoseOptimization graph assembly (src/cOptimizer.cpp:294-430) --------------------------
+ * The frame's mvpMapPoints as indices: key_mp[i] = the map point of keypoint i (index into
+ * pt_id) or -1 (NULL).  Vertex 0 = the frame pose, ids 1..nrCams the Mc vertices, then the IO
+ * vertices, then one fixed point vertex per distinct map-point mnId in order of first
+ * appearance (mapPt_2_obs_idx, :373-392).  One edge per non-NULL keypoint, in keypoint order
+ * (:364-430), bad map points included (the reference does not test isBad here).  The caller
+ * fills edge_meas = mvKeys[i].pt, edge_cam = keypoint_to_cam[i], edge_info =
+ * mvInvLevelSigma2[mvKeys[i].octave] and huber_delta = 1.345 * huberMultiplier (:344, :398-406)
+ * and passes the problem to mcs_pose_optimization; keypoints without an edge keep
+ * mvbOutlier = false (:367). */
+typedef struct mcs_po_frame {
+  int32_t n_keys;             /* N = mvpMapPoints.size() */
+  const int32_t* key_mp;      /* [n_keys] map point index or -1 */
+  int32_t n_mp;
+  const int64_t* pt_id;       /* [n_mp] mnId */
+  int32_t n_cams;
+} mcs_po_frame;
+
+typedef struct mcs_po_graph {
+  int32_t* points;            /* [n_mp] map point index of every point vertex */
+  int64_t* point_vertex_id;   /* [n_mp] nullable */
+  int32_t n_points;
+  int32_t* edge_obs;          /* [edge_cap] keypoint index i of every edge (vnIndexEdge) */
+  int32_t* edge_point;        /* [edge_cap] point slot */
+  int32_t n_edges;
+  int32_t edge_cap;
+} mcs_po_graph;
+
+int mcs_pose_optimization_select(const mcs_po_frame* f, mcs_po_graph* g);
+
 /* cOptimizer::PoseOptimization (src/cOptimizer.cpp:264-486) after graph construction:
  * p->n_poses == 1 (the frame's M_t, optimised; pose_fixed is ignored), every map point fixed
  * (:382), Mc / IO fixed, Huber delta = p->huber_delta (1.345 * huberMultiplier, :344),
@@ -283,8 +369,7 @@ int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const doubl
  * else pad + the pipelined factorisation (one launch) + backward), path 1 = always pad + one
  * panel launch per step + the multi-workgroup backward, path 2 = always pad + pipelined
  * factorisation + backward (bitwise equal to path 1), path 3 = pad + one panel launch per step
- * + the one-workgroup backward substitution (what every path runs above 96 tiles, n > 6144,
- * and the BA with MCS_LDLT_PIPE=0).  Paths 0-2 give bitwise equal x
+ * + the one-workgroup backward substitution (what every path runs above 96 tiles, n > 6144).  Paths 0-2 give bitwise equal x
  * (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled).  A timed-out hand-off wait
  * of the pipelined kernels returns MCS_ERR_HIP (never a zero pivot). */
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,

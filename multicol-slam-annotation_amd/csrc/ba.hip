@@ -1643,7 +1643,7 @@ struct mcs_ba_ctx {
   // optional stage timing (mcs_ba_enable_timing): HIP events on st around each stage,
   // accumulated after the per-trial synchronisation the LM control needs anyway
   bool timing = false;
-  bool ldlt_pipe = true;   // pipelined LDL^T for multi-tile systems (MCS_LDLT_PIPE=0: per-step launches)
+  bool ldlt_pipe = true;   // pipelined LDL^T for multi-tile systems (2 <= T <= kPipeMaxT)
   hipEvent_t ev[8] = {};
   double acc_ms[MCS_BA_NSTAGES] = {};
   double host_ms[MCS_BA_NHOST] = {};   // host phases (mcs_ba_read_host_timing)
@@ -1910,13 +1910,13 @@ struct Optimizer {
       sh.xchg = (double*)c->alloc((size_t)xchg_doubles(p->n_poses) * 8);
       if (!sh.xchg) { set_error("BA: out of device memory"); return MCS_ERR_HIP; }
     }
-    // ---- threaded (config-E-sized) calls with MCS_SPLIT_UPLOAD=1: the problem arrays go up
-    // now, their copy overlapping the structure build; the structure arrays follow from the
-    // second staging buffer (written, not yet measured on the device: off by default)
+    // ---- threaded (config-E-sized) calls: the problem arrays go up now, their copy
+    // overlapping the structure build; the structure arrays follow from the second staging
+    // buffer (GlobalBA 6.15 / 6.20 -> 5.86 / 5.47 ms per call, profiles/r06_split_ab.txt).  The
+    // second flush relies on this first one's spin_sync (Packer::flush): split implies it ran.
     NE = p->n_edges;
     double *d_poses_bk = nullptr, *d_points_bk = nullptr;
-    static const bool split_env = [] { const char* e = std::getenv("MCS_SPLIT_UPLOAD"); return e && e[0] == '1'; }();
-    const bool split = pool && split_env;
+    const bool split = pool != nullptr;
     if (split) {
       Packer pk;
       add_problem(pk, poses, points, &d_poses_bk, &d_points_bk);
@@ -2556,8 +2556,9 @@ struct Optimizer {
     Dev dd = d;
     dd.ctl = dctl;
     // one-tile systems (LocalBA): k_schur adds a split block's chunk slots itself (fused fin)
-    static const int fuse_env = [] { const char* e = std::getenv("MCS_FUSE_FIN"); return e ? std::atoi(e) : -1; }();
-    const bool fuse = fuse_env >= 0 ? fuse_env != 0 : T == 1;
+    // (multi-tile systems keep the k_schur_fin launch: fused, config E measured 7.07 against
+    // 6.90 ms per GlobalBA call)
+    const bool fuse = T == 1;
     dd.blk_arrive = (fuse && nblk > 0) ? (uint32_t*)c->alloc(4 * (size_t)nblk) : nullptr;
     hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(256), 0, st, h0, dctl, dd.blk_arrive, nblk);
     const int* skip = &dctl->done;
@@ -2705,10 +2706,6 @@ int mcs_ba_create(int32_t device, mcs_ba_ctx** out) {
   mcs_ba_ctx* c = new (std::nothrow) mcs_ba_ctx();
   if (!c) return MCS_ERR_ARG;
   c->device = device;
-  {
-    const char* e = std::getenv("MCS_LDLT_PIPE");
-    c->ldlt_pipe = !(e && e[0] == '0');
-  }
   MCS_HIP_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned, 64, hipHostMallocDefault));
   MCS_HIP_CHECK(hipHostMalloc((void**)&c->pinned_i, 64, hipHostMallocMapped));   // k_lba_count writes it

@@ -143,12 +143,9 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   // reuse of level l-1 and its CU slots.)
   // The level-0 blur depends on the input only: on the side stream it runs beside the chain
   // (sharing the chain's level-0 reads while level 1 streams them, and filling the CUs the
-  // small levels 4..7 leave idle); FAST joins both.  MCS_BLUR0_SIDE=0 restores the serial order.
-  static const bool side_blur = [] {
-    const char* e = std::getenv("MCS_BLUR0_SIDE");
-    return !(e && e[0] == '0');
-  }();
-  const bool use_side = side_blur && !h->timing;
+  // small levels 4..7 leave idle); FAST joins both.  With stage timing on, the serial order
+  // (the stage events need one stream).
+  const bool use_side = !h->timing;
   if (use_side && !h->side) {
     MCS_HIP_CHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
     MCS_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));

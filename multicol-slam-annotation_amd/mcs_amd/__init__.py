@@ -122,6 +122,8 @@ SIGNATURES = {
     "mcs_is_in_frustum_device": (ctypes.c_int, [_P, _P, _P, _I32, _P, _I32, _I32, _P, _P, _P,
                                                 _I32, _P, _I32, _P, _P, _P, _P, _P]),
     "mcs_local_ba_select": (ctypes.c_int, [_P, _I32, _P, _I32, _P]),
+    "mcs_global_ba_select": (ctypes.c_int, [_P, _P]),
+    "mcs_pose_optimization_select": (ctypes.c_int, [_P, _P]),
     "mcs_ba_linearize": (ctypes.c_int, [_P] * 5),
     "mcs_ba_xchg_doubles": (_I64, [_I32]),
     "mcs_ba_optimize_sharded": (ctypes.c_int, [_P] * 10),

@@ -338,6 +338,126 @@ def problem_from_graph(m, g, huber_delta=1.345 * 2):
                 edge_info=m["obs_info"][o].copy(), huber_delta=huber_delta)
 
 
+class GbaMap(ctypes.Structure):
+    """Mirror of mcs_gba_map (include/mcs_ba.h)."""
+    _fields_ = [("n_kf", ctypes.c_int32), ("kf_id", ctypes.c_void_p), ("kf_bad", ctypes.c_void_p),
+                ("n_points", ctypes.c_int32), ("pt_id", ctypes.c_void_p), ("pt_bad", ctypes.c_void_p),
+                ("pt_obs_off", ctypes.c_void_p), ("obs_kf", ctypes.c_void_p), ("n_cams", ctypes.c_int32)]
+
+
+class GbaGraph(ctypes.Structure):
+    """Mirror of mcs_gba_graph."""
+    _fields_ = [("pose_kf", ctypes.c_void_p), ("pose_fixed", ctypes.c_void_p), ("n_poses", ctypes.c_int32),
+                ("points", ctypes.c_void_p), ("point_vertex_id", ctypes.c_void_p), ("n_points", ctypes.c_int32),
+                ("mc_vertex_id0", ctypes.c_int64), ("io_vertex_id0", ctypes.c_int64),
+                ("kf_slot", ctypes.c_void_p), ("pt_slot", ctypes.c_void_p),
+                ("edge_obs", ctypes.c_void_p), ("edge_pose", ctypes.c_void_p), ("edge_point", ctypes.c_void_p),
+                ("n_edges", ctypes.c_int32), ("edge_cap", ctypes.c_int32), ("collision_id", ctypes.c_int64)]
+
+
+class PoFrame(ctypes.Structure):
+    """Mirror of mcs_po_frame."""
+    _fields_ = [("n_keys", ctypes.c_int32), ("key_mp", ctypes.c_void_p), ("n_mp", ctypes.c_int32),
+                ("pt_id", ctypes.c_void_p), ("n_cams", ctypes.c_int32)]
+
+
+class PoGraph(ctypes.Structure):
+    """Mirror of mcs_po_graph."""
+    _fields_ = [("points", ctypes.c_void_p), ("point_vertex_id", ctypes.c_void_p), ("n_points", ctypes.c_int32),
+                ("edge_obs", ctypes.c_void_p), ("edge_point", ctypes.c_void_p), ("n_edges", ctypes.c_int32),
+                ("edge_cap", ctypes.c_int32)]
+
+
+def global_ba_select(m, raise_on_error=True):
+    """mcs_global_ba_select: the vertices and edges cOptimizer::BundleAdjustment builds from
+    (vpKFs, vpMP) = the map dict's keyframes and points in list order (src/cOptimizer.cpp:101-234),
+    and the write-back slots of :240-259.  m needs kf_id, kf_bad, pt_id, pt_bad, pt_obs_off,
+    obs_kf and mc (n_cams)."""
+    from . import lib, McsError
+    for k, dt in (("kf_id", np.int64), ("kf_bad", np.uint8), ("pt_id", np.int64), ("pt_bad", np.uint8),
+                  ("pt_obs_off", np.int32), ("obs_kf", np.int32)):
+        m[k] = np.ascontiguousarray(m[k], dt)
+    nk, npt, nobs = len(m["kf_id"]), len(m["pt_bad"]), len(m["obs_kf"])
+    st = GbaMap(nk, _p(m["kf_id"]), _p(m["kf_bad"]), npt, _p(m["pt_id"]), _p(m["pt_bad"]),
+                _p(m["pt_obs_off"]), _p(m["obs_kf"]), len(m["mc"]))
+    b = dict(pose_kf=np.zeros(max(1, nk), np.int32), pose_fixed=np.zeros(max(1, nk), np.uint8),
+             points=np.zeros(max(1, npt), np.int32), point_vertex_id=np.zeros(max(1, npt), np.int64),
+             kf_slot=np.zeros(max(1, nk), np.int32), pt_slot=np.zeros(max(1, npt), np.int32),
+             edge_obs=np.zeros(max(1, nobs), np.int32), edge_pose=np.zeros(max(1, nobs), np.int32),
+             edge_point=np.zeros(max(1, nobs), np.int32))
+    g = GbaGraph(_p(b["pose_kf"]), _p(b["pose_fixed"]), 0, _p(b["points"]), _p(b["point_vertex_id"]), 0,
+                 -1, -1, _p(b["kf_slot"]), _p(b["pt_slot"]), _p(b["edge_obs"]), _p(b["edge_pose"]),
+                 _p(b["edge_point"]), 0, nobs, -1)
+    rc = lib().mcs_global_ba_select(ctypes.byref(st), ctypes.byref(g))
+    if rc < 0 and raise_on_error:
+        raise McsError(rc, lib().mcs_last_error().decode())
+    npo, npp, ne = g.n_poses, g.n_points, g.n_edges
+    return dict(status=rc, collision_id=g.collision_id, pose_kf=b["pose_kf"][:npo].copy(),
+                pose_fixed=b["pose_fixed"][:npo].copy(), points=b["points"][:npp].copy(),
+                point_vertex_id=b["point_vertex_id"][:npp].copy(), mc_vertex_id0=g.mc_vertex_id0,
+                io_vertex_id0=g.io_vertex_id0, kf_slot=b["kf_slot"][:nk].copy(),
+                pt_slot=b["pt_slot"][:npt].copy(), edge_obs=b["edge_obs"][:ne].copy(),
+                edge_pose=b["edge_pose"][:ne].copy(), edge_point=b["edge_point"][:ne].copy())
+
+
+def problem_from_gba_graph(m, g):
+    """mcs_ba_problem of one BundleAdjustment call: poses = the keyframe vertices (mnId 0
+    fixed), points = the point vertices, one edge per selected observation with measurement
+    kp.pt, information I (:209) and Huber sqrt(5.991) (:161)."""
+    o = g["edge_obs"]
+    return dict(poses=np.ascontiguousarray(m["kf_pose"][g["pose_kf"]]), pose_fixed=g["pose_fixed"].copy(),
+                points=np.ascontiguousarray(m["pt_pos"][g["points"]]), mc=m["mc"], cam=m["cam"],
+                edge_pose=g["edge_pose"].astype(np.int32), edge_point=g["edge_point"].astype(np.int32),
+                edge_cam=np.asarray(m["obs_cam"])[o].astype(np.int32),
+                edge_meas=np.ascontiguousarray(np.asarray(m["obs_meas"])[o]), edge_info=np.ones(len(o)),
+                huber_delta=HUBER_GLOBAL)
+
+
+def global_ba_write_back(m, g, poses, points):
+    """The reference's recovery loops (:242-259) over the select's slots: new keyframe poses
+    and point positions for every list entry with a vertex (others keep their values)."""
+    kp = np.array(m["kf_pose"], np.float64, copy=True)
+    pp = np.array(m["pt_pos"], np.float64, copy=True)
+    ks, ps = g["kf_slot"], g["pt_slot"]
+    kp[ks >= 0] = poses[ks[ks >= 0]]
+    pp[ps >= 0] = points[ps[ps >= 0]]
+    return kp, pp
+
+
+def global_map_from_problem(pr):
+    """Config E as the map GlobalBundleAdjustment reads: keyframe i = pose i (mnId = i, so
+    keyframe 0 is the fixed one), point j = point j (mnId = j), observations = the problem's
+    edges in point order (each point's edges are in keyframe order, the std::map order)."""
+    ep = np.asarray(pr["edge_point"])
+    order = np.argsort(ep, kind="stable")
+    npt, nk = len(pr["points"]), len(pr["poses"])
+    off = np.zeros(npt + 1, np.int64)
+    np.add.at(off, ep + 1, 1)
+    return dict(kf_id=np.arange(nk, dtype=np.int64), kf_bad=np.zeros(nk, np.uint8),
+                pt_id=np.arange(npt, dtype=np.int64), pt_bad=np.zeros(npt, np.uint8),
+                pt_obs_off=np.cumsum(off).astype(np.int32),
+                obs_kf=np.asarray(pr["edge_pose"])[order].astype(np.int32),
+                obs_cam=np.asarray(pr["edge_cam"])[order], obs_meas=np.asarray(pr["edge_meas"])[order],
+                kf_pose=pr["poses"], pt_pos=pr["points"], mc=pr["mc"], cam=pr["cam"])
+
+
+def pose_optimization_select(key_mp, pt_id, n_cams):
+    """mcs_pose_optimization_select: PoseOptimization's point vertices (one per distinct
+    mnId, first appearance) and edges (one per non-NULL keypoint), src/cOptimizer.cpp:364-430."""
+    from . import lib, McsError
+    km = np.ascontiguousarray(key_mp, np.int32)
+    pid = np.ascontiguousarray(pt_id, np.int64)
+    f = PoFrame(len(km), _p(km), len(pid), _p(pid), int(n_cams))
+    b = dict(points=np.zeros(max(1, len(pid)), np.int32), point_vertex_id=np.zeros(max(1, len(pid)), np.int64),
+             edge_obs=np.zeros(max(1, len(km)), np.int32), edge_point=np.zeros(max(1, len(km)), np.int32))
+    g = PoGraph(_p(b["points"]), _p(b["point_vertex_id"]), 0, _p(b["edge_obs"]), _p(b["edge_point"]), 0, len(km))
+    rc = lib().mcs_pose_optimization_select(ctypes.byref(f), ctypes.byref(g))
+    if rc < 0:
+        raise McsError(rc, lib().mcs_last_error().decode())
+    return dict(points=b["points"][:g.n_points].copy(), point_vertex_id=b["point_vertex_id"][:g.n_points].copy(),
+                edge_obs=b["edge_obs"][:g.n_edges].copy(), edge_point=b["edge_point"][:g.n_edges].copy())
+
+
 def make_map(n_kf=16, n_points=2500, target_edges=14000, seed=0, bad_kf=(), bad_points=0.01,
              zero_id_kf=None, unmatched_frac=0.1, covis_th=15):
     """Synthetic MultiKeyFrame map for LocalBundleAdjustment assembly: keyframes with mnId,
@@ -640,6 +760,18 @@ def make_global_problem(n_kf=200, n_points=50000, target_edges=400000, ncams=8, 
                 edge_cam=(cols % ncams).astype(np.int32), edge_meas=meas,
                 edge_info=np.ones(ne), huber_delta=HUBER_GLOBAL, gt_poses=gt_poses,
                 gt_points=gt_pts)
+
+
+def config_e_problem(n_kf=200, n_points=50000, target_edges=400000, seed=7, **kw):
+    """Config E through the reference-side boundary: the generated map (make_global_problem as
+    GlobalBundleAdjustment's keyframe / map-point lists) assembled by mcs_global_ba_select into
+    the problem mcs_global_ba takes (src/cOptimizer.cpp:101-234).  Ground truth kept."""
+    pr = make_global_problem(n_kf=n_kf, n_points=n_points, target_edges=target_edges, seed=seed, **kw)
+    m = global_map_from_problem(pr)
+    g = global_ba_select(m)
+    out = problem_from_gba_graph(m, g)
+    out["gt_poses"], out["gt_points"] = pr["gt_poses"], pr["gt_points"]
+    return out
 
 
 def shard_points(pr, world):

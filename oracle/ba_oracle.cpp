@@ -663,11 +663,22 @@ int oracle_ba_edge(const double* pose, const double* X, const double* mc, const 
   return 0;
 }
 
+int oracle_ba_optimize_ex(const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
+                          double* points, const uint8_t* edge_level, double* edge_chi2,
+                          int32_t* stop_flag, mcs_ba_report* rep, int32_t points_fixed);
 int oracle_ba_optimize(const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
                        double* points, const uint8_t* edge_level, double* edge_chi2,
                        int32_t* stop_flag, mcs_ba_report* rep) {
+  return oracle_ba_optimize_ex(p, o, poses, points, edge_level, edge_chi2, stop_flag, rep, 0);
+}
+
+// the same with every point vertex fixed (BundleAdjustment(poseOnly) :178, PoseOptimization :382)
+int oracle_ba_optimize_ex(const mcs_ba_problem* p, const mcs_ba_options* o, double* poses,
+                          double* points, const uint8_t* edge_level, double* edge_chi2,
+                          int32_t* stop_flag, mcs_ba_report* rep, int32_t points_fixed) {
   Graph g;
   g.P = p;
+  g.points_fixed = points_fixed != 0;
   g.poses.assign(poses, poses + 6 * p->n_poses);
   g.points.assign(points, points + 3 * p->n_points);
   g.level.assign(p->n_edges, 0);

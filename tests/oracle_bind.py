@@ -315,7 +315,7 @@ def ba_edge(pose, X, mc, cam, meas):
     return err, jp, jl
 
 
-def ba_optimize(pr, options=None, edge_level=None, stop_flag=None, trace=0):
+def ba_optimize(pr, options=None, edge_level=None, stop_flag=None, trace=0, points_fixed=False):
     import ctypes as C
     from mcs_amd import ba
     L = _ba_sigs()
@@ -329,8 +329,11 @@ def ba_optimize(pr, options=None, edge_level=None, stop_flag=None, trace=0):
     tr = np.zeros(max(trace, 1))
     rep = ba.BAReport(0, 0, 0, 0, 0, 0, 0, 0, _p(tr) if trace else None, trace)
     sf = None if stop_flag is None else C.c_int32(int(stop_flag))
-    L.oracle_ba_optimize(C.byref(s), C.byref(o), _p(poses), _p(points), _p(lvl), _p(chi),
-                         C.byref(sf) if sf is not None else None, C.byref(rep))
+    f = L.oracle_ba_optimize_ex
+    f.restype = _I
+    f.argtypes = [_P] * 8 + [C.c_int32]
+    f(C.byref(s), C.byref(o), _p(poses), _p(points), _p(lvl), _p(chi),
+      C.byref(sf) if sf is not None else None, C.byref(rep), int(bool(points_fixed)))
     return dict(poses=poses, points=points, edge_chi2=chi, report=rep,
                 stop_flag=None if sf is None else sf.value, trace=tr[:min(trace, rep.iterations)])
 

@@ -21,8 +21,9 @@ from tests.test_global_ba import ThreadExchange, _oracle_global
 
 @pytest.fixture(scope="module")
 def eproblem():
+    """The bench's problem, assembled from the map by mcs_global_ba_select."""
     from mcs_amd import ba
-    return ba.make_global_problem(n_kf=200, n_points=50000, target_edges=400000, seed=7)
+    return ba.config_e_problem(n_kf=200, n_points=50000, target_edges=400000, seed=7)
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +37,15 @@ def egpu(eproblem):
     return ba.Solver().global_ba(eproblem, trace=20)
 
 
-def test_config_e_problem_shape(eproblem):
+def test_config_e_problem_shape(built, eproblem):
+    """Config E assembled by mcs_global_ba_select (map -> graph of BundleAdjustment) is the
+    generator's flat problem: same vertices, edge order and measurements."""
+    from mcs_amd import ba
+    raw = ba.make_global_problem(n_kf=200, n_points=50000, target_edges=400000, seed=7)
+    for k in ("poses", "pose_fixed", "points", "mc", "cam", "edge_pose", "edge_point", "edge_cam",
+              "edge_meas", "edge_info"):
+        assert np.array_equal(np.asarray(raw[k]), np.asarray(eproblem[k])), k
+    assert eproblem["huber_delta"] == raw["huber_delta"]
     pr = eproblem
     assert len(pr["poses"]) == 200 and len(pr["points"]) >= 49900
     assert 390000 <= len(pr["edge_pose"]) <= 410000

@@ -13,7 +13,7 @@ CPU: the product's mcs_local_ba_select (host code) reproduces the selection, ver
 edge list exactly; the oracle's select + local_ba_ex reproduce the culling, write-back sets and
 estimates bit for bit (they run the same restated g2o rounds).  GPU: select -> mcs_local_ba_ex
 reproduces the culled edges and written-back points exactly, poses abs 1e-6, points with >= 3
-observations abs 1e-5, 2-observation points abs 1e-3 (as tests/test_local_ba_select.py).
+observations abs 1e-5, 2-observation points 1e-5 of their scale (as tests/test_ba.py).
 """
 import os
 
@@ -148,7 +148,11 @@ def test_gpu_local_ba_matches_reference_text(gpu, name):
     w2 = (pw == 1) & (cnt == 2)
     assert np.abs(r["points"][w3] - z[p + "est_points"][w3]).max() < 1e-5
     if w2.any():
-        assert np.abs(r["points"][w2] - z[p + "est_points"][w2]).max() < 1e-3
+        # two-observation points are weakly constrained along their rays: the same 1e-5 of the
+        # point's own scale (distance from the origin) as tests/test_ba.py
+        scale = np.maximum(1.0, np.linalg.norm(z[p + "est_points"][w2], axis=1))
+        rel = np.abs(r["points"][w2] - z[p + "est_points"][w2]).max(axis=1) / scale
+        assert rel.max() < 1e-5, rel.max()
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="needs the reference checkout")
