@@ -3,7 +3,12 @@
  *
  * Replaces (billamiable/MultiCol-SLAM-Annotation):
  *   cOptimizer::LocalBundleAdjustment(pKF, pMap, nrIters, getCovMats, pbStopFlag)
- *       include/cOptimizer.h:61-65, src/cOptimizer.cpp:489-908   -> mcs_local_ba
+ *       include/cOptimizer.h:61-65, src/cOptimizer.cpp:489-908   -> mcs_local_ba_select + mcs_local_ba_ex
+ *   cOptimizer::BundleAdjustment / GlobalBundleAdjustment
+ *       include/cOptimizer.h:50-59, src/cOptimizer.cpp:59-261     -> mcs_global_ba_select + mcs_global_ba
+ *   cOptimizer::PoseOptimization(pFrame, inliers, huberMultiplier)
+ *       include/cOptimizer.h:67-69, src/cOptimizer.cpp:264-486    -> mcs_pose_optimization_select
+ *                                                                    + mcs_pose_optimization
  *   g2o::SparseOptimizer::initializeOptimization(0) + optimize(n) with
  *       OptimizationAlgorithmLevenberg + BlockSolver_6_3 + LinearSolverEigen and a
  *       SparseOptimizerTerminateAction        (ThirdParty/g2o/g2o/core)        -> mcs_ba_optimize
@@ -366,10 +371,14 @@ int mcs_ba_huber_eval(int32_t device, const double* e, int32_t n, double delta, 
 int mcs_dense_ldlt_solve(int32_t device, const double* S, int32_t n, const double* b, double* x,
                          int32_t* zero_pivot);
 /* Same, choosing the kernels: path 0 = what the BA uses (n <= 64: the fused one-tile solve,
- * else pad + the pipelined factorisation (one launch) + backward), path 1 = always pad + one
+ * else pad + the pipelined factorisation (one launch) over the tile band of S -- tiles below the
+ * widest tile diagonal holding a non-zero are skipped, as the BA skips the pose pairs no point
+ * connects -- + backward; banded systems of any size the pipeline's task bound takes, e.g.
+ * n > 12288), path 1 = always pad + one
  * panel launch per step + the multi-workgroup backward, path 2 = always pad + pipelined
  * factorisation + backward (bitwise equal to path 1), path 3 = pad + one panel launch per step
- * + the one-workgroup backward substitution (what every path runs above 96 tiles, n > 6144).  Paths 0-2 give bitwise equal x
+ * + the one-workgroup backward substitution (dense systems above 96 tiles, n > 6144, run this
+ * path; it takes n <= 12288).  Paths 0-2 give bitwise equal x
  * (tests/test_global_ba.py::test_gpu_one_tile_solve_matches_tiled).  A timed-out hand-off wait
  * of the pipelined kernels returns MCS_ERR_HIP (never a zero pivot). */
 int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const double* b, double* x,

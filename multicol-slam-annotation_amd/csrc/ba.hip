@@ -1804,6 +1804,7 @@ struct Optimizer {
   HostStruct& s;
   Dev d;
   int n = 0, T = 1, NE = 0;
+  int band = 1;          // tile bandwidth of the reduced camera system (ldlt::Work::band)
   int64_t pmax = 0;      // upper bound of the Schur pairs (device-built lists)
   int items_max = 1;     // upper bound of the k_schur work items
   int32_t* it_nch_dev = nullptr;   // chunks of each item's block (checked by the test hook)
@@ -1932,28 +1933,40 @@ struct Optimizer {
     nae_glob = (int)cnt[p->n_poses + 1];
     n = 6 * s.np;
     T = ldlt::tiles_for(std::max(1, n));
-    if ((size_t)T * ldlt::TB * 8 > 96 * 1024) {
-      set_error("more than 2048 active poses: exceeds the backward-solve LDS budget");
-      return MCS_ERR_UNSUPPORTED;
-    }
     X = XLayout(T, s.np);
     xs_count = X.hdiag - X.bs;
-    if (sharded && T > 1) {
+    band = T;
+    if (T > 1) {
       // Tiles of S below the widest tile diagonal any rank's points touch are zero on every
-      // rank (their blocks have no pairs; the padding rows there are zero too), so the
-      // exchange stops at that diagonal: bs + diagonals 0 .. w of the diagonal-major tiles.
-      int w = 1;   // diagonal pose blocks straddling a tile boundary reach diagonal 1
-      for (int q = 0; q < s.nl; q++) {
-        int lo = INT32_MAX, hi = -1;
-        for (int e = s.pt_ptr[q]; e < s.pt_ptr[q + 1]; e++) {
-          const int h = s.pt_h[e];
-          if (h >= 0) { lo = std::min(lo, h); hi = std::max(hi, h); }
+      // rank (their blocks have no pairs; the padding rows there are zero too), and LDL^T keeps
+      // a banded matrix's L inside the same band: the factorisation runs on diagonals 0 .. w
+      // only (ldlt::Work::band), and the sharded exchange stops at diagonal w too.
+      std::vector<int> wpart(pool ? pool->size() : 1, 1);   // >= 1: pose blocks straddling a tile boundary
+      auto span = [&](int t, int nt) {
+        const int q0 = (int)((int64_t)s.nl * t / nt), q1 = (int)((int64_t)s.nl * (t + 1) / nt);
+        int w = 1;
+        for (int q = q0; q < q1; q++) {
+          int lo = INT32_MAX, hi = -1;
+          for (int e = s.pt_ptr[q]; e < s.pt_ptr[q + 1]; e++) {
+            const int h = s.pt_h[e];
+            if (h >= 0) { lo = std::min(lo, h); hi = std::max(hi, h); }
+          }
+          if (hi >= 0) w = std::max(w, (6 * hi + 5) / ldlt::TB - (6 * lo) / ldlt::TB);
         }
-        if (hi >= 0) w = std::max(w, (6 * hi + 5) / ldlt::TB - (6 * lo) / ldlt::TB);
-      }
-      double wd = w;
+        wpart[t] = w;
+      };
+      if (pool && s.nl >= 4096) pool->run([&](int t) { span(t, (int)wpart.size()); });
+      else span(0, 1);
+      double wd = *std::max_element(wpart.begin(), wpart.end());
       if ((rc = allreduce_host(&wd, 1, MCS_REDUCE_MAX, X.sc))) return rc;
-      xs_count = (size_t)ldlt::TB * T + ldlt::band_tiles((int)wd + 1, T) * ldlt::TB * ldlt::TB;
+      band = ldlt::pipe_band(T, (int)wd + 1);
+      if (sharded) xs_count = (size_t)ldlt::TB * T + ldlt::band_tiles((int)wd + 1, T) * ldlt::TB * ldlt::TB;
+    }
+    const bool pipelined = T >= 2 && c->ldlt_pipe && ldlt::pipe_supported(T, band);
+    if (!pipelined && (size_t)T * ldlt::TB * 8 > 96 * 1024) {
+      set_error("more than 2048 active poses with a reduced camera system too wide for the banded "
+                "factorisation (its task table exceeds the pipeline's bound)");
+      return MCS_ERR_UNSUPPORTED;
     }
     {
       Packer pk;
@@ -2011,16 +2024,17 @@ struct Optimizer {
     lw.z = dz((size_t)ldlt::TB * T);
     // pipelined factorisation (one launch per solve) for every multi-tile system
     lw.W = nullptr; lw.du = nullptr; lw.sync = nullptr; lw.tasks = nullptr; lw.ntasks = 0; lw.pipe_T = 0;
-    if (T >= 2 && T <= ldlt::kPipeMaxT && c->ldlt_pipe) {
-      const std::vector<int4>& tq = ldlt::pipe_tasks_host(T);
+    if (pipelined) {
+      const std::vector<int4>& tq = ldlt::pipe_tasks_host(T, band);
       lw.W = dz(ldlt::tile_doubles(T));
       lw.du = dz((size_t)T * 128);
-      lw.sync = (unsigned*)dz((ldlt::pipe_sync_words(T) + 1) / 2);
+      lw.sync = (unsigned*)dz((ldlt::pipe_sync_words(T, band) + 1) / 2);
       lw.tasks = (int4*)dz(2 * tq.size());
       if (he == hipSuccess && lw.tasks)
         he = hipMemcpyAsync(lw.tasks, tq.data(), tq.size() * sizeof(int4), hipMemcpyHostToDevice, st);
       lw.ntasks = (int)tq.size();
       lw.pipe_T = T;
+      lw.band = band;
     }
     // scalars: [0] chi2 [1] point scale [2] pose scale [3] chi_now; the solve flag in [5] (one
     // 48-byte readback per trial)
@@ -3158,8 +3172,19 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
   }
   MCS_HIP_CHECK(hipSetDevice(device));
   const int T = ldlt::tiles_for(n);
-  if ((size_t)T * ldlt::TB * 8 > 96 * 1024) return MCS_ERR_UNSUPPORTED;
   const size_t NT = ldlt::tile_doubles(T), Np = (size_t)ldlt::TB * T;
+  // path 0: the tile band of S (the widest tile diagonal holding a non-zero), as the BA derives
+  // it from its structure; the other paths factor densely
+  int band = T;
+  if (path == 0 && T > 1) {
+    int w = 1;
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < r; c++)
+        if (S[(size_t)r * n + c] != 0.0) { w = std::max(w, r / ldlt::TB - c / ldlt::TB); break; }
+    band = ldlt::pipe_band(T, w + 1);
+  }
+  const bool pipelined = path != 3 && T >= 2 && ldlt::pipe_supported(T, band);
+  if (!pipelined && T > 1 && (size_t)T * ldlt::TB * 8 > 96 * 1024) return MCS_ERR_UNSUPPORTED;
   std::vector<double> hA(NT, 0.0), hb(Np, 0.0);
   for (int r = 0; r < n; r++)
     for (int c = 0; c <= r; c++) hA[ldlt::sidx(r, c, T)] = S[(size_t)r * n + c];
@@ -3185,12 +3210,11 @@ int mcs_dense_ldlt_solve_ex(int32_t device, const double* S, int32_t n, const do
     } else {
       chk(ldlt::pad(dA, db, n, T, 1.0, st), "pad");
       ldlt::Work w{dL, dI, dz};
-      // path 0 and 2: the pipelined factorisation (one launch); path 1: one launch per step;
-      // both with the multi-workgroup backward substitution.  Path 3, and every path above
-      // kPipeMaxT tiles (as in the BA): one launch per step + the one-workgroup backward
-      // substitution, without the pipeline's sync words.
-      const bool pipelined = path != 3 && T <= ldlt::kPipeMaxT;
-      if (rc == MCS_OK && pipelined) chk(ldlt::pipe_prepare(w, T, st), "pipe_prepare");
+      // path 0 (banded) and 2 (dense): the pipelined factorisation (one launch); path 1: one
+      // launch per step; all with the multi-workgroup backward substitution.  Path 3, and a
+      // system the pipeline does not take (as in the BA): one launch per step + the
+      // one-workgroup backward substitution, without the pipeline's sync words.
+      if (rc == MCS_OK && pipelined) chk(ldlt::pipe_prepare(w, T, st, path == 0 ? band : 0), "pipe_prepare");
       w.per_step = (path == 1);
       chk(ldlt::solve(dA, db, dx, T, w, dflag, st), "ldlt");
       chk(hipStreamSynchronize(st), "sync");

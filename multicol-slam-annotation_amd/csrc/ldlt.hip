@@ -16,6 +16,7 @@
 // backward (one workgroup): x_k = Linv_kk^T z_k, z_j -= L_kj^T x_k for j < k.
 #include "ldlt.hpp"
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -831,12 +832,16 @@ struct PipeArgs {
   unsigned* sync;       // [0] ticket, [1] error, [4..] product counters, panel flags, diag flags
   const int4* tasks;    // (type 0 TRSM / 1 UPDATE, i, j, k)
   int ntasks, T, ntile;
+  int D;                // tile bandwidth (tiles with I - J >= D are zero and never touched)
   int* flag;
   const int* skip;
   long long wait_ticks;
 };
 
 __device__ __forceinline__ int tix(int I, int J, int T) { return (int)band_tiles(I - J, T) + J; }
+// the first step whose product reaches tile row i (L_ik = 0 for k < i - (D - 1)); the product
+// counters count from there, so a tile's counter holds (products applied) = (next k) - kbase
+__device__ __forceinline__ int kbase(int i, int D) { return max(0, i - (D - 1)); }
 
 #ifdef MCS_LDLT_PROBE
 // probe builds only: diag step stamps [k][8] and task stamps [ticket][4] (s_memrealtime, 100 MHz)
@@ -923,7 +928,9 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     DSTAMP(k, 0);
     // A_kk after products 0 .. k-2 (UPDATE tasks), then product k-1 from the tiles this
     // workgroup formed at step k-1 (still in sX / sY, u_{k-1} in su)
-    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)(k - 1), nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
+    if (k >= 2 && !wg_wait(cnt + tix(k, k, T), (unsigned)max(0, k - 1 - kbase(k, g.D)), nullptr, 0, nullptr, 0, err,
+                           sh_ok, g.wait_ticks))
+      break;
     DSTAMP(k, 1);
     // A_kk -= L_{k,k-1} W_{k,k-1}^T on the 10 lower 16x16 blocks only (the upper ones are
     // not read by the factorisation), 3 / 3 / 2 / 2 blocks per wave; each block is the same
@@ -992,7 +999,9 @@ __device__ void diag_role(const PipeArgs& g, double* sm, int* sh_ok, int* fail) 
     DSTAMP(k, 4);
     if (k + 1 < T) {
       // the next panel tile: A_{k+1,k} after products 0 .. k-1
-      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)k, nullptr, 0, nullptr, 0, err, sh_ok, g.wait_ticks)) break;
+      if (!wg_wait(cnt + tix(k + 1, k, T), (unsigned)(k - kbase(k + 1, g.D)), nullptr, 0, nullptr, 0, err, sh_ok,
+                   g.wait_ticks))
+        break;
       DSTAMP(k, 5);
       {
         d2 v[8];
@@ -1022,7 +1031,8 @@ __device__ bool trsm_task(const PipeArgs& g, int i, int k, double* sm, int* sh_o
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
   unsigned* dg = pan + g.ntile;
-  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)k, nullptr, 0, err, sh_ok, g.wait_ticks)) return false;
+  if (!wg_wait(dg + k, 1u, cnt + tix(i, k, T), (unsigned)(k - kbase(i, g.D)), nullptr, 0, err, sh_ok, g.wait_ticks))
+    return false;
   TSTAMP(tk, 1);
   {
     d2 vx[8], vi[8];
@@ -1049,7 +1059,9 @@ __device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, 
   unsigned* err = g.sync + 1;
   unsigned* cnt = g.sync + 4;
   unsigned* pan = cnt + g.ntile;
-  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)k, err, sh_ok, g.wait_ticks))
+  const int kb = kbase(i, g.D);
+  if (!wg_wait(pan + tix(i, k, T), 1u, pan + tix(j, k, T), 1u, cnt + tix(i, j, T), (unsigned)(k - kb), err, sh_ok,
+               g.wait_ticks))
     return false;
   TSTAMP(tk, 1);
   double a[4][4];
@@ -1082,7 +1094,7 @@ __device__ bool update_task(const PipeArgs& g, int i, int j, int k, double* sm, 
     const double s = gemv_row(sX, su);
     if ((t & 3) == 0) st_sc1(&g.b[i * TB + (t >> 2)], bv - s);
   }
-  wg_publish(cnt + tix(i, j, T), (unsigned)(k + 1));
+  wg_publish(cnt + tix(i, j, T), (unsigned)(k + 1 - kb));
   __syncthreads();   // LDS tiles are rewritten by the next task
   return true;
 }
@@ -1122,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
 
 // Backward substitution L^T x = z across workgroups (one launch): the workgroup holding
 // ticket t owns block column k = T - 1 - t and forms
-//   r_k = z_k - sum_{i > k} L_ik^T x_i,   x_k = Linv_kk^T r_k,
+//   r_k = z_k - sum_{k < i < k + D} L_ik^T x_i,   x_k = Linv_kk^T r_k   (D: the tile band),
 // accumulating L_ik^T x_i as each x_i is published (i descending, the next tile prefetched
 // into registers while it waits), so only the x_{k+1} term and the Linv product follow the
 // hand-off of x_{k+1}.  Tickets make it deadlock-free without co-residency (a column waits only
@@ -1133,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_pipe(PipeArgs g) {
 // the fused one-tile solve.  sync: [0] ticket, [1] error, [4 .. 4+T) column flags.
 __global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const double* __restrict__ Linv,
                                              const double* __restrict__ z, double* x, unsigned* sync,
-                                             int T, int* flag, const int* skip, long long ticks) {
+                                             int T, int D, int* flag, const int* skip, long long ticks) {
   if (skip && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double bsm[];
   double* part = bsm;              // [16][64]
@@ -1158,13 +1170,14 @@ __global__ __launch_bounds__(256) void k_bwd(const double* __restrict__ L, const
   }
   double acc = 0.0;
   double lt[16];
-  if (k + 1 < T) {
-    const double* Lt = L + toff(T - 1, k, T);
+  const int ilast = min(T - 1, k + D - 1);   // L_ik = 0 beyond the band
+  if (k + 1 <= ilast) {
+    const double* Lt = L + toff(ilast, k, T);
 #pragma unroll
     for (int m = 0; m < 16; m++) lt[m] = Lt[(q + 4 * m) * TB + c];
   }
   bool ok = true;
-  for (int i = T - 1; i > k; i--) {
+  for (int i = ilast; i > k; i--) {
     // wait for x_i
     if (t == 0) {
       int good = 1;
@@ -1331,55 +1344,78 @@ constexpr size_t kPanelLds = (4 * (size_t)TB * LS + 2 * TB) * sizeof(double) + 1
 // i = k+2 .. T-1, then the UPDATE tasks (i, j, k) by column j = k+1 .. T-1 and row i = j .. T-1,
 // except (k+1, k+1, k) (the diag workgroup's).  Every task waits only on earlier tickets or on
 // diag steps <= k, which in turn wait only on tasks of steps <= k - 1.
-static std::vector<int4> pipe_tasks(int T) {
-  std::vector<int4> v;
+// Banded (D < T): only tasks inside the band, i - k < D (so j - k < D too): L_ik = 0 beyond it
+// and A_ij receives no product from outside it; the same order otherwise.
+static size_t pipe_task_count(int T, int D) {
+  size_t n = 0;
   for (int k = 0; k + 1 < T; k++) {
-    for (int i = k + 2; i < T; i++) v.push_back(make_int4(0, i, k, k));
-    for (int j = k + 1; j < T; j++)
-      for (int i = j; i < T; i++)
+    const int m = std::min(T - 1, k + D - 1) - k;   // rows k+1 .. k+m in the band
+    n += (size_t)std::max(0, m - 1) + (size_t)m * (m + 1) / 2 - 1;
+  }
+  return n;
+}
+
+static std::vector<int4> pipe_tasks(int T, int D) {
+  std::vector<int4> v;
+  v.reserve(pipe_task_count(T, D));
+  for (int k = 0; k + 1 < T; k++) {
+    const int ie = std::min(T - 1, k + D - 1);
+    for (int i = k + 2; i <= ie; i++) v.push_back(make_int4(0, i, k, k));
+    for (int j = k + 1; j <= ie; j++)
+      for (int i = j; i <= ie; i++)
         if (!(i == k + 1 && j == k + 1)) v.push_back(make_int4(1, i, j, k));
   }
   return v;
 }
 
+bool pipe_supported(int T, int D) {
+  D = pipe_band(T, D);
+  if (T < 2) return false;
+  if (D >= T) return T <= kPipeMaxT;
+  return T <= kPipeMaxTBand && pipe_task_count(T, D) <= kPipeMaxTasks;
+}
+
 static size_t bwd_sync_words(int T) { return (4 + (size_t)T + 3) & ~(size_t)3; }
 
-size_t pipe_sync_words(int T) {
+size_t pipe_sync_words(int T, int D) {
   // factorisation words, then the backward's (ticket, error, column flags); multiple of 16 B
-  const size_t ntile = (size_t)T * (T + 1) / 2;
+  const size_t ntile = band_tiles(pipe_band(T, D), T);
   return ((4 + 2 * ntile + (size_t)T + 3) & ~(size_t)3) + bwd_sync_words(T);
 }
 
 constexpr size_t kBwdLds = (17 * (size_t)TB) * sizeof(double) + 16;
 
-const std::vector<int4>& pipe_tasks_host(int T) {
+const std::vector<int4>& pipe_tasks_host(int T, int D) {
   static std::mutex mu;
-  static std::vector<int4> cache[kPipeMaxT + 1];
-  static bool made[kPipeMaxT + 1] = {};
+  static std::map<std::pair<int, int>, std::vector<int4>> cache;   // node-based: entries never move
+  D = pipe_band(T, D);
   std::lock_guard<std::mutex> g(mu);
-  if (!made[T]) { cache[T] = pipe_tasks(T); made[T] = true; }
-  return cache[T];   // never reallocated afterwards: safe as an async-copy source
+  auto it = cache.find({T, D});
+  if (it == cache.end()) it = cache.emplace(std::make_pair(T, D), pipe_tasks(T, D)).first;
+  return it->second;   // never reallocated afterwards: safe as an async-copy source
 }
 
-hipError_t pipe_prepare(Work& w, int T, hipStream_t st) {
-  if (T < 1 || T > kPipeMaxT) return hipErrorInvalidValue;
-  const std::vector<int4>& tasks = pipe_tasks_host(T);
+hipError_t pipe_prepare(Work& w, int T, hipStream_t st, int D) {
+  if (T < 1 || !(T == 1 || pipe_supported(T, D))) return hipErrorInvalidValue;
+  D = pipe_band(T, D);
+  const std::vector<int4>& tasks = pipe_tasks_host(T, D);
   hipError_t e = hipMalloc(&w.W, tile_doubles(T) * sizeof(double));
   if (e == hipSuccess) e = hipMalloc(&w.du, (size_t)T * 128 * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc(&w.sync, pipe_sync_words(T) * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc(&w.sync, pipe_sync_words(T, D) * sizeof(unsigned));
   if (e == hipSuccess && !tasks.empty()) e = hipMalloc(&w.tasks, tasks.size() * sizeof(int4));
   if (e == hipSuccess && !tasks.empty())
     e = hipMemcpyAsync(w.tasks, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   w.ntasks = (int)tasks.size();
   w.pipe_T = T;
+  w.band = D;
   return e;
 }
 
 void pipe_release(Work& w) {
   for (void* p : {(void*)w.W, (void*)w.du, (void*)w.sync, (void*)w.tasks})
     if (p) (void)hipFree(p);
-  w.W = nullptr; w.du = nullptr; w.sync = nullptr; w.tasks = nullptr; w.ntasks = 0; w.pipe_T = 0;
+  w.W = nullptr; w.du = nullptr; w.sync = nullptr; w.tasks = nullptr; w.ntasks = 0; w.pipe_T = 0; w.band = 0;
 }
 
 static int device_cus() {
@@ -1406,12 +1442,14 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
   if (e == hipSuccess) e = set_lds_limit((const void*)k_backward, 96 * 1024);
   if (e == hipSuccess) e = set_lds_limit((const void*)k_pipe, (int)kPanelLds);
   if (e != hipSuccess) return e;
-  if ((size_t)T * TB * sizeof(double) > 96 * 1024) return hipErrorInvalidValue;
   if (w.sync && w.pipe_T == T) {
-    e = hipMemsetAsync(w.sync, 0, pipe_sync_words(T) * sizeof(unsigned), st);
+    const int D = pipe_band(T, w.band);
+    if (w.per_step && D < T) return hipErrorInvalidValue;   // k_panel walks every tile
+    e = hipMemsetAsync(w.sync, 0, pipe_sync_words(T, D) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     const long long ticks = wait_ticks();
-    PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, T * (T + 1) / 2, flag, skip, ticks};
+    PipeArgs g{A, b, w.L, w.W, w.Linv, w.du, w.z, w.sync, w.tasks, w.ntasks, T, (int)band_tiles(D, T), D, flag, skip,
+               ticks};
     if (w.per_step) {
       for (int k = 0; k < T; k++) {
         const int m = T - 1 - k;
@@ -1423,9 +1461,12 @@ hipError_t solve(double* A, double* b, double* x, int T, const Work& w, int* fla
       hipLaunchKernelGGL(k_pipe, dim3(grid), dim3(256), kPanelLds, st, g);
     }
     hipLaunchKernelGGL(k_bwd, dim3(T), dim3(256), kBwdLds, st, (const double*)w.L, (const double*)w.Linv,
-                       (const double*)w.z, x, w.sync + pipe_sync_words(T) - bwd_sync_words(T), T, flag, skip, ticks);
+                       (const double*)w.z, x, w.sync + pipe_sync_words(T, D) - bwd_sync_words(T), T, D, flag, skip,
+                       ticks);
     return hipGetLastError();
   }
+  // one k_panel launch per step + the one-workgroup backward (its x lives in LDS: <= 192 tiles)
+  if ((size_t)T * TB * sizeof(double) > 96 * 1024) return hipErrorInvalidValue;
   for (int k = 0; k < T; k++) {
     const int m = T - 1 - k;
     const unsigned grid = 1u + (unsigned)(m * (m + 1) / 2);

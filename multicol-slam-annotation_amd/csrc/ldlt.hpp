@@ -48,15 +48,27 @@ struct Work {
   int4* tasks = nullptr;      // task table
   int ntasks = 0;
   int pipe_T = 0;
+  // tile bandwidth of the pipelined factorisation: tiles (I, J) with I - J >= band are zero in A
+  // (and stay zero in L: a banded matrix factors without fill outside its band), so no task
+  // touches them.  0 = dense (band = T).
+  int band = 0;
   bool per_step = false;      // with the pipeline's sync words: one k_panel launch per step
 };
 
-// largest tile count the pipelined path is set up for (task table ~T^3/6 entries)
+// largest tile count of a DENSE pipelined factorisation (task table ~T^3/6 entries); a banded one
+// (band D) has ~T D^2 / 2 tasks and is limited by kPipeMaxTasks / kPipeMaxTBand instead
 constexpr int kPipeMaxT = 96;
-size_t pipe_sync_words(int T);
-hipError_t pipe_prepare(Work& w, int T, hipStream_t st);   // allocates W, du, sync, tasks
-// the task table for T tiles (host copy, cached for the process: a valid async-copy source)
-const std::vector<int4>& pipe_tasks_host(int T);
+constexpr int kPipeMaxTBand = 4096;
+constexpr size_t kPipeMaxTasks = (size_t)1 << 22;
+// the band the pipelined path runs with (D clamped to [2, T]; 0 = dense)
+inline int pipe_band(int T, int D) { return (D <= 0 || D >= T) ? T : (D < 2 ? 2 : D); }
+// whether the pipelined path takes T tiles of band D (task count and tile-count bounds)
+bool pipe_supported(int T, int D);
+size_t pipe_sync_words(int T, int D = 0);
+hipError_t pipe_prepare(Work& w, int T, hipStream_t st, int D = 0);   // allocates W, du, sync, tasks
+// the task table for T tiles of band D (host copy, cached for the process: a valid async-copy
+// source)
+const std::vector<int4>& pipe_tasks_host(int T, int D = 0);
 void pipe_release(Work& w);
 
 // Solve status bits in *flag (device; callers clear it, the kernels only OR bits in):

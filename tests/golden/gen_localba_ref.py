@@ -475,6 +475,11 @@ SCENARIOS = [
     ("s7", dict(n_kf=4, n_points=60, target_edges=360, seed=11), 3, None, None),
     ("s8", dict(n_kf=5, n_points=90, target_edges=520, seed=12, zero_id_kf=0), 4, None, None),
 ]
+# --big: config C (BASELINE configs[2]: 10 MultiKeyframes / ~3k map points / ~20k edges) through
+# the text, with bad points and a bad keyframe among the fixed ones -> localba_ref_big.npz
+SCENARIOS_BIG = [
+    ("C0", dict(n_kf=13, n_points=3000, target_edges=23000, seed=41, bad_kf=(11,), bad_points=0.02), 9, 10, 0),
+]
 
 
 def main():
@@ -482,7 +487,10 @@ def main():
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(HERE, "localba_ref.npz"))
     ap.add_argument("--dump", default=None)
+    ap.add_argument("--big", action="store_true", help="the config-C-size case -> localba_ref_big.npz")
     a = ap.parse_args()
+    if a.big and a.out == os.path.join(HERE, "localba_ref.npz"):
+        a.out = os.path.join(HERE, "localba_ref_big.npz")
     from tests import oracle_bind as ob
     from mcs_amd import ba
     ctx, srcs, n_stmt, enum, std_recon = translate_all(a.ref)
@@ -501,7 +509,7 @@ def main():
     env = build_env(ctx, rt, extra)
     G = safe_exec("\n".join(srcs), env, "<ref:cOptimizer.cpp / cMapPoint.cpp>")
     out = {"n_statements": n_stmt, "std_recon": std_recon}
-    for name, kw, cur, ncov, stop in SCENARIOS:
+    for name, kw, cur, ncov, stop in (SCENARIOS_BIG if a.big else SCENARIOS):
         m = ba.make_map(**kw)
         log.clear()
         rec.clear()

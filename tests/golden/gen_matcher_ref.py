@@ -420,7 +420,11 @@ def main():
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(HERE, "matcher_ref.npz"))
     ap.add_argument("--dump", default=None)
+    ap.add_argument("--big", action="store_true",
+                    help="only the config-B-density triangulation case -> matcher_ref_big.npz")
     a = ap.parse_args()
+    if a.big and a.out == os.path.join(HERE, "matcher_ref.npz"):
+        a.out = os.path.join(HERE, "matcher_ref_big.npz")
     G, R, Matx, rec, n_stmt, histo = load(a.ref)
     if a.dump:
         _, srcs, _, _ = translate_all(a.ref)
@@ -436,7 +440,7 @@ def main():
         return Mo
 
     # ---------------------------------------------------------------- windowed rules
-    for sc, (seed, masked, nbytes) in enumerate([(11, False, 32), (12, True, 32), (13, False, 16)]):
+    for sc, (seed, masked, nbytes) in enumerate([] if a.big else [(11, False, 32), (12, True, 32), (13, False, 16)]):
         rng = np.random.default_rng(seed)
         f1d, f2d = frame_pair(rng, nbytes=nbytes, masked=masked)
         cams = [cam_standin(R, cams_d[c]) for c in range(NC)]
@@ -614,8 +618,19 @@ def main():
         print("windowed scenario %d done (%.1f s)" % (sc, time.time() - t0), flush=True)
 
     # ---------------------------------------------------------------- SearchForTriangulationRaw
-    for sc, (seed, masked, nbytes, nper) in enumerate([(21, False, 32, 250), (22, True, 32, 250),
-                                                        (23, False, 16, 200), (24, False, 64, 200)]):
+    # (seed, masked, bytes, keypoints per camera, clutter): the small scenarios, and with --big the
+    # config-B-density one (3 cameras x 2000 keypoints per keyframe, as the bench's keyframes) with
+    # clutter groups: 150 consecutive KF2 keypoints of one camera near one descriptor, so a query
+    # lists more candidates in one train segment than the device kernel's slots hold (its
+    # overflow / rescan path) and many queries compete for the same KF2 keypoints
+    tri_cases = [(21, False, 32, 250, False), (22, True, 32, 250, False), (23, False, 16, 200, False),
+                 (24, False, 64, 200, False)]
+    if a.big:
+        tri_cases = [None] * 4 + [(25, False, 32, 2000, True)]
+    for sc, case in enumerate(tri_cases):
+        if case is None:
+            continue
+        seed, masked, nbytes, nper, clutter = case
         rng = np.random.default_rng(seed)
         Mcs = [np.concatenate([rng.normal(0, 0.3, 3), rng.normal(0, 0.1, 3)]) for _ in range(NC)]
         Mt1 = np.concatenate([rng.normal(0, 0.1, 3), rng.normal(0, 0.5, 3)])
@@ -640,9 +655,22 @@ def main():
             n = len(rays)
             if kf == 0:
                 base = rng.integers(0, 256, (n, nbytes), dtype=np.uint8)
+                groups = []
+                if clutter:
+                    for c in range(NC):
+                        for g0 in (nper // 5, 3 * nper // 5):
+                            lo = c * nper + g0
+                            proto = rng.integers(0, 256, nbytes, dtype=np.uint8)
+                            for i in range(lo, lo + 150):
+                                base[i] = _flip(proto, int(rng.integers(0, 7)), rng)
+                            groups.append((lo, lo + 150))
                 descs = base.copy()
             else:
-                descs = np.stack([_flip(base[i], int(rng.integers(0, 40)), rng) for i in range(n)])
+                in_group = np.zeros(n, bool)
+                for lo, hi in groups:
+                    in_group[lo:hi] = True
+                descs = np.stack([_flip(base[i], int(rng.integers(0, 11 if in_group[i] else 40)), rng)
+                                  for i in range(n)])
                 dup = rng.choice(n, n // 10, replace=False)
                 descs[dup] = descs[np.roll(dup, 1)]       # near-identical competitors
             dms = np.packbits((rng.random((n, nbytes * 8)) < 0.85).astype(np.uint8), axis=1) if masked else None
@@ -698,6 +726,10 @@ def main():
         out[pre + "m12"] = m12
         out[pre + "nmatches"] = nm
         print("triangulation scenario %d: %d matches (%.1f s)" % (sc, nm, time.time() - t1), flush=True)
+    if a.big:
+        np.savez_compressed(a.out, **out)
+        print("wrote %s (%d statements translated, %.1f s)" % (a.out, n_stmt, time.time() - t0))
+        return
     # ---------------------------------------------------------------- a11: the distances themselves
     rng = np.random.default_rng(31)
     for nb in (16, 32, 64):

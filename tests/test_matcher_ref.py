@@ -238,9 +238,19 @@ def _tri(z, sc):
     return k, np.ascontiguousarray(z[p + "E"]), masked, nb, th_low, z[p + "m12"], int(z[p + "nmatches"])
 
 
-@pytest.mark.parametrize("sc", [0, 1, 2, 3])
+FIX_BIG = os.path.join(os.path.dirname(__file__), "golden", "matcher_ref_big.npz")
+
+
+def _fix_tri(sc):
+    """Scenarios 0-3 from matcher_ref.npz; 4 = config-B density (3 cameras x 2000 keypoints per
+    keyframe, clutter groups that overflow the device kernel's candidate slots) from
+    matcher_ref_big.npz (gen_matcher_ref.py --big)."""
+    return np.load(FIX_BIG, allow_pickle=False) if sc >= 4 else _fix()
+
+
+@pytest.mark.parametrize("sc", [0, 1, 2, 3, 4])
 def test_oracle_triangulation_matches_reference_text(sc):
-    z = _fix()
+    z = _fix_tri(sc)
     k, E, masked, nb, th_low, m12, nm = _tri(z, sc)
     ref = np.zeros(len(k[0]["rays"]), np.int32)
     n = ob.lib().oracle_search_for_triangulation_raw_ex(
@@ -251,10 +261,10 @@ def test_oracle_triangulation_matches_reference_text(sc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sc", [0, 1, 2, 3])
+@pytest.mark.parametrize("sc", [0, 1, 2, 3, 4])
 def test_gpu_triangulation_matches_reference_text(gpu, sc):
     import mcs_amd
-    z = _fix()
+    z = _fix_tri(sc)
     k, E, masked, nb, th_low, m12, nm = _tri(z, sc)
     got = np.zeros(len(k[0]["rays"]), np.int32)
     n = ctypes.c_int32()
@@ -309,5 +319,19 @@ def test_fixture_regenerates_from_reference_text(tmp_path):
     subprocess.check_call([sys.executable, gen, "--out", str(out)], timeout=900)
     q, z = np.load(out), _fix()
     assert sorted(q.files) == sorted(z.keys())
+    for k in q.files:
+        assert np.array_equal(q[k], z[k]), k
+
+
+@pytest.mark.skipif(not (os.path.isdir("/root/reference") and os.environ.get("MCS_REGEN_BIG") == "1"),
+                    reason="needs the reference checkout and MCS_REGEN_BIG=1 (several minutes)")
+def test_big_fixture_regenerates_from_reference_text(tmp_path):
+    import subprocess
+    import sys
+    out = tmp_path / "mb.npz"
+    gen = os.path.join(os.path.dirname(__file__), "golden", "gen_matcher_ref.py")
+    subprocess.check_call([sys.executable, gen, "--big", "--out", str(out)], timeout=3000)
+    q, z = np.load(out), np.load(FIX_BIG, allow_pickle=False)
+    assert sorted(q.files) == sorted(z.files)
     for k in q.files:
         assert np.array_equal(q[k], z[k]), k
