@@ -7,6 +7,7 @@
 // :1326-1335.  Compiled with -ffp-contract=off; the float/double ops below are additionally
 // spelled with _rn intrinsics so no FMA contraction can change a rounding.
 #include "common.hpp"
+#include "desc_math.hpp"
 #include "extractor_kernels.hpp"
 #include <algorithm>
 
@@ -84,6 +85,21 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
   if (x < 0) a = __fsub_rn(180.f, a);
   if (y < 0) a = __fsub_rn(360.f, a);
   return a;
+}
+
+// signed byte B of v as a float: v_cvt_f32_i32 on an SDWA operand (sign-extended byte select)
+template <int B>
+__device__ __forceinline__ float sbyte_f32(uint32_t v) {
+  float f;
+  if constexpr (B == 0)
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(f) : "v"(v));
+  else if constexpr (B == 1)
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(f) : "v"(v));
+  else if constexpr (B == 2)
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(f) : "v"(v));
+  else
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3" : "=v"(f) : "v"(v));
+  return f;
 }
 
 __device__ __forceinline__ int rot_round(double px, double py, double ca, double sa, bool xaxis) {
@@ -287,42 +303,66 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   }
   // ---- rotated BRIEF on the blurred patch
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
-  const double theta = (double)__fmul_rn(angle, DEG2RADf);
-  double ca, sa;
-  sincos(theta, &sa, &ca);
+  const float thf = __fmul_rn(angle, DEG2RADf);  // the reference's angle, (double)(angle * DEG2RADf)
+  // cos / sin: in float (desc_math.hpp, |error| <= kSinCosErr) for the float rotation; in double
+  // only for a wave whose rounds reach the near-half band (formed on first use, ~5% of waves)
+  float saf, caf;
+  sincos_f32(thf, saf, caf);
+  double ca = 0.0, sa = 0.0;
+  bool have_d = false;
   const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
   const uint8_t* bc = &s_blr[slot][21 * kBlrRow + 21 + mis];
   uint32_t w = 0u;   // lane hl keeps test word hl of its half's descriptor
   // The rotated coordinates are cvRound of double products (rot_x / rot_y).  They are first
-  // taken in float: with |x|, |y| <= 15 the float value is within 4e-6 of the double one, so
-  // both round alike unless the float value lies within 1e-5 of a half-integer; a round where
-  // any lane of the wave is that close takes the double form for every lane (rare), so every
-  // offset is the double form's, bit for bit.  (Software-pipelining several pairs per wave
-  // was measured slower: 0.71 -> 0.94-1.13 ms per step, fewer waves per SIMD; cos / sin in
-  // float with the double pair only for the rare exact rounds: 0.72 -> 0.77 ms, also with the
-  // double pair formed lazily inside that branch (OCML sincosf costs about what the double
-  // sincos does); the two points of a test in packed f32: 0.72 -> 0.72 ms.)
-  const float caf = (float)ca, saf = (float)sa;
-  auto near_half = [](float v, float rv) { return fabsf(v - rv) > 0.5f - 1e-5f; };
+  // taken in float, with cos / sin in float (sincos_f32): the float value is within kNearHalf of
+  // the double one (desc_math.hpp), so both round alike unless the float value lies within
+  // kNearHalf of a half-integer; a round where any lane of the wave is that close takes the
+  // double form for every lane (rare; the double cos / sin are formed then), so every offset is
+  // the double form's, bit for bit.  Round 6: the double sincos (~150 VALU per wave) left the
+  // common path, the pattern bytes convert to float with SDWA operands, both points' x and y
+  // rotate as packed pairs, the LDS addresses come out of one packed fma and the near-half
+  // test is branch-free: 36 -> 26 VALU per round.
+  // (Measured slower in round 4/5: software-pipelining several pairs per wave, 0.71 -> 0.94-1.13
+  // ms per step; OCML sincosf in place of the double sincos, 0.72 -> 0.77 ms.)
+  // LDS byte address of the patch centre as a float (exact: < 2^24), so a sample's address is
+  // one fma + one conversion: (ry * row + rx) + centre, all small integers
+  const uint32_t bc_lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)bc;
+  const float bcf = (float)bc_lds;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
   for (int r = 0; r < nw; r++) {
     const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
     const uint32_t pw = s_pat[t];
-    const int ix0 = (int)(int8_t)(pw & 0xFF), iy0 = (int)(int8_t)((pw >> 8) & 0xFF);
-    const int ix1 = (int)(int8_t)((pw >> 16) & 0xFF), iy1 = (int)(int8_t)(pw >> 24);
-    const float fx0 = (float)ix0, fy0 = (float)iy0, fx1 = (float)ix1, fy1 = (float)iy1;
-    const float xa = __builtin_fmaf(fx0, caf, -(fy0 * saf)), ya = __builtin_fmaf(fx0, saf, fy0 * caf);
-    const float xb = __builtin_fmaf(fx1, caf, -(fy1 * saf)), yb = __builtin_fmaf(fx1, saf, fy1 * caf);
-    const float rxa = __builtin_rintf(xa), rya = __builtin_rintf(ya);
-    const float rxb = __builtin_rintf(xb), ryb = __builtin_rintf(yb);
-    int o0 = (int)rya * kBlrRow + (int)rxa;
-    int o1 = (int)ryb * kBlrRow + (int)rxb;
-    const bool close = near_half(xa, rxa) || near_half(ya, rya) || near_half(xb, rxb) || near_half(yb, ryb);
-    if (__ballot(close)) {
-      const double px0 = (double)ix0, py0 = (double)iy0, px1 = (double)ix1, py1 = (double)iy1;
-      o0 = rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa);
-      o1 = rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa);
+    // the four signed pattern bytes straight to float (v_cvt_f32_i32 with a sign-extended byte
+    // operand: one instruction each instead of a bit-field extract and a conversion)
+    const float fx0 = sbyte_f32<0>(pw), fy0 = sbyte_f32<1>(pw), fx1 = sbyte_f32<2>(pw), fy1 = sbyte_f32<3>(pw);
+    // both points' x and both points' y as packed pairs: X = (xa, xb) = fma((x0, x1), c,
+    // (y0, y1) * -s), Y = (ya, yb) = fma((x0, x1), s, (y0, y1) * c) -- per lane the same
+    // roundings as xa = fma(x0, c, -(y0 s)), ya = fma(x0, s, y0 c), in four packed instructions
+    const f32x2 px = {fx0, fx1}, py = {fy0, fy1};
+    const f32x2 X = __builtin_elementwise_fma(px, (f32x2){caf, caf}, py * (f32x2){-saf, -saf});
+    const f32x2 Y = __builtin_elementwise_fma(px, (f32x2){saf, saf}, py * (f32x2){caf, caf});
+    const f32x2 RX = {__builtin_rintf(X.x), __builtin_rintf(X.y)};
+    const f32x2 RY = {__builtin_rintf(Y.x), __builtin_rintf(Y.y)};
+    // LDS addresses (ry * row + rx) + centre of both points, packed, then converted
+    const f32x2 A = __builtin_elementwise_fma(RY, (f32x2){(float)kBlrRow, (float)kBlrRow}, RX + (f32x2){bcf, bcf});
+    uint32_t a0 = (uint32_t)A.x, a1 = (uint32_t)A.y;
+    // the largest distance of the four values from their rounding, branch-free
+    const f32x2 DX = X - RX, DY = Y - RY;
+    const float dm = fmaxf(fmaxf(fabsf(DX.x), fabsf(DX.y)), fmaxf(fabsf(DY.x), fabsf(DY.y)));
+    if (__ballot(dm > 0.5f - kNearHalf)) {
+      if (!have_d) {
+        double th = (double)thf;
+        asm volatile("" : "+v"(th));   // keeps the double sincos in this rare branch (no hoisting)
+        sincos(th, &sa, &ca);
+        have_d = true;
+      }
+      const double px0 = (double)fx0, py0 = (double)fy0, px1 = (double)fx1, py1 = (double)fy1;
+      a0 = bc_lds + (uint32_t)(rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa));
+      a1 = bc_lds + (uint32_t)(rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa));
     }
-    const uint64_t b = __ballot(bc[o0] < bc[o1]);
+    const auto* p0 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a0;
+    const auto* p1 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a1;
+    const uint64_t b = __ballot(*p0 < *p1);
     if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
   }
   if (valid && hl < nw)

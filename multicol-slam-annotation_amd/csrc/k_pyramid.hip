@@ -235,38 +235,49 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
       constexpr bool SSE = decltype(sse_tag)::value;
       int hA[4] = {0, 0, 0, 0}, hB[4] = {0, 0, 0, 0};
       uint32_t xA[4] = {0, 0, 0, 0}, xB[4] = {0, 0, 0, 0};
+      // the scalar-tail form's operands s = h >> 4 (strips holding the tail only), ping-pong too
+      uint32_t uA[4] = {0, 0, 0, 0}, uB[4] = {0, 0, 0, 0};
       int r = r_begin;
       uint32_t tr = row_tab(r);
       auto consume = [&](int sr, const uint32_t (&v)[NDW], int (&hc)[4], uint32_t (&xc)[4],
-                         int (&hp)[4], uint32_t (&xp)[4]) {
+                         uint32_t (&uc)[4], int (&hp)[4], uint32_t (&xp)[4], uint32_t (&up)[4]) {
         stage_and_gather(sr, v, hc);
-        if (SSE) {
 #pragma unroll
-          for (int k = 0; k < 4; k++) xc[k] = (uint32_t)hc[k] & 0x00FFFF00u;   // hc < 2^24
+        for (int k = 0; k < 4; k++) xc[k] = (uint32_t)hc[k] & 0x00FFFF00u;   // hc < 2^24
+        if (!SSE) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) uc[k] = (uint32_t)hc[k] >> 4;
         }
         while (r < r_end && (int)(tr >> 16) == sr) {
           const bool same = (int)(tr & 0xFFFF) == sr;
           const uint32_t bb = row_beta(r);
           int o[4];
-          if (SSE) {
-            // (x0 b0 >> 16) = mulhi_u24(x0 << 8, b0 << 8) (sse_vres8); b in [0, 2048]
-            const uint32_t B0 = (bb & 0xFFFFu) << 8, B1 = (bb >> 16) << 8;
-            // both taps on this source row (the clamped edge rows, rare): the previous set
-            // takes its value (every later output row of this source row is such a row too).
-            // The empty asm keeps this a scalar branch: if-converted, the selects would also
-            // hide the 24-bit operand range (quarter-rate v_mul_hi_u32)
-            if (same) {
-              asm volatile("" ::: "memory");
+          // (x0 b0 >> 16) = mulhi_u24(x0 << 8, b0 << 8) (sse_vres8); b in [0, 2048]
+          const uint32_t B0 = (bb & 0xFFFFu) << 8, B1 = (bb >> 16) << 8;
+          // both taps on this source row (the clamped edge rows, rare): the previous set
+          // takes its value (every later output row of this source row is such a row too).
+          // The empty asm keeps this a scalar branch: if-converted, the selects would also
+          // hide the 24-bit operand range (quarter-rate v_mul_hi_u32)
+          if (same) {
+            asm volatile("" ::: "memory");
 #pragma unroll
-              for (int k = 0; k < 4; k++) xp[k] = xc[k];
-            }
+            for (int k = 0; k < 4; k++) { xp[k] = xc[k]; up[k] = uc[k]; }
+          }
+          if (SSE) {
 #pragma unroll
             for (int k = 0; k < 4; k++) o[k] = (int)sse_vres8(xp[k], xc[k], B0, B1);
           } else {
-            const int b0 = (int)(int16_t)(bb & 0xFFFF), b1 = (int)(int16_t)(bb >> 16);
+            // the strip holding the scalar tail: the SSE2 form as above for pixels below
+            // simd_end, FixedPtCast's (s0 b0 + s1 b1 + 2^21) >> 22 on 24-bit multiply-adds for
+            // the tail (s <= 522240, b0 + b1 = 2048: no overflow, and the result is <= 255, so
+            // vres_fixed's clamp is a no-op), then a per-pixel select (vres, bit for bit)
+            const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-              o[k] = vres((same ? hc[k] : hp[k]) >> 4, hc[k] >> 4, b0, b1, (simd >> k) & 1);
+            for (int k = 0; k < 4; k++) {
+              const uint32_t vs = sse_vres8(xp[k], xc[k], B0, B1);
+              const uint32_t vf = (__umul24(up[k], b0) + (__umul24(uc[k], b1) + (1u << 21))) >> 22;
+              o[k] = (int)(((simd >> k) & 1) ? vs : vf);
+            }
           }
           push_row(r, pack4(o));
           r++;
@@ -280,8 +291,8 @@ __global__ __launch_bounds__(256, MCS_PYR_OCC) void k_pyr_rows(PyrArgs a) {
 #pragma unroll
         for (int u = 0; u < kPF; u++) {
           if (sr + u <= sr1) {
-            if (u & 1) consume(sr + u, pf[u], hB, xB, hA, xA);
-            else consume(sr + u, pf[u], hA, xA, hB, xB);
+            if (u & 1) consume(sr + u, pf[u], hB, xB, uB, hA, xA, uA);
+            else consume(sr + u, pf[u], hA, xA, uA, hB, xB, uB);
             if (sr + u + kPF <= sr1) load_row(sr + u + kPF, pf[u]);
           }
         }
