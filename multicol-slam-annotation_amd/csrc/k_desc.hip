@@ -71,17 +71,14 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x) {
   const float p1 = __fmul_rn(0.9997878412794807f, k), p3 = __fmul_rn(-0.3258083974640975f, k);
   const float p5 = __fmul_rn(0.1555786518463281f, k), p7 = __fmul_rn(-0.04432655554792128f, k);
   const float ax = fabsf(x), ay = fabsf(y);
-  float a, c, c2;
   const float eps = (float)2.220446049250313080847e-16;
-  if (ax >= ay) {
-    c = __fdiv_rn(ay, __fadd_rn(ax, eps));
-    c2 = __fmul_rn(c, c);
-    a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
-  } else {
-    c = __fdiv_rn(ax, __fadd_rn(ay, eps));
-    c2 = __fmul_rn(c, c);
-    a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
-  }
+  // both branches of the reference as one: the operands are selected first, so a wave whose
+  // lanes disagree runs one division instead of two (the same operations on the same values)
+  const bool xs = ax >= ay;
+  const float c = __fdiv_rn(xs ? ay : ax, __fadd_rn(xs ? ax : ay, eps));
+  const float c2 = __fmul_rn(c, c);
+  const float pa = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+  float a = xs ? pa : __fsub_rn(90.f, pa);
   if (x < 0) a = __fsub_rn(180.f, a);
   if (y < 0) a = __fsub_rn(360.f, a);
   return a;
@@ -148,6 +145,17 @@ constexpr int kBlrRow = 48;
 constexpr int kBlrAlign = 3;
 #endif
 
+// sum over each 32-lane half of the wave (exact integers, any order): xor 1 and 2 (quad_perm),
+// the 8- and 16-lane mirrors (DPP, fused into the adds), then lane ^ 16 (ds_swizzle, bit-mask
+// mode); every lane of a half receives its half's sum
+__device__ __forceinline__ int half_sum32(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);   // row_mirror
+  return v + __builtin_amdgcn_ds_swizzle(v, 0x401F);                // swap 16
+}
+
 // IC moments of the raw patch (see c_icw); one half-wave (32 lanes) per keypoint: lane hl
 // holds patch dwords q = hl + 32k in registers (each dword is used by one lane only, so the
 // raw patch needs no LDS), sums reduced within the half (xor offsets < 32 never cross halves)
@@ -167,13 +175,8 @@ __device__ __forceinline__ float ic_angle_regs(const uint32_t (&raw)[10], int hl
       a01 += (uint32_t)(q / kRawW) * d0;
     }
   }
-  int S = (int)aS, m10 = (int)a10, m01 = (int)a01;
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    S += __shfl_xor(S, o, 64);
-    m10 += __shfl_xor(m10, o, 64);
-    m01 += __shfl_xor(m01, o, 64);
-  }
+  const int S = half_sum32((int)aS);
+  int m10 = half_sum32((int)a10), m01 = half_sum32((int)a01);
   m10 -= kHalfPatch * S;
   m01 -= kHalfPatch * S;
   return fast_atan2_dev((float)m01, (float)m10);
@@ -212,22 +215,52 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   int f, item;
   const int pairs = (a.sel_per_frame + 1) / 2;
   if (!xcd_frame_map(blockIdx.x, a.nframes, (pairs + kDescWaves - 1) / kDescWaves, &f, &item)) return;
-  for (int i = threadIdx.x; i < kRawH * kRawW; i += 64 * kDescWaves) {
-    s_icw[0][i] = c_icw[0][i];
-    s_icw[1][i] = c_icw[1][i];
-  }
-  for (int i = threadIdx.x; i < 512; i += 64 * kDescWaves) s_pat[i] = c_pattern_i8[i];
-  __syncthreads();
+  // The tables are staged after this wave's keypoint and patch loads are issued, and one
+  // barrier covers both: a wave waits on two dependent memory round trips (selection entry, then
+  // the patches, with the table loads beside them) instead of three.  A wave without keypoints
+  // stages its share and meets the barrier on its own (wave-uniform branch: every wave reaches
+  // exactly one s_barrier).
+  static_assert(kDescWaves == 4, "table staging assumes 256 threads");
+  const int tid = threadIdx.x;
+  uint32_t tw[6];   // this thread's table words: icw[0][tid (+256)], icw[1][tid (+256)], pat[tid (+256)]
+  auto load_tables = [&]() {
+    const int t2 = min(tid + 256, kRawH * kRawW - 1);
+    tw[0] = c_icw[0][tid]; tw[1] = c_icw[0][t2];
+    tw[2] = c_icw[1][tid]; tw[3] = c_icw[1][t2];
+    tw[4] = c_pattern_i8[tid]; tw[5] = c_pattern_i8[tid + 256];
+  };
+  auto store_tables = [&]() {
+    s_icw[0][tid] = tw[0];
+    s_icw[1][tid] = tw[2];
+    if (tid + 256 < kRawH * kRawW) {
+      s_icw[0][tid + 256] = tw[1];
+      s_icw[1][tid + 256] = tw[3];
+    }
+    s_pat[tid] = tw[4];
+    s_pat[tid + 256] = tw[5];
+  };
+  auto stage_tables = [&]() {
+    load_tables();
+    store_tables();
+  };
   // even j0: both keypoints on one level (every level's sel_off is even, build_plan)
   const int j0 = 2 * (item * kDescWaves + wv);
-  if (j0 >= a.sel_per_frame) return;
+  if (j0 >= a.sel_per_frame) {
+    stage_tables();
+    __syncthreads();
+    return;
+  }
   int l = 0;
   while (l + 1 < a.nlevels && j0 >= a.lv[l + 1].sel_off) l++;
   const LevelPlan& L = a.lv[l];
   const int32_t* scount = a.sel_count + (int64_t)f * a.nlevels;
   const int cnt = scount[l];
   const int i0 = j0 - L.sel_off;
-  if (i0 >= cnt) return;                      // both halves past the level's selection
+  if (i0 >= cnt) {                             // both halves past the level's selection
+    stage_tables();
+    __syncthreads();
+    return;
+  }
   const bool valid = i0 + half < cnt;          // else: recompute keypoint i0, write nothing
   int outIdx = i0 + (valid ? half : 0);
   for (int t = 0; t < l; t++) outIdx += scount[t];
@@ -249,32 +282,50 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   uint32_t raw[10];
   uint32_t rq[10];
   {
-    const uint32_t o0 = (uint32_t)((cy - kHalfPatch) * pitch + (cx - kHalfPatch)) + 4u * (uint32_t)hl;
+    // dword q = hl + 32k of the patch: row r = q / 9 = (57 q) >> 9 (exact for q < 320), byte
+    // offset r (pitch - 36) + 4 q + origin = r (pitch - 36) + (origin & ~3) + 4 hl + 128 k +
+    // (origin & 3): one 24-bit multiply-add per dword (128 k is the load's immediate offset), and
+    // the misalignment origin & 3 is the wave's (every row shares it: pitches are multiples of 4)
+    const uint32_t org = (uint32_t)((cy - kHalfPatch) * pitch + (cx - kHalfPatch));
+    const uint32_t al = org & 3u;
+    const uint32_t ob4 = (org & ~3u) + 4u * (uint32_t)hl;
     const uint32_t pm = (uint32_t)(pitch - 4 * kRawW);
+    const uint32_t h57 = __umul24((uint32_t)hl, 57u);
 #pragma unroll
-    // every load is unconditional (lanes past the patch re-read its last dword / chunk, unused):
-    // a register loaded on one path only would be merged after a wait for all loads in flight
+    // every load is unconditional (lanes past the patch re-read its last dword, unused): a
+    // register loaded on one path only would be merged after a wait for all loads in flight
     for (int k = 0; k < 10; k++) {
-      const uint32_t q = (uint32_t)(hl + 32 * k);
-      rq[k] = (q * 57u) >> 9;
-      const uint32_t qc = min(q, (uint32_t)(kRawH * kRawW - 1));
-      const uint32_t off = ((qc * 57u) >> 9) * pm + o0 + 4u * (qc - (uint32_t)hl);
-      const uint32_t* ap = reinterpret_cast<const uint32_t*>(img + (off & ~3u));
-      raw[k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], off & 3u);
+      uint32_t r, o;
+      if (k < 9) {            // q <= 31 + 256 < 297
+        r = (h57 + 1824u * k) >> 9;
+        o = __umul24(r, pm) + ob4 + 128u * k;
+      } else {                // q = min(hl + 288, 296)
+        const uint32_t hc = min((uint32_t)hl, 8u);
+        r = (__umul24(hc, 57u) + 1824u * k) >> 9;
+        o = __umul24(r, pm) + (org & ~3u) + 4u * (hc + 32u * k);
+      }
+      rq[k] = r;
+      const uint32_t* ap = reinterpret_cast<const uint32_t*>(img + o);
+      raw[k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], al);
     }
-    const uint32_t bo = (uint32_t)((cy - 21) * bp + (cx - 21 - mis));
-    uint4 bv[6];
+    // blurred patch: chunk q = hl + 32k is row q >> 2 = (hl >> 2) + 8k, 16-byte chunk hl & 3
+    const uint32_t bo0 = (uint32_t)((cy - 21) * bp + (cx - 21 - mis));
+    const uint32_t bo = bo0 + (uint32_t)((hl >> 2) * bp + 16 * (hl & 3));
+    const uint32_t rs = (uint32_t)(8 * bp);
+    uint4 bv[5];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {      // chunk q = hl + 32k: row q >> 2, 16-byte chunk q & 3
-      const int qc = min(hl + 32 * k, kBlrH * 4 - 1);
-      bv[k] = *reinterpret_cast<const uint4*>(blr + (bo + (uint32_t)((qc >> 2) * bp + 16 * (qc & 3))));
-    }
+    for (int k = 0; k < 5; k++) bv[k] = *reinterpret_cast<const uint4*>(blr + (bo + rs * k));
+    // the last 12 chunks (rows 40-42); lanes past them re-read chunk 171 (unused)
+    const int q5 = min(hl + 160, kBlrH * 4 - 1);
+    const uint4 b5 = *reinterpret_cast<const uint4*>(blr + (bo0 + (uint32_t)((q5 >> 2) * bp + 16 * (q5 & 3))));
+    load_tables();   // beside the patch loads
     uint8_t* const sb = &s_blr[slot][(hl >> 2) * kBlrRow + 16 * (hl & 3)];
 #pragma unroll
-    for (int k = 0; k < 6; k++)
-      if (hl + 32 * k < kBlrH * 4) *reinterpret_cast<uint4*>(sb + 8 * k * kBlrRow) = bv[k];
+    for (int k = 0; k < 5; k++) *reinterpret_cast<uint4*>(sb + 8 * k * kBlrRow) = bv[k];
+    if (hl < kBlrH * 4 - 160) *reinterpret_cast<uint4*>(sb + 40 * kBlrRow) = b5;
   }
-  dev::wave_sync();
+  store_tables();
+  __syncthreads();
   // ---- IC_Angle: integer moments over the circular r=16 patch (see c_icw; exact integer
   // sums): m10 = sum (u+16) I - 16 S, m01 = sum (v+16) I - 16 S with v + 16 = the row
   float angle;
@@ -287,16 +338,13 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
         a10 = __builtin_amdgcn_udot4(s_icw[0][q], raw[k], a10, false);
         const uint32_t d0 = __builtin_amdgcn_udot4(s_icw[1][q], raw[k], 0u, false);
         aS += d0;
-        a01 += rq[k] * d0;
+        a01 += __umul24(rq[k], d0);   // row < 33, d0 <= 1020
       }
     }
     int S = (int)aS, m10 = (int)a10, m01 = (int)a01;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      S += __shfl_xor(S, o, 64);
-      m10 += __shfl_xor(m10, o, 64);
-      m01 += __shfl_xor(m01, o, 64);
-    }
+    S = half_sum32(S);
+    m10 = half_sum32(m10);
+    m01 = half_sum32(m01);
     m10 -= kHalfPatch * S;
     m01 -= kHalfPatch * S;
     angle = fast_atan2_dev((float)m01, (float)m10);
@@ -308,20 +356,19 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   // only for a wave whose rounds reach the near-half band (formed on first use, ~5% of waves)
   float saf, caf;
   sincos_f32(thf, saf, caf);
-  double ca = 0.0, sa = 0.0;
-  bool have_d = false;
   const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
   const uint8_t* bc = &s_blr[slot][21 * kBlrRow + 21 + mis];
   uint32_t w = 0u;   // lane hl keeps test word hl of its half's descriptor
   // The rotated coordinates are cvRound of double products (rot_x / rot_y).  They are first
   // taken in float, with cos / sin in float (sincos_f32): the float value is within kNearHalf of
   // the double one (desc_math.hpp), so both round alike unless the float value lies within
-  // kNearHalf of a half-integer; a round where any lane of the wave is that close takes the
-  // double form for every lane (rare; the double cos / sin are formed then), so every offset is
-  // the double form's, bit for bit.  Round 6: the double sincos (~150 VALU per wave) left the
-  // common path, the pattern bytes convert to float with SDWA operands, both points' x and y
-  // rotate as packed pairs, the LDS addresses come out of one packed fma and the near-half
-  // test is branch-free: 36 -> 26 VALU per round.
+  // kNearHalf of a half-integer.  A round where any lane of the wave is that close is marked
+  // and taken again after the loop in the double form for every lane (rare; the double cos /
+  // sin are formed only then), so every test word is the double form's, bit for bit.
+  // Round 6: the double sincos (~150 VALU per wave) left the common path, the pattern bytes
+  // convert to float with SDWA operands, both points' x and y rotate as packed pairs, the LDS
+  // addresses come out of one packed fma and the near-half test is branch-free: 36 -> 23 VALU
+  // per round; the double form's constants no longer occupy registers inside the loop.
   // (Measured slower in round 4/5: software-pipelining several pairs per wave, 0.71 -> 0.94-1.13
   // ms per step; OCML sincosf in place of the double sincos, 0.72 -> 0.77 ms.)
   // LDS byte address of the patch centre as a float (exact: < 2^24), so a sample's address is
@@ -329,7 +376,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   const uint32_t bc_lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)bc;
   const float bcf = (float)bc_lds;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-  for (int r = 0; r < nw; r++) {
+  uint32_t redo = 0u;   // wave-uniform: rounds to take again in double
+  auto round = [&](const int r) {
     const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
     const uint32_t pw = s_pat[t];
     // the four signed pattern bytes straight to float (v_cvt_f32_i32 with a sign-extended byte
@@ -345,25 +393,37 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
     const f32x2 RY = {__builtin_rintf(Y.x), __builtin_rintf(Y.y)};
     // LDS addresses (ry * row + rx) + centre of both points, packed, then converted
     const f32x2 A = __builtin_elementwise_fma(RY, (f32x2){(float)kBlrRow, (float)kBlrRow}, RX + (f32x2){bcf, bcf});
-    uint32_t a0 = (uint32_t)A.x, a1 = (uint32_t)A.y;
     // the largest distance of the four values from their rounding, branch-free
     const f32x2 DX = X - RX, DY = Y - RY;
     const float dm = fmaxf(fmaxf(fabsf(DX.x), fabsf(DX.y)), fmaxf(fabsf(DY.x), fabsf(DY.y)));
-    if (__ballot(dm > 0.5f - kNearHalf)) {
-      if (!have_d) {
-        double th = (double)thf;
-        asm volatile("" : "+v"(th));   // keeps the double sincos in this rare branch (no hoisting)
-        sincos(th, &sa, &ca);
-        have_d = true;
-      }
-      const double px0 = (double)fx0, py0 = (double)fy0, px1 = (double)fx1, py1 = (double)fy1;
-      a0 = bc_lds + (uint32_t)(rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa));
-      a1 = bc_lds + (uint32_t)(rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa));
-    }
-    const auto* p0 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a0;
-    const auto* p1 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a1;
+    if (__ballot(dm > 0.5f - kNearHalf)) redo |= 1u << r;
+    const auto* p0 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(uint32_t)A.x;
+    const auto* p1 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)(uint32_t)A.y;
     const uint64_t b = __ballot(*p0 < *p1);
     if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
+  };
+  // nw is 4, 8 or 16: rounds in pairs (the convergent ballots keep the compiler from unrolling a
+  // loop of unknown count), so the next round's pattern read is in flight
+  for (int r = 0; r < nw; r += 2) {
+    round(r);
+    round(r + 1);
+  }
+  if (redo) {
+    double sa, ca;
+    sincos((double)thf, &sa, &ca);
+    do {
+      const int r = __builtin_ctz(redo);
+      redo &= redo - 1u;
+      const uint32_t pw = s_pat[r * 32 + hl];
+      const double px0 = (double)sbyte_f32<0>(pw), py0 = (double)sbyte_f32<1>(pw);
+      const double px1 = (double)sbyte_f32<2>(pw), py1 = (double)sbyte_f32<3>(pw);
+      const uint32_t a0 = bc_lds + (uint32_t)(rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa));
+      const uint32_t a1 = bc_lds + (uint32_t)(rot_y(px1, py1, ca, sa) * kBlrRow + rot_x(px1, py1, ca, sa));
+      const auto* p0 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a0;
+      const auto* p1 = (const __attribute__((address_space(3))) uint8_t*)(uintptr_t)a1;
+      const uint64_t b = __ballot(*p0 < *p1);
+      if (hl == r) w = half ? (uint32_t)(b >> 32) : (uint32_t)b;
+    } while (redo);
   }
   if (valid && hl < nw)
     reinterpret_cast<uint32_t*>(a.desc + ((int64_t)f * a.cap + outIdx) * a.desc_size)[hl] = w;

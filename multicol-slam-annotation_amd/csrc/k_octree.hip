@@ -28,8 +28,12 @@ __device__ __forceinline__ int oct_quad(uint32_t pk, int midx, int midy) {
 template <int MAXL, int CAP>
 __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   constexpr int kOctPer = MAXL / kOctThreads;  // nodes per thread in node scans
-  int f, l;
-  if (!xcd_frame_map(blockIdx.x, a.nframes, a.nlevels, &f, &l)) return;
+  // level-major dispatch: every frame's level-0 list (the longest: most candidates, most
+  // nodes, most rounds) is issued before any level-1 list, and so on, so the short upper-level
+  // lists fill the tail instead of a few level-0 lists running alone at the end
+  const int xb = blockIdx.x & 7, kb = blockIdx.x >> 3, fg = (a.nframes + 7) >> 3;
+  const int l = kb / fg, f = xb + 8 * (kb - l * fg);
+  if (f >= a.nframes) return;
   const int tid = threadIdx.x;
   const LevelPlan& L = a.lv[l];
   // LDS is what limits residency (workgroups per CU) of this latency-bound kernel, so the

@@ -21,7 +21,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_AC
 A=$(find $O/sqa -name '*counter_collection.csv' | head -1)
 B=$(find $O/sqb -name '*counter_collection.csv' | head -1)
 python3 tools/sq_summary.py "$A" > $O/sq_summary.txt
-python3 tools/valu_per_pixel.py "$A" 513 > $O/valu_per_pixel.json
+python3 tools/valu_per_pixel.py "$A" 256.5 > $O/valu_per_pixel.json   # the step runs as two halves
 python3 tools/sq_summary.py --all --json=$O/sq_issue.json "$B" > $O/sq_summary_b.txt
 head -14 $O/kernel_stats.csv | cut -d, -f1-4 | cut -c1-120
 python3 -c "import json; d=json.load(open('$O/pmc_traffic.json')); print({k: v for k, v in d.items() if k != 'kernels'})"

@@ -27,7 +27,7 @@ def level_px(W, H, n, scale=1.2):
 
 
 def main():
-    path, frames = sys.argv[1], int(sys.argv[2])
+    path, frames = sys.argv[1], float(sys.argv[2])   # per dispatch group (a split step: 513 / 2)
     W, H, nl = (int(v) for v in sys.argv[3:6]) if len(sys.argv) >= 6 else (754, 480, 8)
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
