@@ -37,16 +37,23 @@ struct PyrArgs {
   int core, seg_rows;              // strip width (px, multiple of 4, <= 244), segment height
 };
 // strips of <= 244 columns (61 lanes x 4 px, so a level-0 strip + halo is <= 64 dwords);
-// segment height chosen so that a batch of F
-// frames gives ~16k waves (latency hiding), between 8 and 64 rows
+// segment height chosen for ~32 waves per frame, at least 8k waves per launch (latency hiding
+// for small batches), between 8 and 64 rows.  Per frame that is a fixed geometry, so the
+// production step's two halves on two streams (bench.py --split 2: two launches of ~256 frames
+// side by side) cut their segments as tall as one launch of the whole batch; a fixed 16k-wave
+// target had halved the segments of a half (more halo rows per output row).  Round 6:
+// 399 -> 410 M keypoints/s.
 inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
   const int n = (dw + 243) / 244;
   a.core = ((dw + n - 1) / n + 3) & ~3;
   a.tiles_x = (dw + a.core - 1) / a.core;
 #ifndef MCS_PYR_TARGET
-#define MCS_PYR_TARGET 16384
+#define MCS_PYR_TARGET 8192
 #endif
-  const long target = MCS_PYR_TARGET;
+#ifndef MCS_PYR_WAVES_PER_FRAME
+#define MCS_PYR_WAVES_PER_FRAME 32
+#endif
+  const long target = std::max<long>(MCS_PYR_TARGET, (long)MCS_PYR_WAVES_PER_FRAME * (F > 0 ? F : 1));
   const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
   const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
   int rows = (dh + segs - 1) / segs;
