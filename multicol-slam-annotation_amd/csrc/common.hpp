@@ -60,13 +60,20 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// inclusive prefix sum over the 64 lanes on DPP (integer adds: any order is exact): within each
+// row of 16 the sums of the 1, 2, 3 lanes below, then 4 back (banks 1-3) and 8 back (banks 2-3);
+// then row 15's total into rows 1 and 3 (row_bcast:15) and lane 31's into rows 2 and 3
+// (row_bcast:31).  Seven DPP adds instead of six ds_bpermute round trips with their address
+// arithmetic.  Disabled rows / banks and out-of-row sources contribute the 0 of update_dpp.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int t = __shfl_up(v, o, 64);
-    if (lane_id() >= o) v += t;
-  }
-  return v;
+  int x = v + __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);          // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xF, 0xF, true);          // row_shr:3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xE, true);          // row_shr:4, banks 1-3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xC, true);          // row_shr:8, banks 2-3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);         // row_bcast:15, rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);         // row_bcast:31, rows 2, 3
+  return x;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -98,6 +105,31 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
   *total = s_tmp[NT / 64];
   __syncthreads();
   return r;
+}
+
+// The same with one barrier: the wave totals alternate between two halves of s_tmp2 (2 NT/64
+// ints; `parity` is a per-thread counter every thread of the block advances alike), so a scan's
+// writes never meet the previous scan's reads (those precede the previous scan's barrier in
+// program order) and the two trailing barriers of block_excl_scan go.  Callers that relied on
+// a scan as a block-wide barrier for their own data must not use this form.
+template <int NT>
+__device__ __forceinline__ int block_excl_scan1(int v, int* s_tmp2, int& parity, int* total) {
+  constexpr int NW = NT / 64;
+  const int w = threadIdx.x >> 6, l = lane_id();
+  const int inc = wave_incl_scan(v);
+  int* const t = s_tmp2 + parity * NW;
+  parity ^= 1;
+  if (l == 63) t[w] = inc;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) {
+    const int x = t[i];
+    pre += (i < w) ? x : 0;
+    tot += x;
+  }
+  *total = tot;
+  return pre + inc - v;
 }
 
 }  // namespace dev

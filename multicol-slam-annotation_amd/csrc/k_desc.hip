@@ -129,21 +129,20 @@ __device__ __forceinline__ uint32_t load_aligned_dword(const uint8_t* g) {
   return __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)((uintptr_t)g & 3));
 }
 
-// Blurred patch (+-21 around the keypoint) staged in LDS rows of kBlrRow bytes.
-// Default: 16-byte loads (blurred levels have a 64-byte-aligned pitch, so every row shares
-// mis = (cx - 21) & 15 and 4 aligned 16-byte chunks cover a row: 64-byte LDS rows).
-// MCS_DESC_BLR48 (tuning variant, measured slower: 1.11 vs 0.89 ms/step): 12 aligned dwords
-// per row into 48-byte LDS rows, less LDS per keypoint but three times the load count.
-#ifndef MCS_DESC_BLR48
-#ifndef MCS_DESC_BLR_PITCH
-#define MCS_DESC_BLR_PITCH 64
-#endif
-constexpr int kBlrRow = MCS_DESC_BLR_PITCH;
-constexpr int kBlrAlign = 15;
+// Blurred patch (+-21 around the keypoint) staged in LDS rows of kBlrRow bytes, one 16-byte
+// chunk per load.  Default (round 6): the chunks start at the dword below the patch (mis =
+// (cx - 21) & 3; global loads need dword alignment only), so 3 chunks cover a row's 43 + 3
+// bytes: 48-byte LDS rows, 129 chunks per keypoint (5 loads per lane), 2064 B per keypoint.
+// MCS_DESC_ROW64 (the round-2..5 layout): 16-byte aligned chunks (mis = (cx - 21) & 15), 4
+// per row, 64-byte rows, 172 chunks (6 loads per lane), 2752 B per keypoint.  A/B in round 6:
+// 0.575 (48-byte rows: 20.9 KB per workgroup, 7 per CU) against 0.577 ms (26.4 KB, 6 per CU).
+// (Measured slower in round 2: 12 dword loads per 48-byte row, 1.11 vs 0.89 ms.)
+#ifdef MCS_DESC_ROW64
+constexpr int kBlrRow = 64, kBlrAlign = 15;
 #else
-constexpr int kBlrRow = 48;
-constexpr int kBlrAlign = 3;
+constexpr int kBlrRow = 48, kBlrAlign = 3;
 #endif
+constexpr int kBlrChunks = kBlrRow / 16;   // 16-byte chunks per row
 
 // sum over each 32-lane half of the wave (exact integers, any order): xor 1 and 2 (quad_perm),
 // the 8- and 16-lane mirrors (DPP, fused into the adds), then lane ^ 16 (ds_swizzle, bit-mask
@@ -308,21 +307,33 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
       const uint32_t* ap = reinterpret_cast<const uint32_t*>(img + o);
       raw[k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], al);
     }
-    // blurred patch: chunk q = hl + 32k is row q >> 2 = (hl >> 2) + 8k, 16-byte chunk hl & 3
+    // blurred patch: chunk q = hl + 32k is row q / kBlrChunks, chunk q % kBlrChunks, at byte
+    // q (16 rows-worth) of the wave's LDS patch (rows of kBlrChunks chunks: LDS offset 16 q) and
+    // at r (bp - kBlrRow) + 16 q + origin in the level (r = q / 3 = (171 q) >> 9, exact for
+    // q < 512)
+    constexpr int NQ = kBlrH * kBlrChunks;              // 129 (172)
+    constexpr int NK = NQ / 32;                         // full loads per lane: 4 (5)
     const uint32_t bo0 = (uint32_t)((cy - 21) * bp + (cx - 21 - mis));
-    const uint32_t bo = bo0 + (uint32_t)((hl >> 2) * bp + 16 * (hl & 3));
-    const uint32_t rs = (uint32_t)(8 * bp);
-    uint4 bv[5];
+    const uint32_t bpm = (uint32_t)(bp - kBlrRow);
+    const uint32_t bl = bo0 + 16u * (uint32_t)hl;
+    auto chunk_row = [&](uint32_t q) -> uint32_t {
+      return kBlrChunks == 4 ? (q >> 2) : ((q * 171u) >> 9);
+    };
+    const uint32_t h171 = __umul24((uint32_t)hl, 171u);
+    u32x4a bv[NK];
 #pragma unroll
-    for (int k = 0; k < 5; k++) bv[k] = *reinterpret_cast<const uint4*>(blr + (bo + rs * k));
-    // the last 12 chunks (rows 40-42); lanes past them re-read chunk 171 (unused)
-    const int q5 = min(hl + 160, kBlrH * 4 - 1);
-    const uint4 b5 = *reinterpret_cast<const uint4*>(blr + (bo0 + (uint32_t)((q5 >> 2) * bp + 16 * (q5 & 3))));
+    for (int k = 0; k < NK; k++) {
+      const uint32_t r = kBlrChunks == 4 ? (((uint32_t)hl >> 2) + 8u * k) : ((h171 + 5472u * k) >> 9);
+      bv[k] = *reinterpret_cast<const u32x4a*>(blr + (__umul24(r, bpm) + bl + 512u * k));
+    }
+    // the last NQ - 32 NK chunks; lanes past them re-read the last chunk (unused)
+    const uint32_t qt = min((uint32_t)hl + 32u * NK, (uint32_t)NQ - 1u);
+    const u32x4a bt = *reinterpret_cast<const u32x4a*>(blr + (__umul24(chunk_row(qt), bpm) + bo0 + 16u * qt));
     load_tables();   // beside the patch loads
-    uint8_t* const sb = &s_blr[slot][(hl >> 2) * kBlrRow + 16 * (hl & 3)];
+    uint8_t* const sb = &s_blr[slot][16 * hl];
 #pragma unroll
-    for (int k = 0; k < 5; k++) *reinterpret_cast<uint4*>(sb + 8 * k * kBlrRow) = bv[k];
-    if (hl < kBlrH * 4 - 160) *reinterpret_cast<uint4*>(sb + 40 * kBlrRow) = b5;
+    for (int k = 0; k < NK; k++) *reinterpret_cast<u32x4a*>(sb + 512 * k) = bv[k];
+    if (hl < NQ - 32 * NK) *reinterpret_cast<u32x4a*>(sb + 512 * NK) = bt;
   }
   store_tables();
   __syncthreads();
@@ -377,9 +388,10 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   const float bcf = (float)bc_lds;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   uint32_t redo = 0u;   // wave-uniform: rounds to take again in double
-  auto round = [&](const int r) {
-    const int t = r * 32 + hl;  // test t: byte t/8, bit t%8
-    const uint32_t pw = s_pat[t];
+  // (Measured slower in round 6: the pattern words from global memory, a pair of rounds ahead,
+  // without s_pat: 18.9 KB and 60 VGPRs allow 8 waves per SIMD, but 0.575 -> 0.61 ms.)
+  auto patw = [&](int r) -> uint32_t { return s_pat[r * 32 + hl]; };
+  auto round = [&](const int r, const uint32_t pw) {
     // the four signed pattern bytes straight to float (v_cvt_f32_i32 with a sign-extended byte
     // operand: one instruction each instead of a bit-field extract and a conversion)
     const float fx0 = sbyte_f32<0>(pw), fy0 = sbyte_f32<1>(pw), fx1 = sbyte_f32<2>(pw), fy1 = sbyte_f32<3>(pw);
@@ -405,8 +417,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   // nw is 4, 8 or 16: rounds in pairs (the convergent ballots keep the compiler from unrolling a
   // loop of unknown count), so the next round's pattern read is in flight
   for (int r = 0; r < nw; r += 2) {
-    round(r);
-    round(r + 1);
+    round(r, patw(r));
+    round(r + 1, patw(r + 1));
   }
   if (redo) {
     double sa, ca;
@@ -414,7 +426,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
     do {
       const int r = __builtin_ctz(redo);
       redo &= redo - 1u;
-      const uint32_t pw = s_pat[r * 32 + hl];
+      const uint32_t pw = patw(r);
       const double px0 = (double)sbyte_f32<0>(pw), py0 = (double)sbyte_f32<1>(pw);
       const double px1 = (double)sbyte_f32<2>(pw), py1 = (double)sbyte_f32<3>(pw);
       const uint32_t a0 = bc_lds + (uint32_t)(rot_y(px0, py0, ca, sa) * kBlrRow + rot_x(px0, py0, ca, sa));

@@ -298,16 +298,13 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
                          : PAT != 16 ? detm
                                      : ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
                                          ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm);
-      // compaction: the lane's survivor count c (0..4) as three ballots of its bits gives the
-      // lane's exclusive prefix by mbcnt; the four entries are written unconditionally, those
-      // of non-survivors to a dummy slot
-      const uint32_t c = (uint32_t)__builtin_popcount(s);
-      const uint64_t q0 = __ballot(c & 1u), q1 = __ballot(c & 2u), q2 = __ballot(c & 4u);
-      auto mbcnt = [](uint64_t m) {
-        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      };
-      const int pos0 = ncarry + ns + mbcnt(q0) + 2 * mbcnt(q1) + 4 * mbcnt(q2);
-      ns += __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
+      // compaction: the lane's exclusive prefix of the survivor counts c (0..4) by a DPP scan
+      // (dev::wave_incl_scan; round 5 took three ballots of c's bits and six mbcnt); the four
+      // entries are written unconditionally, those of non-survivors to a dummy slot
+      const int c = __builtin_popcount(s);
+      const int inc = dev::wave_incl_scan(c);
+      const int pos0 = ncarry + ns + inc - c;
+      ns += __builtin_amdgcn_readlane(inc, 63);
       const int k0 = (s >> 7) & 1, k1 = (s >> 15) & 1, k2 = (s >> 23) & 1, k3 = s >> 31;
       const int pos1 = pos0 + k0, pos2 = pos1 + k1, pos3 = pos2 + k2;
       const int idx = (y << 8) | (4 * lane);

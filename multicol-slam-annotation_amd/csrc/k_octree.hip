@@ -40,7 +40,8 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
   // tables are sized to their value ranges: positions < MAXL fit int16, flags are 0/1/2;
   // counts stay int (a node may hold tens of thousands of candidates on noise images).
   __shared__ __attribute__((aligned(8))) int s_pref[2 * MAXL];  // cell prefix (<= 2*MAXL cells, launch_octree); then u64 sort keys
-  __shared__ int s_scan[kOctThreads / 64 + 1];
+  __shared__ int s_scan[2 * (kOctThreads / 64)];   // double-buffered wave totals (block_excl_scan1)
+  int scan_par = 0;
   __shared__ int16_t nx0[2][MAXL], ny0[2][MAXL], nx1[2][MAXL], ny1[2][MAXL];
   __shared__ int ncnt[2][MAXL], nseq[2][MAXL];
   __shared__ int ccnt[MAXL * 4];      // child counts; reused for best keys
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
     const int v = i < nc ? counts[i] : 0;
     if (i < nc) ccnt[i] = a.cells[L.cell_begin + i].slot_off;
     int tot;
-    const int ex = dev::block_excl_scan<kOctThreads>(v, s_scan, &tot);
+    const int ex = dev::block_excl_scan1<kOctThreads>(v, s_scan, scan_par, &tot);
     if (i < nc) s_pref[i] = n + ex;
     n += tot;
   }
@@ -195,13 +196,13 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
       // a round builds, P + K, stays <= N <= MAXL, and E2 <= P), so no field carries into the
       // next (3 barriers and one wave scan instead of three of each)
       int T3;
-      const int ex = dev::block_excl_scan<kOctThreads>(pushes | (kept << 10) | (expandKids << 20), s_scan, &T3);
+      const int ex = dev::block_excl_scan1<kOctThreads>(pushes | (kept << 10) | (expandKids << 20), s_scan, scan_par, &T3);
       pushBase = ex & 0x3FF; keptBase = (ex >> 10) & 0x3FF;
       P = T3 & 0x3FF; K = (T3 >> 10) & 0x3FF; E2 = (T3 >> 20) & 0x3FF;
     } else {
-      pushBase = dev::block_excl_scan<kOctThreads>(pushes, s_scan, &P);
-      keptBase = dev::block_excl_scan<kOctThreads>(kept, s_scan, &K);
-      dev::block_excl_scan<kOctThreads>(expandKids, s_scan, &E2);
+      pushBase = dev::block_excl_scan1<kOctThreads>(pushes, s_scan, scan_par, &P);
+      keptBase = dev::block_excl_scan1<kOctThreads>(kept, s_scan, scan_par, &K);
+      dev::block_excl_scan1<kOctThreads>(expandKids, s_scan, scan_par, &E2);
     }
     {
       int s = pushBase, kp = keptBase;
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
         if (i < Lsz) inE += (nseq[cur][i] >= roundBase && ncnt[cur][i] > 1);
       }
       int M;
-      int eb = dev::block_excl_scan<kOctThreads>(inE, s_scan, &M);
+      int eb = dev::block_excl_scan1<kOctThreads>(inE, s_scan, scan_par, &M);
       int M2 = 1;
       while (M2 < M) M2 <<= 1;
       for (int j = 0; j < kOctPer; j++) {
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
         dsum += dl[jj];
       }
       int Dtot;
-      int dpre = dev::block_excl_scan<kOctThreads>(dsum, s_scan, &Dtot);
+      int dpre = dev::block_excl_scan1<kOctThreads>(dsum, s_scan, scan_par, &Dtot);
       // first j with Lsz + inclusive(delta) >= N -> processed = j+1
       if (tid == 0) s_var[1] = M;
       __syncthreads();
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
           if (i < Lsz && nflag[i] != 2) kept++;
         }
         int T2;
-        const int ex = dev::block_excl_scan<kOctThreads>(mykids | (kept << 10), s_scan, &T2);
+        const int ex = dev::block_excl_scan1<kOctThreads>(mykids | (kept << 10), s_scan, scan_par, &T2);
         kbase = ex & 0x3FF; kb = ex >> 10;
         Pn = T2 & 0x3FF; Kn = T2 >> 10;
       } else {
@@ -412,7 +413,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
         int mykids = 0;
         for (int jj = 0; jj < kOctPer; jj++)
           if (j0 + jj < Mp) mykids += kl[jj];
-        kbase = dev::block_excl_scan<kOctThreads>(mykids, s_scan, &Pn);
+        kbase = dev::block_excl_scan1<kOctThreads>(mykids, s_scan, scan_par, &Pn);
         for (int jj = 0; jj < kOctPer; jj++) {
           const int j = j0 + jj;
           if (j >= Mp) break;
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(OctArgs a) {
           const int i = i0 + j;
           if (i < Lsz && nflag[i] != 2) kept++;
         }
-        kb = dev::block_excl_scan<kOctThreads>(kept, s_scan, &Kn);
+        kb = dev::block_excl_scan1<kOctThreads>(kept, s_scan, scan_par, &Kn);
       }
       // place the processed nodes' children (sorted order, n1..n4) and the kept nodes after them
       {

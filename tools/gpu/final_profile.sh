@@ -15,7 +15,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py $ARGS > /dev/null 2> $O/write.err || { echo "write pass failed"; tail -5 $O/write.err; exit 1; }
 F=$(find $O/fetch -name '*counter_collection.csv' | head -1)
 W=$(find $O/write -name '*counter_collection.csv' | head -1)
-python3 tools/pmc_traffic.py "$F" "$W" $O/pmc_traffic.json > /dev/null || { echo "traffic summary failed"; exit 1; }
+python3 tools/pmc_traffic.py "$F" "$W" $O/pmc_traffic.json 2 > /dev/null || { echo "traffic summary failed"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $O/sqa -o run -- python3 bench.py $ARGS --stage-timing 0 > /dev/null 2> $O/sqa.err || { echo "sq pass A failed"; tail -5 $O/sqa.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LEVEL_WAVES SQ_INST_CYCLES_SALU --output-format csv -d $O/sqb -o run -- python3 bench.py $ARGS --stage-timing 0 > /dev/null 2> $O/sqb.err || { echo "sq pass B failed"; tail -5 $O/sqb.err; exit 1; }
 A=$(find $O/sqa -name '*counter_collection.csv' | head -1)

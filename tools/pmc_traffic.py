@@ -8,7 +8,8 @@ read bytes are 2 * FETCH_SIZE * 1024; for other access widths the factor is unca
 so both the raw and the x2-corrected figures are recorded.  WRITE_SIZE * 1024 is exact for
 16 B/lane stores.
 
-usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json> [extractor calls per step]
+(bench.py runs a step as two extractor calls, one per half of its multi-frames: pass 2)
 """
 import csv
 import json
@@ -31,7 +32,8 @@ def short(name):
     return name.split("(")[0].replace("void ", "").replace("mcs::", "")
 
 
-def main(fetch_csv, write_csv, out_json):
+def main(fetch_csv, write_csv, out_json, per_step="1"):
+    per_step = int(per_step)
     fe = load(fetch_csv, "FETCH_SIZE")
     wr = load(write_csv, "WRITE_SIZE")
     out = {"note": "bytes per launch; fetch_raw = FETCH_SIZE*1024, fetch_x2 = gfx950 wide-read "
@@ -52,10 +54,11 @@ def main(fetch_csv, write_csv, out_json):
     fa = next((v for n, v in k.items() if n.startswith("k_fast_rows") or n.startswith("k_fast_cells")), None)
     rs = [v for n, v in k.items() if n.startswith("k_pyr_rows<true")]
     if rs and fa and fa["launches"]:
-        calls = fa["launches"]
-        rd = sum(v["fetch_raw"] * v["launches"] for v in rs) / calls + fa["fetch_raw"]
-        rd2 = sum(v["fetch_x2"] * v["launches"] for v in rs) / calls + fa["fetch_x2"]
-        wt = sum((v["write"] or 0) * v["launches"] for v in rs) / calls + (fa["write"] or 0)
+        calls = fa["launches"] / per_step   # bench steps (a "call" below is one step)
+        out["extractor_calls_per_step"] = per_step
+        rd = sum(v["fetch_raw"] * v["launches"] for v in rs) / calls + fa["fetch_raw"] * per_step
+        rd2 = sum(v["fetch_x2"] * v["launches"] for v in rs) / calls + fa["fetch_x2"] * per_step
+        wt = sum((v["write"] or 0) * v["launches"] for v in rs) / calls + (fa["write"] or 0) * per_step
         out["pyr_launches_per_call"] = sum(v["launches"] for v in rs) / calls
         out["pyramid+fast_raw_bytes_per_call"] = rd + wt
         out["pyramid+fast_fetch_raw_per_call"] = rd
@@ -68,4 +71,4 @@ def main(fetch_csv, write_csv, out_json):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
