@@ -164,7 +164,9 @@ __device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double
   double dn = readlane_d(a[0], P), c1 = readlane_d(a[0], P + 1);
   double r = __builtin_amdgcn_rcp(dn);
   r = __builtin_fma(r, __builtin_fma(-dn, r, 1.0), r);
+#ifndef MCS_LDLT_NEWTON1
   r = __builtin_fma(r, __builtin_fma(-dn, r, 1.0), r);
+#endif
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const int J = P + j;
@@ -210,6 +212,7 @@ __device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double
     rn = __builtin_fma(rn, e, rn);
     __builtin_amdgcn_sched_barrier(0);
     panel_bulk(a, cm, lj, j + 8, j + 9);
+#ifndef MCS_LDLT_NEWTON1
     __builtin_amdgcn_sched_barrier(0);
     e = __builtin_fma(-dn, rn, 1.0);
     __builtin_amdgcn_sched_barrier(0);
@@ -218,6 +221,9 @@ __device__ __forceinline__ void panel_elim(double* sA, double* sx, int P, double
     rn = __builtin_fma(rn, e, rn);
     __builtin_amdgcn_sched_barrier(0);
     panel_bulk(a, cm, lj, j + 10, 16);
+#else
+    panel_bulk(a, cm, lj, j + 9, 16);
+#endif
     r = rn;
     c1 = c1n;
   }
