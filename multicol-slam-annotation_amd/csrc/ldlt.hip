@@ -764,7 +764,8 @@ __device__ __forceinline__ void store_tile_sc1(double* g, const double* s) {
 // first row.  So the consumer reads the handed-off bytes with sc1 loads (16-B buffer loads for
 // tiles, 8-B global loads for words) and skips the agent acquire after each wait (an L2
 // invalidate on the diagonal chain twice per step).  Config E (n = 1194, 19 tile steps): solve
-// 0.395 -> 0.390 ms per trial, parity tests green (tools/gpu/host_threads_ab.sh, round 5).
+// 0.395 -> 0.390 ms per trial, parity tests green on both forms (round 5,
+// profiles/r05_c_gba_host_ab.txt).
 // MCS_PIPE_ACQUIRE builds the acquire form.
 #ifdef MCS_PIPE_ACQUIRE
 constexpr bool kSc1Consume = false;
