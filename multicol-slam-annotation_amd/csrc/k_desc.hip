@@ -207,7 +207,6 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   __shared__ uint32_t s_icw[2][kRawH * kRawW];
   __shared__ uint32_t s_pat[512];
   typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
-  typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
   // wave index as a scalar: the pair, its level and counts are wave-uniform
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int half = lane >> 5, hl = lane & 31, slot = 2 * wv + half;
@@ -273,10 +272,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
       (l == 0) ? a.img0 + (int64_t)f * a.img0_fstride : a.pyr + (int64_t)f * a.pyr_fstride + L.pyr_off);
   const uint8_t* const blr = dev::uniform_ptr(a.blur + (int64_t)f * a.blur_fstride + L.img_off);
   // ---- raw patch: dword q = hl + 32k (row q / 9, column q % 9) of the 33 x 9 dwords per
-  // lane, consecutive lanes on consecutive dwords (coalesced); blurred patch into LDS
-  // (independent loads, issued together).  Offsets are 32-bit from the uniform bases: with
-  // r = q / 9 = (57 q) >> 9 (exact for q < 320), the dword's byte offset is
-  // r (pitch - 36) + 4 q + the patch origin.
+  // lane, consecutive lanes on consecutive dwords (coalesced), kept in registers; blurred patch
+  // into LDS (independent loads, issued together), 32-bit offsets from the uniform bases
   const int mis = (cx - 21) & kBlrAlign;
   uint32_t raw[10];
   uint32_t rq[10];
@@ -364,7 +361,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   const float DEG2RADf = (float)3.14159265358979323846 / 180.f;
   const float thf = __fmul_rn(angle, DEG2RADf);  // the reference's angle, (double)(angle * DEG2RADf)
   // cos / sin: in float (desc_math.hpp, |error| <= kSinCosErr) for the float rotation; in double
-  // only for a wave whose rounds reach the near-half band (formed on first use, ~5% of waves)
+  // only for a wave whose rounds reach the near-half band (after the rounds, see `redo`)
   float saf, caf;
   sincos_f32(thf, saf, caf);
   const int nw = a.desc_size / 4;               // 32-test words: 4 / 8 / 16
@@ -378,7 +375,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orient_desc(DescArgs a) {
   // sin are formed only then), so every test word is the double form's, bit for bit.
   // Round 6: the double sincos (~150 VALU per wave) left the common path, the pattern bytes
   // convert to float with SDWA operands, both points' x and y rotate as packed pairs, the LDS
-  // addresses come out of one packed fma and the near-half test is branch-free: 36 -> 23 VALU
+  // addresses come out of one packed fma and the near-half test is branch-free: 36 -> ~25 VALU
   // per round; the double form's constants no longer occupy registers inside the loop.
   // (Measured slower in round 4/5: software-pipelining several pairs per wave, 0.71 -> 0.94-1.13
   // ms per step; OCML sincosf in place of the double sincos, 0.72 -> 0.77 ms.)
