@@ -739,9 +739,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--multiframes", type=int, default=171, help="multi-frames per rank per step")
     ap.add_argument("--split", type=int, default=2,
-                    help="2: extract the step's two halves on two streams, matching the first "
-                         "half beside the second's extraction (3: the second half starts after "
-                         "the first)")
+                    help="K: extract the step's multi-frames as K parts on K streams, each "
+                         "part's pairs matched beside the other parts' extraction (1: one launch "
+                         "chain over the whole batch)")
     ap.add_argument("--unique", type=int, default=12, help="distinct rendered multi-frames")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--cpu-sample", type=int, default=12, help="multi-frames timed on the CPU")
@@ -810,19 +810,22 @@ def main():
 
     ev_m0 = torch.cuda.Event(enable_timing=True)
     ev_m1 = torch.cuda.Event(enable_timing=True)
-    # --split 2: the batch as two halves of multi-frames, each with its own extractor (its own
-    # workspace) on its own stream; the first half's pairs are matched as soon as it is
-    # extracted (MFMA work beside the second half's VALU-bound extraction), the second half's
-    # pairs (the boundary pair included) after both.  Same kernels, same outputs.
-    split = args.split > 1 and M >= 4
+    # --split K (default 2): the batch as K parts of consecutive multi-frames, each with its own
+    # extractor (its own workspace) on its own stream; a part's pairs are matched as soon as it
+    # is extracted (MFMA work beside the other parts' VALU-bound extraction), the pairs across a
+    # part boundary once both sides are.  Same kernels, same outputs.
+    K = max(1, min(args.split, M // 2))
+    split = K > 1
     if split:
-        MA = M // 2
-        FA, FB = MA * NC, F - MA * NC
-        NPA = (MA - 1) * NC
-        ex2 = mcs_amd.Extractor(params, W, H, max_frames=FB, device=local_rank)
-        ex2.set_masks_device(d_mask.data_ptr(), NC, stream.cuda_stream)
-        s2 = torch.cuda.Stream(device=dev)
-        ev_a, ev_b, ev_go = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
+        mb = [M * k // K for k in range(K + 1)]            # part k = multi-frames [mb[k], mb[k+1])
+        exs = [ex] + [mcs_amd.Extractor(params, W, H, max_frames=(mb[k + 1] - mb[k]) * NC, device=local_rank)
+                      for k in range(1, K)]
+        for e in exs[1:]:
+            e.set_masks_device(d_mask.data_ptr(), NC, stream.cuda_stream)
+        sts = [stream] + [torch.cuda.Stream(device=dev) for _ in range(1, K)]
+        ev_go = torch.cuda.Event()
+        ev_done = [torch.cuda.Event() for _ in range(K)]
+        ev_end = [torch.cuda.Event() for _ in range(K)]
 
     def match(p0, n, st):
         rc = L.mcs_hamming_top2_batch_device(d_desc.data_ptr(), d_cnt.data_ptr(),
@@ -831,25 +834,29 @@ def main():
         if rc != 0:
             raise RuntimeError("matcher failed %d" % rc)
 
+    def extract_part(k, st):
+        f0, nf = mb[k] * NC, (mb[k + 1] - mb[k]) * NC
+        exs[k].extract_batch_device(d_img.data_ptr() + f0 * W * H, nf, d_midx.data_ptr() + 4 * f0,
+                                    d_kps.data_ptr() + 4 * f0 * cap * 7, d_cnt.data_ptr() + 4 * f0,
+                                    d_desc.data_ptr() + f0 * cap * 32, st.cuda_stream)
+
     def step(timed, allow_split=True):
         if split and allow_split:
             ev_go.record(stream)
-            s2.wait_event(ev_go)
-            ex.extract_batch_device(d_img.data_ptr(), FA, d_midx.data_ptr(), d_kps.data_ptr(),
-                                    d_cnt.data_ptr(), d_desc.data_ptr(), stream.cuda_stream)
-            ev_a.record(stream)
-            if args.split == 3:   # staggered: B's extraction starts once A's is done
-                s2.wait_event(ev_a)
-            ex2.extract_batch_device(d_img.data_ptr() + FA * W * H, FB, d_midx.data_ptr() + 4 * FA,
-                                     d_kps.data_ptr() + 4 * FA * cap * 7, d_cnt.data_ptr() + 4 * FA,
-                                     d_desc.data_ptr() + FA * cap * 32, s2.cuda_stream)
+            for k in range(1, K):
+                sts[k].wait_event(ev_go)
+            for k in range(K):
+                extract_part(k, sts[k])
+                ev_done[k].record(sts[k])
             if timed:
                 ev_m0.record(stream)
-            match(0, NPA, stream.cuda_stream)
-            s2.wait_event(ev_a)
-            match(NPA, NP - NPA, s2.cuda_stream)
-            ev_b.record(s2)
-            stream.wait_event(ev_b)
+            match(0, (mb[1] - 1) * NC, stream.cuda_stream)      # part 0's own pairs
+            for k in range(1, K):   # the boundary pair (mb[k] - 1, mb[k]) and part k's own pairs
+                sts[k].wait_event(ev_done[k - 1])
+                p0 = (mb[k] - 1) * NC
+                match(p0, (mb[k + 1] - 1) * NC - p0, sts[k].cuda_stream)
+                ev_end[k].record(sts[k])
+                stream.wait_event(ev_end[k])
             if timed:
                 ev_m1.record(stream)
             return
@@ -996,8 +1003,8 @@ def main():
                        "keypoints_per_step_per_gpu": kp_per_step,
                        "match_pairs_per_step_per_gpu": NP,
                        "parallelism": "dp%d (independent multi-frame segments)" % world,
-                       "schedule": ("two halves of the step's multi-frames on two streams "
-                                    "(two extractors), each half's pairs matched after it"
+                       "schedule": ("%d parts of the step's multi-frames on %d streams "
+                                    "(%d extractors), each part's pairs matched after it" % (K, K, K)
                                     if split else "one stream")},
             "roofline": roofline,
             "roofline_orient_desc": roofline_od,
