@@ -1,4 +1,4 @@
-// Pixel arithmetic shared by the pyramid kernels (k_pyramid.hip, k_pyr_small.hip): the
+// Pixel arithmetic of the pyramid kernels (k_pyramid.hip): the
 // BORDER_REFLECT_101 index, the INTER_LINEAR vertical pass in both OpenCV 3.1 forms and the
 // rounding of the normalised 5x5 box filter.
 #pragma once
