@@ -134,6 +134,7 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
   fa.cell_counts = h->d_cell_counts;
   fa.threshold = std::min(std::max(pl.p.fast_threshold, 0), 255);
   fa.pattern = pl.p.fast_agast_type == 2 ? 16 : pl.p.fast_agast_type == 1 ? 12 : 8;
+  fa.frame_count = d_counts;
   fa.nframes = F;
   fill_level_ptrs(pl, fa.lp);
   const bool wide = pl.scale_factor > 1.5;
@@ -169,9 +170,8 @@ static int run_batch(mcs_extractor* h, const uint8_t* d_images, int F, const uin
     fl.units = per_mask ? h->d_munits : h->d_units;
     fl.nunits = per_mask ? (int)h->munit_stride : (int)pl.fast_units.size();
     fl.unit_mstride = per_mask ? h->munit_stride : 0;
-    launch_fast_rows(fl, st);
+    launch_fast_rows(fl, st);   // also zeroes d_counts
   }
-  MCS_HIP_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * F, st));
   stage_mark(h, 3, st);
   // K3: octree
   {

@@ -87,6 +87,7 @@ struct FastRowArgs {
   int threshold;
   uint32_t kk, rbits;     // byte-wise compare constants (v_lerp_u8), see launch_fast_rows
   int pattern;            // FAST circle: 16 (TYPE_9_16), 12 (TYPE_7_12) or 8 (TYPE_5_8)
+  int32_t* frame_count;   // per-frame keypoint counts the octree adds into: zeroed here (unit 0)
   int nframes;
   LevelPtrs lp;
 };

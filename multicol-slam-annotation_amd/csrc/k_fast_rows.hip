@@ -133,6 +133,11 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   if (!xcd_frame_map(blockIdx.x, a.nframes, (a.nunits + 3) / 4, &f, &item)) return;
   const int ui = item * 4 + wv;
   if (ui >= a.nunits) return;
+  // the octree (next launch) adds the frame's keypoint count into frame_count[f]: unit 0 zeroes
+  // it on its way out instead of a memset launch between the two.  Only on the way out: a store
+  // before the kernel's uniform loads would make them vector loads (the compiler may no longer
+  // prove them unclobbered), which cost 0.1 ms per step
+  auto zero_count = [&] { if (ui == 0 && lane == 0) a.frame_count[f] = 0; };
   const int mi = a.mask_index ? min(max(a.mask_index[f], 0), a.nmasks - 1) : 0;
   const FastUnit u = a.units[(int64_t)mi * a.unit_mstride + ui];
 #ifdef MCS_FAST_PROBE
@@ -143,6 +148,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
   int32_t* const cnt_out = a.cell_counts + (int64_t)f * a.ncells + u.cell0;
   if (wh <= 0) {
     if (lane < nc) cnt_out[lane] = 0;
+    zero_count();
     return;
   }
   // mask rows of the run (the level of the frame's mask pyramid, pitch bpitch: aligned dwords)
@@ -282,6 +288,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     // appended after the carried corners in raster order
     int ns = 0;
     const uint64_t lt = dev::lanemask_lt();
+    uint32_t sv[kBand];
 #pragma unroll
     for (int i = 0; i < kBand; i++) {
       const int y = y0 + i;
@@ -294,17 +301,34 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
       auto dk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(c1, ~q, a.rbits), a.kk, 0u); };
       auto bk = [&](uint32_t q) { return __builtin_amdgcn_lerp(__builtin_amdgcn_lerp(q, nv, a.rbits), a.kk, 0u); };
       // 12 / 8 point circles: no pre-test, every detection pixel goes to the exact test
-      const uint32_t s = (y >= y1) ? 0u
-                         : PAT != 16 ? detm
-                                     : ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
-                                         ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm);
-      // compaction: the lane's exclusive prefix of the survivor counts c (0..4) by a DPP scan
-      // (dev::wave_incl_scan; round 5 took three ballots of c's bits and six mbcnt); the four
-      // entries are written unconditionally, those of non-survivors to a dummy slot
-      const int c = __builtin_popcount(s);
-      const int inc = dev::wave_incl_scan(c);
-      const int pos0 = ncarry + ns + inc - c;
-      ns += __builtin_amdgcn_readlane(inc, 63);
+      sv[i] = (y >= y1) ? 0u
+              : PAT != 16 ? detm
+                          : ((((dk(dn) | dk(up)) & (dk(rt) | dk(lf))) |
+                              ((bk(dn) | bk(up)) & (bk(rt) | bk(lf)))) & detm);
+    }
+    // compaction: the lane's exclusive prefix of its survivor counts (0..4 per row) by DPP
+    // scans, three rows per scan in 10-bit fields (a row's wave total is <= 62 x 4 = 248, so
+    // no field carries into the next; one scan per row measured 0.652 against 0.638 ms per
+    // step); the four entries per row are written unconditionally, those of non-survivors to a
+    // dummy slot
+    constexpr int kNP = (kBand + 2) / 3;
+    uint32_t pc[kNP], px[kNP], ptot[kNP];
+#pragma unroll
+    for (int q = 0; q < kNP; q++) pc[q] = 0u;
+#pragma unroll
+    for (int i = 0; i < kBand; i++) pc[i / 3] |= (uint32_t)__builtin_popcount(sv[i]) << (10 * (i % 3));
+#pragma unroll
+    for (int q = 0; q < kNP; q++) {
+      const uint32_t inc = (uint32_t)dev::wave_incl_scan((int)pc[q]);
+      px[q] = inc - pc[q];                               // exclusive, field by field (no borrows)
+      ptot[q] = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    }
+#pragma unroll
+    for (int i = 0; i < kBand; i++) {
+      const int y = y0 + i;
+      const uint32_t s = sv[i];
+      const int pos0 = ncarry + ns + (int)((px[i / 3] >> (10 * (i % 3))) & 0x3FFu);
+      ns += (int)((ptot[i / 3] >> (10 * (i % 3))) & 0x3FFu);
       const int k0 = (s >> 7) & 1, k1 = (s >> 15) & 1, k2 = (s >> 23) & 1, k3 = s >> 31;
       const int pos1 = pos0 + k0, pos2 = pos1 + k1, pos3 = pos2 + k2;
       const int idx = (y << 8) | (4 * lane);
@@ -468,6 +492,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(FastRowArgs a) {
     FP_ADD(3, t4_ - t3_);
   }
   if (lane < nc) cnt_out[lane] = cnt;
+  zero_count();
 #ifdef MCS_FAST_PROBE
   acc_[4] += (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin_);
   if (lane == 0)
