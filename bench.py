@@ -742,6 +742,9 @@ def main():
                     help="K: extract the step's multi-frames as K parts on K streams, each "
                          "part's pairs matched beside the other parts' extraction (1: one launch "
                          "chain over the whole batch)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: consecutive steps overlap (step s+1's extraction beside step s's "
+                         "matching on a match stream; the outputs are double-buffered)")
     ap.add_argument("--unique", type=int, default=12, help="distinct rendered multi-frames")
     ap.add_argument("--nfeatures", type=int, default=2000)
     ap.add_argument("--cpu-sample", type=int, default=12, help="multi-frames timed on the CPU")
@@ -807,6 +810,10 @@ def main():
     d_pairs = torch.from_numpy(pairs).to(dev)
     NP = len(pairs)
     d_m = [torch.zeros((NP, cap), dtype=torch.int32, device=dev) for _ in range(4)]
+    # --pipeline: a second output set, so that step s+1 extracts while step s's pairs are matched
+    bufs = [(d_kps, d_cnt, d_desc)]
+    if args.pipeline:
+        bufs.append((torch.zeros_like(d_kps), torch.zeros_like(d_cnt), torch.zeros_like(d_desc)))
 
     ev_m0 = torch.cuda.Event(enable_timing=True)
     ev_m1 = torch.cuda.Event(enable_timing=True)
@@ -827,20 +834,54 @@ def main():
         ev_done = [torch.cuda.Event() for _ in range(K)]
         ev_end = [torch.cuda.Event() for _ in range(K)]
 
-    def match(p0, n, st):
-        rc = L.mcs_hamming_top2_batch_device(d_desc.data_ptr(), d_cnt.data_ptr(),
+    def match(p0, n, st, b=0):
+        _, cnt_b, desc_b = bufs[b]
+        rc = L.mcs_hamming_top2_batch_device(desc_b.data_ptr(), cnt_b.data_ptr(),
                                              d_pairs.data_ptr() + 8 * p0, n, cap, 32,
                                              *[t.data_ptr() + 4 * p0 * cap for t in d_m], st)
         if rc != 0:
             raise RuntimeError("matcher failed %d" % rc)
 
-    def extract_part(k, st):
+    def extract_part(k, st, b=0):
+        kps_b, cnt_b, desc_b = bufs[b]
         f0, nf = mb[k] * NC, (mb[k + 1] - mb[k]) * NC
         exs[k].extract_batch_device(d_img.data_ptr() + f0 * W * H, nf, d_midx.data_ptr() + 4 * f0,
-                                    d_kps.data_ptr() + 4 * f0 * cap * 7, d_cnt.data_ptr() + 4 * f0,
-                                    d_desc.data_ptr() + f0 * cap * 32, st.cuda_stream)
+                                    kps_b.data_ptr() + 4 * f0 * cap * 7, cnt_b.data_ptr() + 4 * f0,
+                                    desc_b.data_ptr() + f0 * cap * 32, st.cuda_stream)
+
+    # --pipeline: the parts' extraction streams run from step to step without waiting for the
+    # matching, which follows on its own stream; output set s % 2 is reused by step s + 2 only
+    # after step s's matching (ev_free)
+    if args.pipeline:
+        if not split:
+            mb, exs, sts, K = [0, M], [ex], [stream], 1
+        mst = torch.cuda.Stream(device=dev)
+        ev_x = [[torch.cuda.Event() for _ in range(K)] for _ in range(2)]
+        ev_free = [torch.cuda.Event() for _ in range(2)]
+        free_rec = [False, False]
+        pstep = [0]
+
+    def step_pipelined():
+        b = pstep[0] % 2
+        pstep[0] += 1
+        for k in range(K):
+            if free_rec[b]:
+                sts[k].wait_event(ev_free[b])
+            extract_part(k, sts[k], b)
+            ev_x[b][k].record(sts[k])
+        mst.wait_event(ev_x[b][0])
+        match(0, (mb[1] - 1) * NC, mst.cuda_stream, b)
+        for k in range(1, K):
+            mst.wait_event(ev_x[b][k])
+            p0 = (mb[k] - 1) * NC
+            match(p0, (mb[k + 1] - 1) * NC - p0, mst.cuda_stream, b)
+        ev_free[b].record(mst)
+        free_rec[b] = True
+        return b
 
     def step(timed, allow_split=True):
+        if args.pipeline and allow_split:
+            return step_pipelined()
         if split and allow_split:
             ev_go.record(stream)
             for k in range(1, K):
@@ -884,7 +925,7 @@ def main():
     # matcher device time (events on the launch stream around the match launch alone): in split
     # mode the timed step's events also wrap the wait on the second half's extraction, so the
     # figure comes from the one-stream stage-timing steps below instead
-    match_ms_last = None if split else ev_m0.elapsed_time(ev_m1)
+    match_ms_last = None if (split or args.pipeline) else ev_m0.elapsed_time(ev_m1)
     # per-stage kernel times for the roofline: a few extra, untimed steps with the stage
     # events on (which run the stages back to back on one stream)
     stages, ncalls = {}, 0
@@ -1005,7 +1046,10 @@ def main():
                        "parallelism": "dp%d (independent multi-frame segments)" % world,
                        "schedule": ("%d parts of the step's multi-frames on %d streams "
                                     "(%d extractors), each part's pairs matched after it" % (K, K, K)
-                                    if split else "one stream")},
+                                    if split else "one stream") +
+                                   ("; steps pipelined: step s+1 extracts while step s's pairs are "
+                                    "matched on a match stream (double-buffered keypoints and "
+                                    "descriptors)" if args.pipeline else "")},
             "roofline": roofline,
             "roofline_orient_desc": roofline_od,
             "roofline_octree": roofline_oct,

@@ -10,7 +10,7 @@ TAG=${1:-r02}
 O=gpurun_out/fp_$TAG; mkdir -p $O
 # --split 1: every launch covers the whole 513-frame batch on one stream (the bench's stage-timed
 # roofline launches), so per-launch durations, bytes and VALU counts are per step
-ARGS="--steps 5 --warmup 1 --split 1 --no-cpu-baseline --ba-calls 0 --gba-calls 0 --d-multiframes 0 --bow-reps 0 --latency-reps 0 --tri-reps 0"
+ARGS="--steps 5 --warmup 1 --split 1 --pipeline 0 --no-cpu-baseline --ba-calls 0 --gba-calls 0 --d-multiframes 0 --bow-reps 0 --latency-reps 0 --tri-reps 0"
 # kernel-trace pass: one timed step, then the bench's stage-timed steps (stages back to back, the
 # level-0 blur not beside the resize chain), so the per-kernel averages are those launches'
 SARGS=$(echo "$ARGS" | sed "s/--steps 5 --warmup 1/--steps 1 --warmup 0/")
