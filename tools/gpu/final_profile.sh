@@ -16,6 +16,9 @@ ARGS="--steps 5 --warmup 1 --split 1 --pipeline 0 --no-cpu-baseline --ba-calls 0
 SARGS=$(echo "$ARGS" | sed "s/--steps 5 --warmup 1/--steps 1 --warmup 0/")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py $SARGS > $O/bench_stats.json 2> $O/stats.err || { echo "stats pass failed"; tail -5 $O/stats.err; exit 1; }
 S=$(find $O/stats -name '*kernel_stats.csv' | head -1); cp "$S" $O/kernel_stats.csv
+T=$(find $O/stats -name '*kernel_trace.csv' | head -1); cp "$T" $O/kernel_trace.csv
+ALG=$(python3 -c "import json; print(json.load(open('$O/bench_stats.json'))['roofline']['alg_bytes_per_call'])")
+python3 tools/stage_trace_summary.py $O/kernel_trace.csv 2 8 $ALG "final_profile.sh $TAG stats pass: the 2 stage-timed extractor calls (stages back to back on one stream)" > $O/stage_kernel_trace.json || { echo "stage trace summary failed"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py $ARGS > /dev/null 2> $O/fetch.err || { echo "fetch pass failed"; tail -5 $O/fetch.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py $ARGS > /dev/null 2> $O/write.err || { echo "write pass failed"; tail -5 $O/write.err; exit 1; }
 F=$(find $O/fetch -name '*counter_collection.csv' | head -1)
