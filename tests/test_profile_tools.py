@@ -73,3 +73,29 @@ def test_valu_per_pixel(tmp_path):
     assert d["k_fast_rows<16>"]["calls"] == 2.0
     assert abs(d["k_fast_rows<16>"]["valu_lane_ops_per_pixel"]
                - round(5000 * 64 / (sum(px) * 2.5), 2)) < 1e-9
+
+
+def test_stage_trace_summary(tmp_path):
+    """tools/stage_trace_summary.py: the last CALLS extractor calls of a kernel trace, the
+    median per level (one stretched dispatch does not move it) and the roofline fraction."""
+    path = str(tmp_path / "trace.csv")
+    lv = [170, 140, 90, 77, 68, 61, 35]                      # us per level launch
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        t, n = 1000, 0
+        for call in range(4):                                # call 0 is a timed step: dropped
+            for l, us in enumerate(lv):
+                d = us * 1000 * (3 if (call == 0 or (call == 2 and l == 1)) else 1)
+                w.writerow([n, PYR, t, t + d]); t += d + 500; n += 1
+            w.writerow([n, FAST, t, t + 650000]); t += 650500; n += 1
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "stage_trace_summary.py"), path,
+                        "3", "8", "1523973204", "synthetic"], check=True, capture_output=True,
+                       text=True, timeout=60)
+    d = json.loads(r.stdout)
+    assert d["k_pyr_rows_per_level_us"] == [float(v) for v in lv]
+    assert d["k_pyr_rows_per_level_us_mean"][1] == round((140 * 3 + 140 * 2) / 3, 1)
+    assert abs(d["k_pyr_rows<true,2>_ms_per_call"] - sum(lv) / 1e3) < 1e-9
+    assert abs(d["k_fast_rows<16>_ms_per_call"] - 0.65) < 1e-9
+    frac = 1523973204 / ((sum(lv) / 1e3 + 0.65) / 1e3) / 1e9 / 8000.0
+    assert abs(d["frac_of_8000"] - round(frac, 4)) < 1e-12

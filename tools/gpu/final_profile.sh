@@ -11,14 +11,15 @@ O=gpurun_out/fp_$TAG; mkdir -p $O
 # --split 1: every launch covers the whole 513-frame batch on one stream (the bench's stage-timed
 # roofline launches), so per-launch durations, bytes and VALU counts are per step
 ARGS="--steps 5 --warmup 1 --split 1 --pipeline 0 --no-cpu-baseline --ba-calls 0 --gba-calls 0 --d-multiframes 0 --bow-reps 0 --latency-reps 0 --tri-reps 0"
-# kernel-trace pass: one timed step, then the bench's stage-timed steps (stages back to back, the
-# level-0 blur not beside the resize chain), so the per-kernel averages are those launches'
-SARGS=$(echo "$ARGS" | sed "s/--steps 5 --warmup 1/--steps 1 --warmup 0/")
+# kernel-trace pass: 2 warmup + 5 timed steps (the clocks settle: a pass of one step measured
+# every kernel 7-13 % slower), then the bench's 5 stage-timed steps (stages back to back, the
+# level-0 blur not beside the resize chain), which stage_trace_summary.py picks out
+SARGS=$(echo "$ARGS" | sed "s/--warmup 1/--warmup 2/")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py $SARGS > $O/bench_stats.json 2> $O/stats.err || { echo "stats pass failed"; tail -5 $O/stats.err; exit 1; }
 S=$(find $O/stats -name '*kernel_stats.csv' | head -1); cp "$S" $O/kernel_stats.csv
 T=$(find $O/stats -name '*kernel_trace.csv' | head -1); cp "$T" $O/kernel_trace.csv
 ALG=$(python3 -c "import json; print(json.load(open('$O/bench_stats.json'))['roofline']['alg_bytes_per_call'])")
-python3 tools/stage_trace_summary.py $O/kernel_trace.csv 2 8 $ALG "final_profile.sh $TAG stats pass: the 2 stage-timed extractor calls (stages back to back on one stream)" > $O/stage_kernel_trace.json || { echo "stage trace summary failed"; exit 1; }
+python3 tools/stage_trace_summary.py $O/kernel_trace.csv 5 8 $ALG "final_profile.sh $TAG stats pass: the 5 stage-timed extractor calls (stages back to back on one stream)" > $O/stage_kernel_trace.json || { echo "stage trace summary failed"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 bench.py $ARGS > /dev/null 2> $O/fetch.err || { echo "fetch pass failed"; tail -5 $O/fetch.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 bench.py $ARGS > /dev/null 2> $O/write.err || { echo "write pass failed"; tail -5 $O/write.err; exit 1; }
 F=$(find $O/fetch -name '*counter_collection.csv' | head -1)
