@@ -53,7 +53,14 @@ inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
 #ifndef MCS_PYR_WAVES_PER_FRAME
 #define MCS_PYR_WAVES_PER_FRAME 32
 #endif
-  const long target = std::max<long>(MCS_PYR_TARGET, (long)MCS_PYR_WAVES_PER_FRAME * (F > 0 ? F : 1));
+#ifndef MCS_PYR_SMALL_WPF
+#define MCS_PYR_SMALL_WPF MCS_PYR_WAVES_PER_FRAME
+#endif
+#ifndef MCS_PYR_SMALL_ROWS
+#define MCS_PYR_SMALL_ROWS 200
+#endif
+  const long wpf = dh < MCS_PYR_SMALL_ROWS ? MCS_PYR_SMALL_WPF : MCS_PYR_WAVES_PER_FRAME;
+  const long target = std::max<long>(MCS_PYR_TARGET, wpf * (F > 0 ? F : 1));
   const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
   const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
   int rows = (dh + segs - 1) / segs;
