@@ -53,14 +53,9 @@ inline void pyr_strips(int dw, int dh, int F, PyrArgs& a) {
 #ifndef MCS_PYR_WAVES_PER_FRAME
 #define MCS_PYR_WAVES_PER_FRAME 32
 #endif
-#ifndef MCS_PYR_SMALL_WPF
-#define MCS_PYR_SMALL_WPF MCS_PYR_WAVES_PER_FRAME
-#endif
-#ifndef MCS_PYR_SMALL_ROWS
-#define MCS_PYR_SMALL_ROWS 200
-#endif
-  const long wpf = dh < MCS_PYR_SMALL_ROWS ? MCS_PYR_SMALL_WPF : MCS_PYR_WAVES_PER_FRAME;
-  const long target = std::max<long>(MCS_PYR_TARGET, wpf * (F > 0 ? F : 1));
+  // (more waves per frame for the levels under 200 rows only, 48 or 64 with segments down to
+  // 6 / 4 rows, and segments down to 4 rows alone measured flat or slower at the end of round 6)
+  const long target = std::max<long>(MCS_PYR_TARGET, (long)MCS_PYR_WAVES_PER_FRAME * (F > 0 ? F : 1));
   const long per_seg = (long)a.tiles_x * (F > 0 ? F : 1);
   const int segs = (int)std::max<long>(1, (target + per_seg - 1) / per_seg);
   int rows = (dh + segs - 1) / segs;
