@@ -253,7 +253,7 @@ def cpu_baseline(imgs, masks, ncams, nfeatures, n_multiframes):
     return nkp / dt / 1e3, sample, ncams, (kpss, descs, top2), stages
 
 
-def check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, ncams):
+def check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, ncams, of_step="last timed step"):
     """Untimed post-run parity check of the timed batch: the camera-frames and match pairs the
     CPU baseline leg computed (the first multi-frames of the batch) against the GPU's outputs of
     the LAST timed step, bit-exact: keypoint fields, descriptors, (best idx, best dist, second
@@ -284,7 +284,7 @@ def check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, ncams):
                 raise RuntimeError("bench parity: match pair %d differs from the oracle" % p)
     return {"camera_frames_bitexact": len(frames), "match_pairs_bitexact": npairs,
             "keypoints_checked": int(sum(len(k) for row in kpss for k in row)),
-            "of_step": "last timed step"}
+            "of_step": of_step}
 
 
 def single_multiframe_latency(ex, d_img, d_midx, d_kps, d_cnt, d_desc, ncams, stream, reps):
@@ -916,8 +916,9 @@ def main():
         dist.barrier()
     # timed region: the production path, no stage events between the kernels
     t0 = time.perf_counter()
+    last_b = 0
     for _ in range(args.steps):
-        step(True)
+        last_b = step(True) or 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1022,7 +1023,11 @@ def main():
                        "(no -march, no SIMD intrinsics, -ffp-contract=off), not the reference's "
                        "OpenCV SSE/AVX build"}
         cpu.update(host_cpu_info())
-        parity = check_against_cpu_baseline(ref, d_kps, d_cnt, d_desc, d_m, NC)
+        # the stage-timed steps (one stream, output set 0) ran last when stage timing is on;
+        # otherwise the last timed step's output set
+        chk = bufs[0] if args.stage_timing else bufs[last_b]
+        parity = check_against_cpu_baseline(ref, chk[0], chk[1], chk[2], d_m, NC,
+                                            "last stage-timed step" if args.stage_timing else "last timed step")
 
     if rank == 0:
         out = {
