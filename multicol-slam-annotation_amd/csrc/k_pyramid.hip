@@ -29,9 +29,11 @@ namespace mcs {
 // wave-uniform and kept scalar (readfirstlane of the wave index and of table reads).
 constexpr int kStageDW = 192;    // staged source row (dwords), scale <= 2.2
 #ifndef MCS_PYR_KPF
-#define MCS_PYR_KPF 4
+#define MCS_PYR_KPF 6
 #endif
-constexpr int kPF = MCS_PYR_KPF;  // source rows in flight per wave
+// source rows in flight per wave: 6 (end of round 6: pyramid 0.632-0.633 -> 0.622-0.626 ms per
+// step over three A/B runs; 2 and 8 measured 0.671 and 0.80 ms)
+constexpr int kPF = MCS_PYR_KPF;
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
